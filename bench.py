@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric on config C2: batched 4K RGB -> 1080p Lanczos3
+resize (batch 256 uchar per GPU) through libmipx.so, device-resident input.
+
+    python bench.py --gpus N --steps K --warmup W
+
+One process per GPU (torchrun for N > 1, RANK/LOCAL_RANK/WORLD_SIZE from the
+env); requests are independent, so every rank runs its own batch with no
+collective on the data path ("scaling": "weak").  torch is plumbing only:
+device memory, the stream, and a gloo barrier / max-reduce for the timing.
+
+A step = one mipx_execute_dev() of the bimg plan for /resize?width=1920&height=1080
+on a 3840x2160x3 decoded image (one Lanczos3 reduce 2x2, the fused k_reduce2x2
+kernel) over the whole resident batch.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (import before libmipx: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+W_IN, H_IN, BANDS = 3840, 2160, 3
+W_OUT, H_OUT = 1920, 1080
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU (BASELINE C2: 256)")
+    ap.add_argument("--cpu-images", type=int, default=96, help="CPU baseline sample size (images)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, sample):
+    """Oracle (C restatement of libvips reduce, -O2, OpenMP across images, each
+    image single-threaded as libvips concurrency 1) on a bounded sample."""
+    from oracle import oracle as o
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    imgs = [sample[i % len(sample)] for i in range(args.cpu_images)]
+    o.reduce_batch(imgs[:threads], 2.0, 2.0, threads)  # warm
+    t0 = time.perf_counter()
+    o.reduce_batch(imgs, 2.0, 2.0, threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(len(imgs) / dt, 2), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"{len(imgs)} x 3840x2160x3 uniform-random images, oracle/vips_ref.c ref_reduce "
+                      f"(reducev+reduceh Lanczos3 2x2), {threads} OpenMP threads, {dt:.2f} s wall"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    import imaginary_amd as ia
+    from imaginary_amd._abi import check, lib
+    import ctypes as C
+    check(lib.mipx_set_device(local), "mipx_set_device")
+
+    n = args.batch
+    plan = ia.plan_make(ia.make_opts(width=W_OUT, height=H_OUT, embed=1), ia.make_input(W_IN, H_IN, BANDS, "png"))
+    assert plan.describe() == [("reduce", (0,) * 8, (2.0, 2.0, 0.0, 0.0), (W_OUT, H_OUT, BANDS))], plan.describe()
+    in_img = W_IN * H_IN * BANDS
+    out_img = W_OUT * H_OUT * BANDS
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device=dev)
+    g.manual_seed(20241220 + rank)
+    d_in = torch.randint(0, 256, (n, in_img), dtype=torch.uint8, device=dev, generator=g)
+    d_out = torch.empty((n, out_img), dtype=torch.uint8, device=dev)
+    wsb = lib.mipx_workspace_bytes(C.byref(plan), n)
+    d_ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+
+    def step():
+        check(lib.mipx_execute_dev(C.byref(plan), n, d_in.data_ptr(), d_out.data_ptr(), None,
+                                   d_ws.data_ptr(), wsb, sp), "mipx_execute_dev")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel launch per step, on `stream`
+    t = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+
+    verify = None
+    if not args.no_verify and rank == 0:
+        from oracle import oracle as o
+        idx = [0, n - 1]
+        got = d_out[idx].cpu().numpy().reshape(len(idx), H_OUT, W_OUT, BANDS)
+        src = d_in[idx].cpu().numpy().reshape(len(idx), H_IN, W_IN, BANDS)
+        verify = all(np.array_equal(got[i], o.reduce(src[i], 2.0, 2.0)) for i in range(len(idx)))
+        if not verify:
+            raise SystemExit("bench: GPU output differs from the oracle")
+        cpu_sample = list(src)
+    if rank == 0:
+        images = n * world * args.steps
+        value = images / wall_max
+        alg_bytes = n * (in_img + out_img)
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        line = {
+            "metric": "images/sec (4K RGB->1080p Lanczos3 batch) + achieved HBM GB/s, 1/2/4/8 GPUs",
+            "value": round(value, 1),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic uniform-random uchar, device-resident (seed 20241220+rank)",
+            "config": {"workload": "C2: batched 3840x2160x3 -> 1920x1080x3 Lanczos3 reduce (bimg "
+                                   "/resize?width=1920&height=1080), fused k_reduce2x2",
+                       "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world} (independent shards)"},
+            "achieved_hbm_gbs": round(achieved, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
+            "verified_vs_oracle": verify,
+        }
+        if not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(args, cpu_sample if verify is not None else
+                                                [np.random.default_rng(1).integers(0, 256, (H_IN, W_IN, BANDS),
+                                                                                   dtype=np.uint8)])
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,65 @@
+// mipx_internal.h — shared declarations between the planner, the runtime and
+// the gfx950 kernels of libmipx.so.  Not part of the ABI (see include/mipx.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "mipx.h"
+
+namespace mipx {
+
+// ---- errors -------------------------------------------------------------
+void set_error(const char *fmt, ...);
+int hip_fail(hipError_t e, const char *what);  // records detail, returns MIPX_EDEVICE
+#define MIPX_HIP(call)                                                    \
+    do {                                                                  \
+        hipError_t e_ = (call);                                           \
+        if (e_ != hipSuccess) return ::mipx::hip_fail(e_, #call);         \
+    } while (0)
+
+// ---- libvips resample constants (resample/templates.h, [U]) ----------------
+constexpr int kTransformScale = 128;  // VIPS_TRANSFORM_SCALE: 129 sub-pixel phases
+constexpr int kInterpShift = 12;      // VIPS_INTERPOLATE_SHIFT
+constexpr int kInterpScale = 1 << kInterpShift;
+
+// Lanczos3 reduce geometry (libvips reduceh.cpp / reducev.cpp).
+int reduce_points(double shrink);                      // 2 * rint(3 * shrink) + 1
+void reduce_table(double shrink, std::vector<int> &t); // 129 x n truncated 12-bit taps
+int out_size_reduce(int in, double shrink);            // VIPS_ROUND(in / shrink)
+int out_size_shrink(int in, int shrink);               // VIPS_ROUND(in / shrink)
+
+// Integer gaussmat (libvips create/gaussmat.c): returns width, fills mask/scale.
+int gaussmat(double sigma, double min_ampl, std::vector<int> &mask, int &scale);
+
+// Colour LUTs for the smartcrop scorer (libvips colour/*.c, [U]).
+constexpr int kQuantElements = 100000;
+const float *v2y8_table();    // 256 entries: sRGB 8-bit -> linear
+const float *cbrt_table();    // kQuantElements entries: Lab f(t)
+
+// vips_resize() downsize schedule used by the smartcrop scorer.
+struct ResizeSchedule {
+    int shrink_h = 1, shrink_v = 1;    // integer box shrink
+    double reduce_h = 1.0, reduce_v = 1.0;  // residual Lanczos3 (1.0 = none)
+    int w1 = 0, h1 = 0;                // after shrink
+    int w2 = 0, h2 = 0;                // after reduce
+};
+int resize_schedule(int w, int h, double hscale, double vscale, ResizeSchedule &s);
+
+// ---- device-side cached tables ----------------------------------------------
+// float copy of reduce_table(shrink) resident on the current device.
+const float *device_reduce_table(double shrink, int *n_taps);
+const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt]
+void free_device_tables();
+
+// ---- kernels (mipx_kernels.hip) ------------------------------------------------
+size_t op_workspace_bytes(int op, int n, int w, int h, int bands, double p0, double p1);
+int smartcrop_extract(const uint8_t *in, uint8_t *out, int n, int w, int h, int bands,
+                      int cw, int ch, void *ws, size_t ws_bytes, hipStream_t st);
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace mipx

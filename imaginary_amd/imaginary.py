@@ -1,0 +1,399 @@
+"""Host-side mirror of imaginary's operation layer over the MI355X engine.
+
+Reference: image.go (OperationsMap 15-32, Process 81-113, Resize 115, Fit 139,
+calculateDestinationFitDimension 190, Enlarge 202, Extract 213, Crop 226,
+SmartCrop 236, Rotate 247, Flip 267, Flop 273, Thumbnail 279, Zoom 286,
+WatermarkImage 343, GaussianBlur 372, Pipeline 379), options.go (ImageOptions
+11-52, BimgOptions 128-172) and params.go (buildParamsFromQuery 354-366,
+parseInt 376-390, parseExtendMode 421-437, parseGravity 439-453).
+
+Same operation names, argument meaning and error behaviour; the one change is
+the seam: Process() hands DECODED pixels to libmipx (mipx_plan_make +
+mipx_process) instead of calling bimg.Resize on encoded bytes.  Codec decode /
+encode stay with the host (here: a `Decoded` value carrying the pixels plus
+the header facts bimg would read: type, EXIF orientation).  Operations the
+engine does not implement raise EngineUnsupported — the Go shim falls back to
+bimg.Resize there.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+import numpy as np
+
+from . import _abi
+from .engine import Engine, fit_dimension, make_input, make_opts, plan_make
+
+HTTP_BAD_REQUEST = 400
+HTTP_NOT_ACCEPTABLE = 406
+
+
+class ImaginaryError(Exception):
+    """error.go NewError: message + HTTP status."""
+
+    def __init__(self, message: str, code: int = HTTP_BAD_REQUEST):
+        super().__init__(message)
+        self.message = message
+        self.code = code
+
+
+class EngineUnsupported(ImaginaryError):
+    """The plan needs an op libmipx lacks (MIPX_EUNSUPPORTED): caller falls back to bimg."""
+
+    def __init__(self, message: str):
+        super().__init__(message, 501)
+
+
+@dataclass
+class IsDefinedField:
+    flip: bool = False
+    flop: bool = False
+    force: bool = False
+    embed: bool = False
+    no_crop: bool = False
+    no_rotation: bool = False
+
+
+@dataclass
+class ImageOptions:
+    """options.go:11-52 (pixel-relevant subset)."""
+    width: int = 0
+    height: int = 0
+    area_width: int = 0
+    area_height: int = 0
+    rotate: int = 0
+    top: int = 0
+    left: int = 0
+    factor: int = 0
+    flip: bool = False
+    flop: bool = False
+    force: bool = False
+    embed: bool = False
+    no_crop: bool = False
+    no_rotation: bool = False
+    opacity: float = 0.0
+    sigma: float = 0.0
+    min_ampl: float = 0.0
+    image: str = ""
+    type: str = ""
+    aspect_ratio: str = ""
+    background: List[int] = field(default_factory=list)
+    extend: int = 1          # bimg.ExtendCopy default (params.go:342, 356)
+    gravity: int = 0
+    operations: List[Dict[str, Any]] = field(default_factory=list)
+    is_defined: IsDefinedField = field(default_factory=IsDefinedField)
+
+
+@dataclass
+class Decoded:
+    """What the host codec hands over: pixels (h, w, bands) + header facts."""
+    pixels: np.ndarray
+    type: str = "png"
+    orientation: int = 0
+    # full-resolution header size when `pixels` were decoded with shrink-on-load
+    header_w: int = 0
+    header_h: int = 0
+
+    @property
+    def w(self):
+        return self.header_w or self.pixels.shape[1]
+
+    @property
+    def h(self):
+        return self.header_h or self.pixels.shape[0]
+
+
+# ---- params.go helpers -----------------------------------------------------------
+def parse_int(v: str) -> int:
+    """params.go:376-390: round half up of |float|."""
+    if v == "":
+        return 0
+    return int(math.floor(abs(float(v)) + 0.5))
+
+
+def parse_float(v: str) -> float:
+    return abs(float(v)) if v != "" else 0.0
+
+
+def parse_bool(v: str) -> bool:
+    if v == "":
+        return False
+    s = v.strip().lower()
+    if s in ("1", "t", "true"):
+        return True
+    if s in ("0", "f", "false"):
+        return False
+    raise ValueError(v)
+
+
+def parse_extend_mode(v: str) -> int:
+    """params.go:421-437 (default mirror)."""
+    m = {"white": 4, "black": 0, "copy": 1, "background": 5, "lastpixel": 6}
+    return m.get(v.strip().lower(), 3)
+
+
+def parse_gravity(v: str) -> int:
+    """params.go:439-453."""
+    m = {"south": 3, "north": 1, "east": 2, "west": 4, "smart": 5}
+    return m.get(v.strip().lower(), 0)
+
+
+def parse_color(v: str) -> List[int]:
+    return [min(int(x.strip() or 0), 255) for x in v.split(",")] if v else []
+
+
+def build_params_from_query(query: Dict[str, Any]) -> ImageOptions:
+    """params.go:354-366 for the pixel-relevant parameters (Extend defaults to copy)."""
+    o = ImageOptions()
+    ints = {"width": "width", "height": "height", "areawidth": "area_width", "areaheight": "area_height",
+            "rotate": "rotate", "top": "top", "left": "left", "factor": "factor"}
+    for k, v in query.items():
+        v = v if isinstance(v, str) else str(v) if not isinstance(v, (list, dict, bool)) else v
+        if k in ints:
+            setattr(o, ints[k], parse_int(v) if isinstance(v, str) else int(v))
+        elif k in ("sigma", "minampl", "opacity"):
+            setattr(o, {"sigma": "sigma", "minampl": "min_ampl", "opacity": "opacity"}[k],
+                    parse_float(v) if isinstance(v, str) else float(v))
+        elif k in ("flip", "flop", "force", "embed", "nocrop", "norotation"):
+            attr = {"nocrop": "no_crop", "norotation": "no_rotation"}.get(k, k)
+            setattr(o, attr, parse_bool(v) if isinstance(v, str) else bool(v))
+            setattr(o.is_defined, attr, True)
+        elif k == "extend":
+            o.extend = parse_extend_mode(v)
+        elif k == "gravity":
+            o.gravity = parse_gravity(v)
+        elif k == "background":
+            o.background = parse_color(v) if isinstance(v, str) else list(v)
+        elif k == "type":
+            o.type = v
+        elif k == "aspectratio":
+            o.aspect_ratio = v
+        elif k == "image":
+            o.image = v
+        elif k == "operations":
+            o.operations = v
+    return o
+
+
+# ---- options.go BimgOptions ----------------------------------------------------------
+def _aspect(o: ImageOptions, w: int, h: int):
+    if (w != 0 and h != 0) or (w == 0 and h == 0) or not o.aspect_ratio:
+        return w, h
+    parts = o.aspect_ratio.strip().lower().split(":")
+    if len(parts) < 2:
+        return w, h
+    ar = {"width": int(parts[0] or 0), "height": int(parts[1] or 0)}
+    if w != 0:
+        h = int(w / ar["width"]) * ar["height"]   # Go integer arithmetic
+    else:
+        w = int(h / ar["height"]) * ar["width"]
+    return w, h
+
+
+def bimg_options(o: ImageOptions) -> Dict[str, Any]:
+    """options.go:128-172 -> the mipx_opts field dict."""
+    b = dict(width=o.width, height=o.height, flip=int(o.flip), flop=int(o.flop),
+             no_auto_rotate=int(o.no_rotation), force=int(o.force), gravity=o.gravity,
+             embed=int(o.embed), extend=o.extend, rotate=o.rotate)
+    if o.background:
+        b["background"] = (list(o.background) + [0, 0, 0])[:3]
+    b["width"], b["height"] = _aspect(o, o.width, o.height)
+    if o.sigma > 0 or o.min_ampl > 0:
+        b["sigma"], b["min_ampl"] = o.sigma, o.min_ampl
+    return b
+
+
+# ---- Process (image.go:81) ------------------------------------------------------------
+_ENGINE: Optional[Engine] = None
+
+
+def engine() -> Engine:
+    global _ENGINE
+    if _ENGINE is None:
+        _ENGINE = Engine()
+    return _ENGINE
+
+
+Decoder = Callable[[Decoded, int], np.ndarray]
+
+
+def process(img: Decoded, opts: Dict[str, Any], wm: Optional[np.ndarray] = None,
+            redecode: Optional[Decoder] = None) -> np.ndarray:
+    """image.go:81-113 with bimg.Resize's pixel work on the GPU.
+
+    `redecode(img, s)` is the host codec's shrink-on-load (libjpeg scale 1/s);
+    without one, a plan that asks for load_shrink > 1 is rejected."""
+    px = img.pixels if img.pixels.ndim == 3 else img.pixels[:, :, None]
+    inp = make_input(img.w, img.h, px.shape[2], img.type, img.orientation)
+    if wm is not None:
+        wm = wm if wm.ndim == 3 else wm[:, :, None]
+        opts = dict(opts, wm_enable=1)
+        inp.wm_w, inp.wm_h, inp.wm_bands = wm.shape[1], wm.shape[0], wm.shape[2]
+    try:
+        plan = plan_make(make_opts(**opts), inp)
+        if plan.load_shrink > 1:
+            if redecode is None:
+                raise ImaginaryError("shrink-on-load requested but no host decoder given", 500)
+            px = redecode(img, plan.load_shrink)
+            inp.decoded_w, inp.decoded_h = px.shape[1], px.shape[0]
+            plan = plan_make(make_opts(**opts), inp)
+        elif img.header_w and (img.header_w, img.header_h) != (px.shape[1], px.shape[0]):
+            raise ImaginaryError("decoded size does not match the header", 500)
+        return engine().process(plan, px, wm)
+    except _abi.MipxError as e:
+        if e.code == _abi.MIPX_EUNSUPPORTED:
+            raise EngineUnsupported(str(e)) from e
+        raise ImaginaryError(f"image processing error: {e}", 500) from e
+
+
+# ---- image.go operations ----------------------------------------------------------------
+def Resize(img: Decoded, o: ImageOptions, **kw):
+    if o.width == 0 and o.height == 0:
+        raise ImaginaryError("Missing required param: height or width")
+    opts = bimg_options(o)
+    opts["embed"] = 1
+    if o.is_defined.no_crop:
+        opts["crop"] = int(not o.no_crop)
+    return process(img, opts, **kw)
+
+
+def calculate_destination_fit_dimension(iw, ih, fw, fh):
+    return fit_dimension(iw, ih, fw, fh)
+
+
+def Fit(img: Decoded, o: ImageOptions, **kw):
+    if o.width == 0 or o.height == 0:
+        raise ImaginaryError("Missing required params: height, width")
+    w, h = img.w, img.h
+    if w == 0 or h == 0:
+        raise ImaginaryError("Width or height of requested image is zero", HTTP_NOT_ACCEPTABLE)
+    o = dataclasses.replace(o)
+    if o.no_rotation or img.orientation <= 4:
+        o.width, o.height = calculate_destination_fit_dimension(w, h, o.width, o.height)
+    else:  # width/height switched by auto rotation
+        o.height, o.width = calculate_destination_fit_dimension(h, w, o.height, o.width)
+    opts = bimg_options(o)
+    opts["embed"] = 1
+    return process(img, opts, **kw)
+
+
+def Enlarge(img: Decoded, o: ImageOptions, **kw):
+    if o.width == 0 or o.height == 0:
+        raise ImaginaryError("Missing required params: height, width")
+    opts = bimg_options(o)
+    opts["enlarge"] = 1
+    opts["crop"] = int(not o.no_crop)
+    return process(img, opts, **kw)
+
+
+def Extract(img: Decoded, o: ImageOptions, **kw):
+    if o.area_width == 0 or o.area_height == 0:
+        raise ImaginaryError("Missing required params: areawidth or areaheight")
+    opts = bimg_options(o)
+    opts.update(top=o.top, left=o.left, area_width=o.area_width, area_height=o.area_height)
+    return process(img, opts, **kw)
+
+
+def Crop(img: Decoded, o: ImageOptions, **kw):
+    if o.width == 0 and o.height == 0:
+        raise ImaginaryError("Missing required param: height or width")
+    opts = bimg_options(o)
+    opts["crop"] = 1
+    return process(img, opts, **kw)
+
+
+def SmartCrop(img: Decoded, o: ImageOptions, **kw):
+    if o.width == 0 and o.height == 0:
+        raise ImaginaryError("Missing required param: height or width")
+    opts = bimg_options(o)
+    opts["crop"] = 1
+    opts["gravity"] = 5
+    return process(img, opts, **kw)
+
+
+def Rotate(img: Decoded, o: ImageOptions, **kw):
+    if o.rotate == 0:
+        raise ImaginaryError("Missing required param: rotate")
+    return process(img, bimg_options(o), **kw)
+
+
+def Flip(img: Decoded, o: ImageOptions, **kw):
+    opts = bimg_options(o)
+    opts["flip"] = 1
+    return process(img, opts, **kw)
+
+
+def Flop(img: Decoded, o: ImageOptions, **kw):
+    opts = bimg_options(o)
+    opts["flop"] = 1
+    return process(img, opts, **kw)
+
+
+def Thumbnail(img: Decoded, o: ImageOptions, **kw):
+    if o.width == 0 and o.height == 0:
+        raise ImaginaryError("Missing required params: width or height")
+    return process(img, bimg_options(o), **kw)
+
+
+def Zoom(img: Decoded, o: ImageOptions, **kw):
+    if o.factor == 0:
+        raise ImaginaryError("Missing required param: factor")
+    opts = bimg_options(o)
+    if o.top > 0 or o.left > 0:
+        if o.area_width == 0 and o.area_height == 0:
+            raise ImaginaryError("Missing required params: areawidth, areaheight")
+        opts.update(top=o.top, left=o.left, area_width=o.area_width, area_height=o.area_height)
+        if o.is_defined.no_crop:
+            opts["crop"] = int(not o.no_crop)
+    opts["zoom"] = o.factor
+    return process(img, opts, **kw)
+
+
+def GaussianBlur(img: Decoded, o: ImageOptions, **kw):
+    if o.sigma == 0 and o.min_ampl == 0:
+        raise ImaginaryError("Missing required param: sigma or minampl")
+    return process(img, bimg_options(o), **kw)
+
+
+def WatermarkImage(img: Decoded, o: ImageOptions, wm: Optional[np.ndarray] = None, **kw):
+    """image.go:343-370; the watermark bytes are fetched (and decoded) by the host."""
+    if o.image == "" and wm is None:
+        raise ImaginaryError("Missing required param: image")
+    if wm is None or wm.size == 0:
+        raise ImaginaryError("Unable to read watermark image")
+    opts = bimg_options(o)
+    opts.update(wm_left=o.left, wm_top=o.top, wm_opacity=float(o.opacity))
+    return process(img, opts, wm=wm, **kw)
+
+
+OperationsMap: Dict[str, Callable] = {
+    "crop": Crop, "resize": Resize, "enlarge": Enlarge, "extract": Extract, "rotate": Rotate,
+    "flip": Flip, "flop": Flop, "thumbnail": Thumbnail, "zoom": Zoom,
+    "watermarkImage": WatermarkImage, "blur": GaussianBlur, "smartcrop": SmartCrop, "fit": Fit,
+}
+
+
+def Pipeline(img: Decoded, o: ImageOptions, **kw):
+    """image.go:379-410 with lossless (PNG) intermediates kept as pixels."""
+    if len(o.operations) == 0:
+        raise ImaginaryError("Missing pipeline operations")
+    if len(o.operations) > 10:
+        raise ImaginaryError("Maximum pipeline operations (10) exceeded")
+    cur = img
+    for i, op in enumerate(o.operations):
+        name = op.get("operation")
+        fn = OperationsMap.get(name)
+        if fn is None:
+            raise ImaginaryError(f"Unsupported operation: {name}")
+        opts = build_params_from_query(op.get("params", {}))
+        try:
+            out = fn(cur, opts, **kw)
+        except ImaginaryError:
+            if not op.get("ignore_failure"):
+                raise
+            continue
+        cur = Decoded(out, type="png", orientation=0)
+    return cur.pixels

@@ -1,0 +1,960 @@
+/*
+ * vips_ref.c — CPU ORACLE.  TEST INFRASTRUCTURE ONLY: loaded by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker; the
+ * product (imaginary_amd/libmipx.so) never links or calls it.
+ *
+ * Plain-C restatement of the libvips 8.12.2 pixel operations and the bimg
+ * v1.1.9 geometry planner that imaginary's Process() reaches through
+ * bimg.Resize (reference image.go:81-113, :96).  Upstream sources are not in
+ * /root/reference (go.mod:6 pins bimg v1.1.9, Dockerfile:5 pins libvips
+ * 8.12.2, neither vendored), so each function names the upstream file it
+ * restates and every result-changing detail is a switch (ref_set_switch,
+ * PARITY_ASSUMPTIONS.md).
+ *
+ * PARITY STATUS: planner pinned by the reference's dimension tests; pixel
+ * values "parity unpinned" (no libvips binary, no pixel test in the reference).
+ */
+#include "vips_ref.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------- */
+/* parity switches                                                           */
+/* ------------------------------------------------------------------------- */
+static struct {
+    const char *name;
+    int value;
+} g_switch[] = {
+    {"reduce_centre", 0},        /* 1: centre sampling convention in reduceh/v */
+    {"reduce_hfirst", 0},        /* 1: reduceh before reducev */
+    {"reduce_round_coeff", 0},   /* 1: rint() instead of truncation for 12-bit taps */
+    {"shrink_floor", 0},         /* 1: shrink output = floor(in/n) instead of round */
+    {"shrink_hfirst", 0},        /* 1: shrinkh before shrinkv */
+    {"blur_vfirst", 0},          /* 1: vertical conv pass before horizontal */
+    {"blur_honor_minampl", 0},   /* 1: bimg passes min_ampl (no NULL-terminator bug) */
+    {"cast_round", 0},           /* 1: float->uchar cast rounds instead of truncating */
+    {NULL, 0}};
+
+void ref_set_switch(const char *name, int value) {
+    for (int i = 0; g_switch[i].name; i++)
+        if (!strcmp(g_switch[i].name, name)) g_switch[i].value = value;
+}
+int ref_get_switch(const char *name) {
+    for (int i = 0; g_switch[i].name; i++)
+        if (!strcmp(g_switch[i].name, name)) return g_switch[i].value;
+    return -1;
+}
+#define SW(n) ref_get_switch(n)
+
+void ref_free(void *p) { free(p); }
+
+static int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* VIPS_ROUND: round half away from zero (libvips vips.h). */
+static int vips_round(double v) { return (int)(v < 0.0 ? ceil(v - 0.5) : floor(v + 0.5)); }
+
+static int img_alloc(ref_img *o, int w, int h, int bands) {
+    if (w <= 0 || h <= 0 || bands <= 0) return REF_EINVAL;
+    o->w = w;
+    o->h = h;
+    o->bands = bands;
+    o->data = (uint8_t *)malloc((size_t)w * h * bands);
+    return o->data ? REF_OK : REF_ENOMEM;
+}
+static int img_copy(const ref_img *in, ref_img *out) {
+    int e = img_alloc(out, in->w, in->h, in->bands);
+    if (e) return e;
+    memcpy(out->data, in->data, (size_t)in->w * in->h * in->bands);
+    return REF_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Lanczos3 reduce (libvips resample/reduce.c, reduceh.cpp, reducev.cpp,     */
+/* templates.h)                                                              */
+/* ------------------------------------------------------------------------- */
+#define TRANSFORM_SCALE 128   /* VIPS_TRANSFORM_SCALE: 1/128 sub-pixel phases */
+#define INTERP_SHIFT 12       /* VIPS_INTERPOLATE_SHIFT */
+#define INTERP_SCALE (1 << INTERP_SHIFT)
+
+/* vips_reduce_get_points(LANCZOS3): 2 * rint(3 * shrink) + 1 */
+int ref_reduce_points(double shrink) { return (int)(2 * rint(3.0 * shrink) + 1); }
+
+static double lanczos3(double x) {
+    if (x == 0.0) return 1.0;
+    if (x < -3.0 || x > 3.0) return 0.0;
+    double pix = M_PI * x;
+    return 3.0 * sin(pix) * sin(pix / 3.0) / (pix * pix);
+}
+
+/* vips_reduce_make_mask(): tap i sits at (i - (n-2)/2 - x) / shrink, the mask
+ * is normalised to sum 1. */
+static void reduce_mask(double *c, int n, double shrink, double x) {
+    double sum = 0.0;
+    for (int i = 0; i < n; i++) {
+        double xp = (i - (n - 2) / 2 - x) / shrink;
+        c[i] = lanczos3(xp);
+        sum += c[i];
+    }
+    for (int i = 0; i < n; i++) c[i] /= sum;
+}
+
+/* matrixi[x][i] = matrixf[x][i] * VIPS_INTERPOLATE_SCALE (implicit double->int
+ * conversion = truncation toward zero), for the 129 phases x = 0..128. */
+int ref_reduce_table(double shrink, int *table, int max_points) {
+    int n = ref_reduce_points(shrink);
+    if (n > max_points) return REF_EINVAL;
+    double *f = (double *)malloc(sizeof(double) * n);
+    for (int x = 0; x <= TRANSFORM_SCALE; x++) {
+        reduce_mask(f, n, shrink, (float)x / TRANSFORM_SCALE);
+        for (int i = 0; i < n; i++) {
+            double v = f[i] * INTERP_SCALE;
+            table[x * n + i] = SW("reduce_round_coeff") ? (int)rint(v) : (int)v;
+        }
+    }
+    free(f);
+    return n;
+}
+
+int ref_out_size_reduce(int in, double shrink) { return vips_round(in / shrink); }
+
+/* Sample position of output index o: corner convention X = o * shrink. */
+static double reduce_pos(int o, double shrink) {
+    return SW("reduce_centre") ? (o + 0.5) * shrink - 0.5 : o * shrink;
+}
+/* phase: sx = X * 128 * 2; tx = ((sx & 255) + 1) >> 1  (reduceh.cpp gen loop) */
+static int reduce_phase(double X) {
+    int sx = (int)(X * TRANSFORM_SCALE * 2);
+    int six = sx & (TRANSFORM_SCALE * 2 - 1);
+    return (six + 1) >> 1;
+}
+/* uchar: (sum + 2048) >> 12, clipped (unsigned_fixed_round + VIPS_CLIP). */
+static uint8_t fixed_round_u8(int sum) {
+    int v = (sum + (INTERP_SCALE >> 1)) >> INTERP_SHIFT;
+    return (uint8_t)clampi(v, 0, 255);
+}
+
+int ref_reducev(const ref_img *in, ref_img *out, double vshrink) {
+    if (vshrink < 1.0) return REF_EINVAL;
+    if (vshrink == 1.0) return img_copy(in, out);
+    int n = ref_reduce_points(vshrink);
+    int *tab = (int *)malloc(sizeof(int) * n * (TRANSFORM_SCALE + 1));
+    ref_reduce_table(vshrink, tab, n);
+    int oh = ref_out_size_reduce(in->h, vshrink);
+    int e = img_alloc(out, in->w, oh, in->bands);
+    if (e) { free(tab); return e; }
+    /* embed(0, n/2 - 1, ..., EXTEND_COPY): padded row p = original p - pad */
+    int pad = n / 2 - 1;
+    size_t ne = (size_t)in->w * in->bands;
+    int *rows = (int *)malloc(sizeof(int) * n);
+    for (int y = 0; y < oh; y++) {
+        double Y = reduce_pos(y, vshrink);
+        int iy = (int)Y;
+        const int *c = tab + reduce_phase(Y) * n;
+        for (int i = 0; i < n; i++) rows[i] = clampi(iy + i - pad, 0, in->h - 1);
+        uint8_t *q = out->data + (size_t)y * ne;
+        for (size_t j = 0; j < ne; j++) {
+            int sum = 0;
+            for (int i = 0; i < n; i++) sum += c[i] * in->data[(size_t)rows[i] * ne + j];
+            q[j] = fixed_round_u8(sum);
+        }
+    }
+    free(rows);
+    free(tab);
+    return REF_OK;
+}
+
+int ref_reduceh(const ref_img *in, ref_img *out, double hshrink) {
+    if (hshrink < 1.0) return REF_EINVAL;
+    if (hshrink == 1.0) return img_copy(in, out);
+    int n = ref_reduce_points(hshrink);
+    int *tab = (int *)malloc(sizeof(int) * n * (TRANSFORM_SCALE + 1));
+    ref_reduce_table(hshrink, tab, n);
+    int ow = ref_out_size_reduce(in->w, hshrink);
+    int e = img_alloc(out, ow, in->h, in->bands);
+    if (e) { free(tab); return e; }
+    int pad = n / 2 - 1, b = in->bands;
+    int *cols = (int *)malloc(sizeof(int) * n);
+    for (int x = 0; x < ow; x++) {
+        double X = reduce_pos(x, hshrink);
+        int ix = (int)X;
+        const int *c = tab + reduce_phase(X) * n;
+        for (int i = 0; i < n; i++) cols[i] = clampi(ix + i - pad, 0, in->w - 1);
+        for (int y = 0; y < in->h; y++) {
+            const uint8_t *p = in->data + (size_t)y * in->w * b;
+            uint8_t *q = out->data + ((size_t)y * ow + x) * b;
+            for (int z = 0; z < b; z++) {
+                int sum = 0;
+                for (int i = 0; i < n; i++) sum += c[i] * p[cols[i] * b + z];
+                q[z] = fixed_round_u8(sum);
+            }
+        }
+    }
+    free(cols);
+    free(tab);
+    return REF_OK;
+}
+
+/* vips_reduce(): reducev then reduceh, uchar intermediate (reduce.c build). */
+int ref_reduce(const ref_img *in, ref_img *out, double hshrink, double vshrink) {
+    ref_img t = {0};
+    int e;
+    if (SW("reduce_hfirst")) {
+        if ((e = ref_reduceh(in, &t, hshrink))) return e;
+        e = ref_reducev(&t, out, vshrink);
+    } else {
+        if ((e = ref_reducev(in, &t, vshrink))) return e;
+        e = ref_reduceh(&t, out, hshrink);
+    }
+    free(t.data);
+    return e;
+}
+
+/* ------------------------------------------------------------------------- */
+/* box shrink (libvips resample/shrink.c, shrinkh.c, shrinkv.c)              */
+/* ------------------------------------------------------------------------- */
+int ref_out_size_shrink(int in, int shrink) {
+    if (SW("shrink_floor")) return in / shrink;
+    return vips_round((double)in / shrink);
+}
+
+/* Partial blocks at the far edge read the EXTEND_COPY border (clamp). */
+int ref_shrinkv(const ref_img *in, ref_img *out, int n) {
+    if (n < 1) return REF_EINVAL;
+    if (n == 1) return img_copy(in, out);
+    int oh = ref_out_size_shrink(in->h, n);
+    if (oh < 1) oh = 1;
+    int e = img_alloc(out, in->w, oh, in->bands);
+    if (e) return e;
+    size_t ne = (size_t)in->w * in->bands;
+    for (int y = 0; y < oh; y++)
+        for (size_t j = 0; j < ne; j++) {
+            int sum = 0;
+            for (int k = 0; k < n; k++)
+                sum += in->data[(size_t)clampi(y * n + k, 0, in->h - 1) * ne + j];
+            out->data[(size_t)y * ne + j] = (uint8_t)((sum + n / 2) / n);
+        }
+    return REF_OK;
+}
+
+int ref_shrinkh(const ref_img *in, ref_img *out, int n) {
+    if (n < 1) return REF_EINVAL;
+    if (n == 1) return img_copy(in, out);
+    int ow = ref_out_size_shrink(in->w, n);
+    if (ow < 1) ow = 1;
+    int e = img_alloc(out, ow, in->h, in->bands);
+    if (e) return e;
+    int b = in->bands;
+    for (int y = 0; y < in->h; y++)
+        for (int x = 0; x < ow; x++)
+            for (int z = 0; z < b; z++) {
+                int sum = 0;
+                for (int k = 0; k < n; k++)
+                    sum += in->data[((size_t)y * in->w + clampi(x * n + k, 0, in->w - 1)) * b + z];
+                out->data[((size_t)y * ow + x) * b + z] = (uint8_t)((sum + n / 2) / n);
+            }
+    return REF_OK;
+}
+
+int ref_shrink(const ref_img *in, ref_img *out, int hshrink, int vshrink) {
+    ref_img t = {0};
+    int e;
+    if (SW("shrink_hfirst")) {
+        if ((e = ref_shrinkh(in, &t, hshrink))) return e;
+        e = ref_shrinkv(&t, out, vshrink);
+    } else {
+        if ((e = ref_shrinkv(in, &t, vshrink))) return e;
+        e = ref_shrinkh(&t, out, hshrink);
+    }
+    free(t.data);
+    return e;
+}
+
+/* ------------------------------------------------------------------------- */
+/* conversion (libvips conversion/embed.c, extract.c, rot.c, flip.c)         */
+/* ------------------------------------------------------------------------- */
+/* Positive modulo. */
+static int pmod(int a, int m) {
+    int r = a % m;
+    return r < 0 ? r + m : r;
+}
+
+/* vips_embed(): the input placed at (x, y) on a w x h canvas.  COPY clamps,
+ * REPEAT tiles with period W, MIRROR tiles the 2x2 [in, flip(in)] mosaic with
+ * period 2W (the extract offset nx = 2W - x % 2W gives (X - x) mod 2W). */
+int ref_embed(const ref_img *in, ref_img *out, int x, int y, int w, int h, int extend,
+              const int bg[3]) {
+    int e = img_alloc(out, w, h, in->bands);
+    if (e) return e;
+    int b = in->bands;
+    uint8_t fill[4] = {0, 0, 0, 0};
+    if (extend == REF_EXTEND_LAST) extend = REF_EXTEND_BACKGROUND; /* bimg vipsEmbed: >5 */
+    if (extend == REF_EXTEND_WHITE) memset(fill, 255, 4);
+    if (extend == REF_EXTEND_BACKGROUND) {
+        for (int z = 0; z < 4; z++) fill[z] = (uint8_t)clampi(bg[z < 3 ? z : 2], 0, 255);
+        if (b == 4) fill[3] = 255;
+        if (b <= 2) fill[0] = (uint8_t)clampi(bg[0], 0, 255), fill[1] = 255;
+    }
+    for (int Y = 0; Y < h; Y++)
+        for (int X = 0; X < w; X++) {
+            int sx = X - x, sy = Y - y;
+            uint8_t *q = out->data + ((size_t)Y * w + X) * b;
+            int inside = sx >= 0 && sx < in->w && sy >= 0 && sy < in->h;
+            if (!inside) {
+                switch (extend) {
+                case REF_EXTEND_COPY:
+                    sx = clampi(sx, 0, in->w - 1);
+                    sy = clampi(sy, 0, in->h - 1);
+                    break;
+                case REF_EXTEND_REPEAT:
+                    sx = pmod(sx, in->w);
+                    sy = pmod(sy, in->h);
+                    break;
+                case REF_EXTEND_MIRROR: {
+                    int u = pmod(sx, 2 * in->w), v = pmod(sy, 2 * in->h);
+                    sx = u < in->w ? u : 2 * in->w - 1 - u;
+                    sy = v < in->h ? v : 2 * in->h - 1 - v;
+                    break;
+                }
+                default:
+                    memcpy(q, fill, b);
+                    continue;
+                }
+            }
+            memcpy(q, in->data + ((size_t)sy * in->w + sx) * b, b);
+        }
+    return REF_OK;
+}
+
+int ref_extract(const ref_img *in, ref_img *out, int left, int top, int w, int h) {
+    if (left < 0 || top < 0 || w <= 0 || h <= 0 || left + w > in->w || top + h > in->h)
+        return REF_EINVAL; /* vips_extract_area: "bad extract area" */
+    int e = img_alloc(out, w, h, in->bands);
+    if (e) return e;
+    for (int y = 0; y < h; y++)
+        memcpy(out->data + (size_t)y * w * in->bands,
+               in->data + ((size_t)(top + y) * in->w + left) * in->bands, (size_t)w * in->bands);
+    return REF_OK;
+}
+
+/* vips_rot(): D90 is clockwise; D270 anticlockwise. */
+int ref_rot(const ref_img *in, ref_img *out, int angle) {
+    int W = in->w, H = in->h, b = in->bands, e;
+    angle = pmod(angle, 360);
+    if (angle == 0) return img_copy(in, out);
+    if (angle == 180) e = img_alloc(out, W, H, b);
+    else if (angle == 90 || angle == 270) e = img_alloc(out, H, W, b);
+    else return REF_EINVAL;
+    if (e) return e;
+    for (int y = 0; y < out->h; y++)
+        for (int x = 0; x < out->w; x++) {
+            int sx, sy;
+            if (angle == 90) { sx = y; sy = H - 1 - x; }
+            else if (angle == 180) { sx = W - 1 - x; sy = H - 1 - y; }
+            else { sx = W - 1 - y; sy = x; }
+            memcpy(out->data + ((size_t)y * out->w + x) * b, in->data + ((size_t)sy * W + sx) * b, b);
+        }
+    return REF_OK;
+}
+
+int ref_flip(const ref_img *in, ref_img *out, int vertical) {
+    int e = img_alloc(out, in->w, in->h, in->bands);
+    if (e) return e;
+    int b = in->bands;
+    for (int y = 0; y < in->h; y++)
+        for (int x = 0; x < in->w; x++) {
+            int sx = vertical ? x : in->w - 1 - x, sy = vertical ? in->h - 1 - y : y;
+            memcpy(out->data + ((size_t)y * in->w + x) * b, in->data + ((size_t)sy * in->w + sx) * b, b);
+        }
+    return REF_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* gaussian blur (libvips create/gaussmat.c, convolution/gaussblur.c,        */
+/* convsep.c, convi.c)                                                       */
+/* ------------------------------------------------------------------------- */
+/* Integer separable mask: v = rint(20 * exp(-x^2 / 2 sigma^2)), cut where the
+ * unscaled amplitude drops below min_ampl; width 2 * max(x - 1, 0) + 1;
+ * scale = sum of the mask.  Returns width. */
+int ref_gaussmat(double sigma, double min_ampl, int *mask, int max_width, int *scale) {
+    if (!(sigma > 0.0)) return REF_EINVAL;
+    double sig2 = 2.0 * sigma * sigma;
+    double mx = 8.0 * sigma;
+    int max_x = (int)(mx < 0 ? 0 : (mx > 5000 ? 5000 : mx));
+    int x;
+    for (x = 0; x < max_x; x++) {
+        double v = exp(-((double)(x * x)) / sig2);
+        if (v < min_ampl) break;
+    }
+    if (x >= 5000) return REF_EINVAL;
+    int width = 2 * (x - 1 > 0 ? x - 1 : 0) + 1;
+    if (width > max_width) return REF_EINVAL;
+    int sum = 0;
+    for (int i = 0; i < width; i++) {
+        int xo = i - width / 2;
+        double v = exp(-(double)(xo * xo) / sig2);
+        mask[i] = (int)rint(20.0 * v);
+        sum += mask[i];
+    }
+    *scale = sum == 0 ? 1 : sum;
+    return width;
+}
+
+/* convi uchar: sum = ((sum + rounding) / scale) + offset, rounding = (scale+1)/2,
+ * clipped; the input is embedded with EXTEND_COPY so out size == in size. */
+static void convi_pass(const ref_img *in, ref_img *out, const int *m, int n, int scale,
+                       int vertical) {
+    int W = in->w, H = in->h, b = in->bands, half = n / 2;
+    int rounding = (scale + 1) / 2;
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++)
+            for (int z = 0; z < b; z++) {
+                int sum = 0;
+                for (int i = 0; i < n; i++) {
+                    int sx = vertical ? x : clampi(x + i - half, 0, W - 1);
+                    int sy = vertical ? clampi(y + i - half, 0, H - 1) : y;
+                    sum += m[i] * in->data[((size_t)sy * W + sx) * b + z];
+                }
+                sum = (sum + rounding) / scale;
+                out->data[((size_t)y * W + x) * b + z] = (uint8_t)clampi(sum, 0, 255);
+            }
+}
+
+int ref_gaussblur(const ref_img *in, ref_img *out, double sigma, double min_ampl) {
+    int mask[10001], scale;
+    int n = ref_gaussmat(sigma, min_ampl, mask, 10001, &scale);
+    if (n < 0) return n;
+    ref_img t = {0};
+    int e;
+    if ((e = img_alloc(&t, in->w, in->h, in->bands))) return e;
+    if ((e = img_alloc(out, in->w, in->h, in->bands))) { free(t.data); return e; }
+    int vfirst = SW("blur_vfirst");
+    convi_pass(in, &t, mask, n, scale, vfirst);
+    convi_pass(&t, out, mask, n, scale, !vfirst);
+    free(t.data);
+    return REF_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* watermark image (bimg vips.h vips_watermark_image)                        */
+/* ------------------------------------------------------------------------- */
+/* bandjoin alpha 255 where missing; embed the watermark at (left, top) on a
+ * canvas of the base size (BLACK); mask = (uchar) (alpha * opacity);
+ * ifthenelse blend: (m * a + (255 - m) * b + 128) / 255 on every band. */
+static int has_alpha(int bands) { return bands == 2 || bands > 3; }
+
+int ref_watermark(const ref_img *base, const ref_img *wm, ref_img *out, int left, int top,
+                  float opacity) {
+    int bb = has_alpha(base->bands) ? base->bands : base->bands + 1;
+    int wb = has_alpha(wm->bands) ? wm->bands : wm->bands + 1;
+    if (bb != wb) return REF_EUNSUPPORTED;
+    int e = img_alloc(out, base->w, base->h, bb);
+    if (e) return e;
+    for (int y = 0; y < base->h; y++)
+        for (int x = 0; x < base->w; x++) {
+            uint8_t a[4], bp[4];
+            const uint8_t *p = base->data + ((size_t)y * base->w + x) * base->bands;
+            for (int z = 0; z < bb; z++) bp[z] = z < base->bands ? p[z] : 255;
+            int wx = x - left, wy = y - top;
+            int m = 0;
+            if (wx >= 0 && wx < wm->w && wy >= 0 && wy < wm->h) {
+                const uint8_t *s = wm->data + ((size_t)wy * wm->w + wx) * wm->bands;
+                for (int z = 0; z < wb; z++) a[z] = z < wm->bands ? s[z] : 255;
+                float f = (float)a[wb - 1] * opacity + 0.0f;
+                if (SW("cast_round")) f = rintf(f);
+                m = f < 0 ? 0 : (f > 255 ? 255 : (int)f);
+            } else {
+                memset(a, 0, 4);
+            }
+            uint8_t *q = out->data + ((size_t)y * base->w + x) * bb;
+            for (int z = 0; z < bb; z++) q[z] = (uint8_t)((m * a[z] + (255 - m) * bp[z] + 128) / 255);
+        }
+    return REF_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* smartcrop attention (libvips conversion/smartcrop.c, resample/resize.c,   */
+/* colour/sRGB2scRGB.c, scRGB2XYZ.c, XYZ2Lab.c)                               */
+/* ------------------------------------------------------------------------- */
+static float g_v2Y_8[256];
+#define QUANT_ELEMENTS 100000
+static float g_cbrt_table[QUANT_ELEMENTS];
+static int g_tables_ready = 0;
+
+static void colour_tables(void) {
+    if (g_tables_ready) return;
+    for (int i = 0; i < 256; i++) {
+        float f = (float)i / 255;
+        float v;
+        if (f <= 0.04045) v = f / 12.92;
+        else v = pow((f + 0.055) / 1.055, 2.4);
+        g_v2Y_8[i] = v;
+    }
+    for (int i = 0; i < QUANT_ELEMENTS; i++) {
+        float Y = (double)i / QUANT_ELEMENTS;
+        if (Y < 0.008856) g_cbrt_table[i] = 7.787 * Y + (16.0 / 116.0);
+        else g_cbrt_table[i] = cbrt(Y);
+    }
+    g_tables_ready = 1;
+}
+
+static float lab_cbrt(float v, double white) {
+    float n = QUANT_ELEMENTS * v / white;
+    int i = clampi((int)n, 0, QUANT_ELEMENTS - 2);
+    float f = n - i;
+    return g_cbrt_table[i] + f * (g_cbrt_table[i + 1] - g_cbrt_table[i]);
+}
+
+/* vips_resize(in, hscale, "vscale", vscale) for downsizing: integer box shrink
+ * by floor(1 / (2 scale)), then Lanczos3 reducev / reduceh of the residual. */
+static int resize_int_shrink(double scale) {
+    if (scale > 1.0) return 1;
+    int s = (int)floor(1.0 / (scale * 2));
+    return s < 1 ? 1 : s;
+}
+static int ref_resize_down(const ref_img *in, ref_img *out, double hscale, double vscale) {
+    int ih = resize_int_shrink(hscale), iv = resize_int_shrink(vscale);
+    ref_img a = {0}, b = {0};
+    const ref_img *cur = in;
+    int e;
+    if (ih > 1 || iv > 1) {
+        if ((e = ref_shrink(cur, &a, ih, iv))) return e;
+        cur = &a;
+        hscale *= ih;
+        vscale *= iv;
+    }
+    if (hscale < 1.0 / cur->w) hscale = 1.0 / cur->w;
+    if (vscale < 1.0 / cur->h) vscale = 1.0 / cur->h;
+    if (hscale > 1.0 || vscale > 1.0) { free(a.data); return REF_EUNSUPPORTED; }
+    if (vscale < 1.0) {
+        if ((e = ref_reducev(cur, &b, 1.0 / vscale))) { free(a.data); return e; }
+        free(a.data);
+        a = b;
+        b.data = NULL;
+        cur = &a;
+    }
+    if (hscale < 1.0) {
+        e = ref_reduceh(cur, out, 1.0 / hscale);
+    } else {
+        e = img_copy(cur, out);
+    }
+    free(a.data);
+    return e;
+}
+
+/* float separable blur with the integer gaussmat mask (convf: double sum,
+ * / scale, COPY edges), as vips_gaussblur does for a float image. */
+static void convf_pass(const float *in, float *out, int W, int H, const int *m, int n,
+                       int scale, int vertical) {
+    int half = n / 2;
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            double sum = 0.0;
+            for (int i = 0; i < n; i++) {
+                int sx = vertical ? x : clampi(x + i - half, 0, W - 1);
+                int sy = vertical ? clampi(y + i - half, 0, H - 1) : y;
+                sum += (double)m[i] * in[(size_t)sy * W + sx];
+            }
+            out[(size_t)y * W + x] = (float)(sum / scale + 0.0);
+        }
+}
+
+int ref_smartcrop_origin(const ref_img *in, int width, int height, int *left, int *top) {
+    if (width > in->w || height > in->h || width <= 0 || height <= 0) return REF_EINVAL;
+    if (in->bands < 3) return REF_EUNSUPPORTED;
+    colour_tables();
+    double hscale = 32.0 / in->w, vscale = 32.0 / in->h;
+    double sigma = sqrt(pow(width * hscale, 2) + pow(height * vscale, 2)) / 10;
+    if (sigma < 1.0) sigma = 1.0;
+    ref_img s = {0};
+    int e = ref_resize_down(in, &s, hscale, vscale);
+    if (e) return e;
+    int W = s.w, H = s.h, N = W * H;
+    float *X = malloc(sizeof(float) * N * 3), *Yb = X + N, *Z = X + 2 * N;
+    float *score = malloc(sizeof(float) * N * 3), *tmp = score + N, *blur = score + 2 * N;
+    for (int i = 0; i < N; i++) {
+        const uint8_t *p = s.data + (size_t)i * s.bands;
+        float R = g_v2Y_8[p[0]], G = g_v2Y_8[p[1]], B = g_v2Y_8[p[2]];
+        R *= 100.0;
+        G *= 100.0;
+        B *= 100.0;
+        X[i] = 0.4124 * R + 0.3576 * G + 0.1805 * B;
+        Yb[i] = 0.2126 * R + 0.7152 * G + 0.0722 * B;
+        Z[i] = 0.0193 * R + 0.1192 * G + 0.9505 * B;
+    }
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            int i = y * W + x;
+            /* edge: 3x3 Laplacian on Y (convf, double sum, row-major nonzeros) x5, abs */
+            double acc = 0.0;
+            acc += -1.0 * Yb[clampi(y - 1, 0, H - 1) * W + x];
+            acc += -1.0 * Yb[y * W + clampi(x - 1, 0, W - 1)];
+            acc += 4.0 * Yb[i];
+            acc += -1.0 * Yb[y * W + clampi(x + 1, 0, W - 1)];
+            acc += -1.0 * Yb[clampi(y + 1, 0, H - 1) * W + x];
+            float edge = (float)(acc / 1.0 + 0.0);
+            edge = 5.0f * edge + 0.0f;
+            edge = fabsf(edge);
+            /* skin: distance of the normalised XYZ from (-0.78, -0.57, -0.44) shifted */
+            float sq = X[i] * X[i];
+            sq = sq + Yb[i] * Yb[i];
+            sq = sq + Z[i] * Z[i];
+            float mag = (float)pow((double)sq, 0.5);
+            float nx = mag == 0.0f ? 0.0f : X[i] / mag;
+            float ny = mag == 0.0f ? 0.0f : Yb[i] / mag;
+            float nz = mag == 0.0f ? 0.0f : Z[i] / mag;
+            float dx = 1.0f * nx + (float)-0.78, dy = 1.0f * ny + (float)-0.57,
+                  dz = 1.0f * nz + (float)-0.44;
+            float d2 = dx * dx;
+            d2 = d2 + dy * dy;
+            d2 = d2 + dz * dz;
+            float dist = (float)pow((double)d2, 0.5);
+            float skin = -100.0f * dist + 100.0f;
+            int bright = Yb[i] > 5.0;
+            if (!bright) skin = 0.0f;
+            /* saturation: LAB a band where Y > 5 */
+            float cbx = lab_cbrt(X[i], 95.047), cby = lab_cbrt(Yb[i], 100.0);
+            float sat = (float)(500.0 * (cbx - cby));
+            if (!bright) sat = 0.0f;
+            float sum = edge + skin;
+            sum = sum + sat;
+            score[i] = sum;
+        }
+    int mask[1001], mscale;
+    int n = ref_gaussmat(sigma, 0.2, mask, 1001, &mscale);
+    if (n < 0) { free(X); free(score); free(s.data); return n; }
+    convf_pass(score, tmp, W, H, mask, n, mscale, 0);
+    convf_pass(tmp, blur, W, H, mask, n, mscale, 1);
+    int best = 0;
+    for (int i = 1; i < N; i++)
+        if (blur[i] > blur[best]) best = i;
+    int xp = best % W, yp = best / W;
+    double l = xp / hscale - width / 2, t = yp / vscale - height / 2;
+    double lmax = in->w - width, tmax = in->h - height;
+    l = l > lmax ? lmax : l;
+    t = t > tmax ? tmax : t;
+    *left = (int)(l < 0 ? 0 : l);
+    *top = (int)(t < 0 ? 0 : t);
+    free(X);
+    free(score);
+    free(s.data);
+    return REF_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* planner — bimg v1.1.9 resizer.go restated                                 */
+/* ------------------------------------------------------------------------- */
+/* imaginary image.go:190-200 calculateDestinationFitDimension */
+int ref_fit_dimension(int iw, int ih, int fw, int fh, int *ow, int *oh) {
+    if ((long long)iw * fh > (long long)fw * ih)
+        fh = (int)round((double)fw * (double)ih / (double)iw);
+    else
+        fw = (int)round((double)fh * (double)iw / (double)ih);
+    *ow = fw;
+    *oh = fh;
+    return REF_OK;
+}
+
+static int round_float(double f) { return f < 0 ? (int)ceil(f - 0.5) : (int)floor(f + 0.5); }
+
+static int push(ref_plan *p, int op, int *w, int *h, int *b) {
+    if (p->n_steps >= REF_MAX_STEPS) return REF_EINVAL;
+    ref_step *s = &p->steps[p->n_steps++];
+    memset(s, 0, sizeof(*s));
+    s->op = op;
+    (void)w; (void)h; (void)b;
+    return REF_OK;
+}
+#define LAST(p) (&(p)->steps[(p)->n_steps - 1])
+static void set_geom(ref_plan *p, int w, int h, int b) {
+    LAST(p)->out_w = w;
+    LAST(p)->out_h = h;
+    LAST(p)->out_bands = b;
+}
+
+int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
+    ref_opts o = *oin;
+    memset(plan, 0, sizeof(*plan));
+    if (in->w <= 0 || in->h <= 0 || in->bands <= 0 || in->bands > 4) return REF_EINVAL;
+    int W = in->w, H = in->h, B = in->bands;
+    if (o.zoom > 0) return REF_EUNSUPPORTED; /* vips_zoom: §8(f) next */
+
+    /* rotateAndFlipImage — EXIF via calculateRotationAndFlip, o by value */
+    int rotate = o.rotate, flip = o.flip, flop = o.flop;
+    if (!o.no_auto_rotate && o.rotate <= 0) {
+        int r = 0, f = 0;
+        switch (in->orientation) {
+        case 6: r = 90; break;
+        case 3: r = 180; break;
+        case 8: r = 270; break;
+        case 2: f = 1; break;
+        case 7: f = 1; r = 270; break;
+        case 4: f = 1; r = 180; break;
+        case 5: f = 1; r = 90; break;
+        }
+        if (f) flip = 1;
+        if (r > 0 && rotate == 0) rotate = r;
+    }
+    int angle = 0;
+    if (rotate > 0) { /* getAngle: drop the remainder mod 90, cap at 270 */
+        angle = rotate - rotate % 90;
+        if (angle > 270) angle = 270;
+        angle %= 360; /* vips_rotate_bridge */
+    }
+
+    /* normalizeOperation (uses the caller's o.Rotate) */
+    if (!o.force && !o.crop && !o.embed && !o.enlarge && o.rotate == 0 && (o.width > 0 || o.height > 0))
+        o.force = 1;
+
+    /* shrink-on-load needs the (rotated) header size: bimg reloads the rotated
+     * buffer.  Compute on rotated header dims. */
+    int hw = (angle == 90 || angle == 270) ? H : W;
+    int hh = (angle == 90 || angle == 270) ? W : H;
+
+    /* imageCalculations */
+    double factor = 1.0;
+    double xf = (double)hw / o.width, yf = (double)hh / o.height;
+    if (o.width > 0 && o.height > 0) {
+        factor = o.crop ? fmin(xf, yf) : fmax(xf, yf);
+    } else if (o.width > 0) {
+        if (o.crop) o.height = hh;
+        else { factor = xf; o.height = round_float((double)hh / factor); }
+    } else if (o.height > 0) {
+        if (o.crop) o.width = hw;
+        else { factor = yf; o.width = round_float((double)hw / factor); }
+    } else {
+        o.width = hw;
+        o.height = hh;
+    }
+    /* calculateShrink with the default bicubic interpolator (window 4) */
+    double sh = factor >= 2 ? floor(factor * 3.0 / 4.0) : floor(factor);
+    int shrink = (int)(sh < 1 ? 1 : sh);
+    double residual = (double)shrink / factor;
+    if (!o.enlarge && !o.force) {
+        if (hw < o.width && hh < o.height) {
+            factor = 1.0;
+            shrink = 1;
+            residual = 0;
+            o.width = hw;
+            o.height = hh;
+        }
+    }
+    plan->load_shrink = 1;
+    if ((in->type == REF_TYPE_JPEG || in->type == REF_TYPE_WEBP) && shrink >= 2) {
+        int sol = shrink >= 8 ? 8 : (shrink >= 4 ? 4 : 2);
+        factor /= sol;
+        plan->load_shrink = sol;
+        if (factor < 1.0) factor = 1.0;
+        shrink = (int)floor(factor);
+        residual = (double)shrink / factor;
+    }
+    /* the pixel engine starts from the decoded (possibly codec-shrunk) image */
+    int dw = W, dh = H;
+    if (plan->load_shrink > 1) {
+        dw = in->decoded_w > 0 ? in->decoded_w : (W + plan->load_shrink - 1) / plan->load_shrink;
+        dh = in->decoded_h > 0 ? in->decoded_h : (H + plan->load_shrink - 1) / plan->load_shrink;
+    }
+    plan->in_w = dw;
+    plan->in_h = dh;
+    plan->in_bands = B;
+    int cw = dw, ch = dh, cb = B;
+    if (rotate > 0) {
+        if (push(plan, REF_OP_ROT, 0, 0, 0)) return REF_EINVAL;
+        LAST(plan)->a[0] = angle;
+        if (angle == 90 || angle == 270) { int t = cw; cw = ch; ch = t; }
+        set_geom(plan, cw, ch, cb);
+        if (angle == 0) plan->n_steps--; /* D0: identity */
+    }
+    if (flip) {
+        push(plan, REF_OP_FLIP, 0, 0, 0);
+        LAST(plan)->a[0] = 0;
+        set_geom(plan, cw, ch, cb);
+    }
+    if (flop) {
+        push(plan, REF_OP_FLIP, 0, 0, 0);
+        LAST(plan)->a[0] = 1;
+        set_geom(plan, cw, ch, cb);
+    }
+
+    /* shouldTransformImage (inWidth/inHeight = rotated header size) */
+    int transform = o.force || (o.width > 0 && o.width != hw) || (o.height > 0 && o.height != hh) ||
+                    o.area_width > 0 || o.area_height > 0;
+    if (transform) {
+        if (shrink > 1) { /* shrinkImage */
+            push(plan, REF_OP_SHRINK, 0, 0, 0);
+            LAST(plan)->a[0] = shrink;
+            LAST(plan)->a[1] = shrink;
+            cw = ref_out_size_shrink(cw, shrink);
+            ch = ref_out_size_shrink(ch, shrink);
+            if (cw < 1) cw = 1;
+            if (ch < 1) ch = 1;
+            set_geom(plan, cw, ch, cb);
+            double rx = (double)o.width / cw, ry = (double)o.height / ch;
+            residual = o.crop ? fmax(rx, ry) : fmin(rx, ry);
+        }
+        double rx = residual, ry = residual;
+        if (o.force) {
+            rx = (double)o.width / cw;
+            ry = (double)o.height / ch;
+        }
+        if (o.force || residual != 0) {
+            if (rx < 1 && ry < 1) {
+                push(plan, REF_OP_REDUCE, 0, 0, 0);
+                LAST(plan)->d[0] = 1.0 / rx;
+                LAST(plan)->d[1] = 1.0 / ry;
+                cw = ref_out_size_reduce(cw, 1.0 / rx);
+                ch = ref_out_size_reduce(ch, 1.0 / ry);
+                set_geom(plan, cw, ch, cb);
+            } else if (!(rx == 1.0 && ry == 1.0)) {
+                return REF_EUNSUPPORTED; /* vips_affine bicubic (enlarge): §8(f) next */
+            }
+        }
+        if (o.force) { o.crop = 0; o.embed = 0; }
+        /* extractOrEmbedImage */
+        if (o.gravity == REF_GRAVITY_SMART || o.smart_crop) {
+            if (!(cw <= o.width && ch <= o.height)) {
+                int w = cw < o.width ? cw : o.width, h = ch < o.height ? ch : o.height;
+                push(plan, REF_OP_SMARTCROP, 0, 0, 0);
+                LAST(plan)->a[0] = w;
+                LAST(plan)->a[1] = h;
+                cw = w;
+                ch = h;
+                set_geom(plan, cw, ch, cb);
+            }
+        } else if (o.crop) {
+            if (!(cw <= o.width && ch <= o.height)) {
+                int w = cw < o.width ? cw : o.width, h = ch < o.height ? ch : o.height;
+                int l = 0, t = 0;
+                switch (o.gravity) {
+                case REF_GRAVITY_NORTH: l = (cw - o.width + 1) / 2; break;
+                case REF_GRAVITY_EAST: l = cw - o.width; t = (ch - o.height + 1) / 2; break;
+                case REF_GRAVITY_SOUTH: l = (cw - o.width + 1) / 2; t = ch - o.height; break;
+                case REF_GRAVITY_WEST: t = (ch - o.height + 1) / 2; break;
+                default: l = (cw - o.width + 1) / 2; t = (ch - o.height + 1) / 2;
+                }
+                if (l < 0) l = 0;
+                if (t < 0) t = 0;
+                push(plan, REF_OP_EXTRACT, 0, 0, 0);
+                int *a = LAST(plan)->a;
+                a[0] = l; a[1] = t; a[2] = w; a[3] = h;
+                if (l + w > cw || t + h > ch) return REF_EINVAL;
+                cw = w;
+                ch = h;
+                set_geom(plan, cw, ch, cb);
+            }
+        } else if (o.embed) {
+            int l = (o.width - cw) / 2, t = (o.height - ch) / 2;
+            if (!(l == 0 && t == 0 && o.width == cw && o.height == ch)) {
+                push(plan, REF_OP_EMBED, 0, 0, 0);
+                int *a = LAST(plan)->a;
+                a[0] = l; a[1] = t; a[2] = o.width; a[3] = o.height;
+                a[4] = o.extend > 5 ? REF_EXTEND_BACKGROUND : o.extend;
+                a[5] = o.background[0]; a[6] = o.background[1]; a[7] = o.background[2];
+                cw = o.width;
+                ch = o.height;
+                set_geom(plan, cw, ch, cb);
+            }
+        } else if (o.top != 0 || o.left != 0 || o.area_width != 0 || o.area_height != 0) {
+            int aw = o.area_width ? o.area_width : o.width;
+            int ah = o.area_height ? o.area_height : o.height;
+            if (aw == 0 || ah == 0) return REF_EINVAL;
+            if (o.left < 0 || o.top < 0 || o.left + aw > cw || o.top + ah > ch) return REF_EINVAL;
+            push(plan, REF_OP_EXTRACT, 0, 0, 0);
+            int *a = LAST(plan)->a;
+            a[0] = o.left; a[1] = o.top; a[2] = aw; a[3] = ah;
+            cw = aw;
+            ch = ah;
+            set_geom(plan, cw, ch, cb);
+        }
+    }
+    /* applyEffects: GaussianBlur when sigma or min_ampl > 0 */
+    if (o.sigma > 0 || o.min_ampl > 0) {
+        if (!(o.sigma > 0)) return REF_EUNSUPPORTED;
+        push(plan, REF_OP_BLUR, 0, 0, 0);
+        LAST(plan)->d[0] = o.sigma;
+        LAST(plan)->d[1] = ref_get_switch("blur_honor_minampl") ? o.min_ampl : 0.2;
+        set_geom(plan, cw, ch, cb);
+    }
+    if (o.wm_enable) {
+        float op = o.wm_opacity == 0.0f ? 1.0f : o.wm_opacity;
+        int bb = has_alpha(cb) ? cb : cb + 1;
+        int wb = has_alpha(in->wm_bands) ? in->wm_bands : in->wm_bands + 1;
+        if (bb != wb || in->wm_w <= 0 || in->wm_h <= 0) return REF_EUNSUPPORTED;
+        push(plan, REF_OP_WATERMARK, 0, 0, 0);
+        LAST(plan)->a[0] = o.wm_left;
+        LAST(plan)->a[1] = o.wm_top;
+        LAST(plan)->a[2] = in->wm_w;
+        LAST(plan)->a[3] = in->wm_h;
+        LAST(plan)->a[4] = in->wm_bands;
+        LAST(plan)->d[0] = op;
+        cb = bb;
+        set_geom(plan, cw, ch, cb);
+    }
+    plan->out_w = cw;
+    plan->out_h = ch;
+    plan->out_bands = cb;
+    return REF_OK;
+}
+
+int ref_execute(const ref_plan *plan, const ref_img *in, const ref_img *wm, ref_img *out) {
+    if (in->w != plan->in_w || in->h != plan->in_h || in->bands != plan->in_bands) return REF_EINVAL;
+    ref_img cur = {0};
+    int e = img_copy(in, &cur);
+    if (e) return e;
+    for (int i = 0; i < plan->n_steps; i++) {
+        const ref_step *s = &plan->steps[i];
+        ref_img nx = {0};
+        switch (s->op) {
+        case REF_OP_ROT: e = ref_rot(&cur, &nx, s->a[0]); break;
+        case REF_OP_FLIP: e = ref_flip(&cur, &nx, s->a[0]); break;
+        case REF_OP_SHRINK: e = ref_shrink(&cur, &nx, s->a[0], s->a[1]); break;
+        case REF_OP_REDUCE: e = ref_reduce(&cur, &nx, s->d[0], s->d[1]); break;
+        case REF_OP_EXTRACT: e = ref_extract(&cur, &nx, s->a[0], s->a[1], s->a[2], s->a[3]); break;
+        case REF_OP_EMBED: e = ref_embed(&cur, &nx, s->a[0], s->a[1], s->a[2], s->a[3], s->a[4], s->a + 5); break;
+        case REF_OP_SMARTCROP: {
+            int l, t;
+            e = ref_smartcrop_origin(&cur, s->a[0], s->a[1], &l, &t);
+            if (!e) e = ref_extract(&cur, &nx, l, t, s->a[0], s->a[1]);
+            break;
+        }
+        case REF_OP_BLUR: e = ref_gaussblur(&cur, &nx, s->d[0], s->d[1]); break;
+        case REF_OP_WATERMARK:
+            if (!wm || !wm->data) e = REF_EINVAL;
+            else e = ref_watermark(&cur, wm, &nx, s->a[0], s->a[1], (float)s->d[0]);
+            break;
+        default: e = REF_EINVAL;
+        }
+        free(cur.data);
+        if (e) { free(nx.data); return e; }
+        cur = nx;
+        if (cur.w != s->out_w || cur.h != s->out_h || cur.bands != s->out_bands) {
+            free(cur.data);
+            return REF_EINVAL;
+        }
+    }
+    *out = cur;
+    return REF_OK;
+}
+
+/* CPU baseline: each image single-threaded (libvips concurrency 1 per request),
+ * OpenMP across images. */
+int ref_reduce_batch(const uint8_t *const *in, uint8_t *const *out, int n, int w, int h,
+                     int bands, double hshrink, double vshrink, int threads) {
+    int err = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+    for (int i = 0; i < n; i++) {
+        ref_img a = {(uint8_t *)in[i], w, h, bands}, o = {0};
+        int e = ref_reduce(&a, &o, hshrink, vshrink);
+        if (e) { err |= 1; continue; }
+        memcpy(out[i], o.data, (size_t)o.w * o.h * o.bands);
+        free(o.data);
+    }
+    return err ? REF_EINVAL : REF_OK;
+}

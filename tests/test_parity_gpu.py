@@ -1,0 +1,219 @@
+"""GPU parity: every libmipx kernel against the CPU oracle on the same seeded
+inputs, through the C-ABI.  The bar is BIT-EXACT for every op (the integer
+libvips C paths are reproduced exactly; the north star's ±1 LSB allowance for
+resize/blur/composite covers libvips' ORC vector paths, which the oracle does
+not model — see PARITY_ASSUMPTIONS.md)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def rand_img(rng, h, w, b):
+    return rng.integers(0, 256, (h, w, b), dtype=np.uint8)
+
+
+def smooth_img(rng, h, w, b):
+    """Band-limited content (exercises mid-range sums rather than noise)."""
+    y, x = np.mgrid[0:h, 0:w]
+    out = np.empty((h, w, b), np.uint8)
+    for c in range(b):
+        f = rng.uniform(0.01, 0.2, 2)
+        out[..., c] = (127.5 + 127.5 * np.sin(x * f[0] + c) * np.cos(y * f[1] - c)).astype(np.uint8)
+    return out
+
+
+def assert_same(got, want, what=""):
+    got = np.asarray(got)
+    want = np.asarray(want)
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    if not np.array_equal(got, want):
+        d = np.argwhere(got != want)
+        raise AssertionError(f"{what}: {len(d)} bytes differ, first at {d[0].tolist()} "
+                             f"got {got[tuple(d[0])]} want {want[tuple(d[0])]}")
+
+
+# ---------------------------------------------------------------- Lanczos3 reduce
+REDUCE_CASES = [
+    # (h, w, bands, hshrink, vshrink) — the first group takes the fused 2x2 kernel
+    (64, 64, 3, 2.0, 2.0), (270, 480, 3, 2.0, 2.0), (37, 52, 3, 2.0, 2.0), (130, 260, 4, 2.0, 2.0),
+    (9, 12, 3, 2.0, 2.0), (100, 300, 4, 2.0, 2.0),
+    # generic path
+    (64, 65, 3, 2.0, 2.0), (50, 77, 1, 2.0, 2.0), (40, 40, 2, 2.0, 2.0),
+    (270, 480, 3, 1.6, 1.6), (300, 200, 3, 2.4666666666666666, 2.4666666666666666),
+    (101, 131, 4, 1.3333333333333333, 1.3333333333333333), (60, 90, 3, 3.7, 1.2), (33, 17, 3, 1.0, 2.5),
+    (64, 64, 3, 2.5, 1.0), (128, 96, 3, 7.3, 7.3),
+]
+
+
+@pytest.mark.parametrize("h,w,b,hs,vs", REDUCE_CASES)
+def test_reduce_matches_oracle(gpu, oracle, rng, h, w, b, hs, vs):
+    imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+    got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+    for i in range(len(imgs)):
+        assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"reduce {h}x{w}x{b} {hs}x{vs} img{i}")
+
+
+@pytest.mark.parametrize("h,w,b,s", [(50, 60, 3, 1.6), (31, 45, 4, 2.0), (20, 33, 1, 3.3)])
+def test_reducev_reduceh_separately(gpu, oracle, rng, h, w, b, s):
+    img = rand_img(rng, h, w, b)
+    assert_same(gpu.run_op("reducev", img, vshrink=s)[0], oracle.reducev(img, s), "reducev")
+    assert_same(gpu.run_op("reduceh", img, hshrink=s)[0], oracle.reduceh(img, s), "reduceh")
+
+
+def test_reduce_extremes(gpu, oracle):
+    """All-0 / all-255 / checkerboard: clip paths and negative lobes."""
+    h, w = 40, 64
+    cases = [np.zeros((h, w, 3), np.uint8), np.full((h, w, 3), 255, np.uint8),
+             ((np.indices((h, w)).sum(0) % 2) * 255).astype(np.uint8)[..., None].repeat(3, 2)]
+    for img in cases:
+        for s in (2.0, 1.6):
+            assert_same(gpu.run_op("reduce", img, hshrink=s, vshrink=s)[0], oracle.reduce(img, s, s), f"reduce {s}")
+
+
+@pytest.mark.slow
+def test_reduce_4k_to_1080p_full_size(gpu, oracle, rng):
+    """BASELINE C2 geometry at full size (3840x2160x3 -> 1920x1080x3), bit-exact."""
+    imgs = np.stack([rand_img(rng, 2160, 3840, 3), smooth_img(rng, 2160, 3840, 3)])
+    got = gpu.run_op("reduce", imgs, hshrink=2.0, vshrink=2.0)
+    for i in range(2):
+        assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"4k img{i}")
+
+
+# ---------------------------------------------------------------- box shrink
+@pytest.mark.parametrize("h,w,b,hs,vs", [(64, 64, 3, 2, 2), (100, 75, 3, 8, 8), (31, 47, 4, 3, 5),
+                                         (3000 // 10, 4000 // 10, 3, 11, 11), (9, 9, 1, 4, 4), (20, 20, 2, 1, 3)])
+def test_shrink_matches_oracle(gpu, oracle, rng, h, w, b, hs, vs):
+    img = rand_img(rng, h, w, b)
+    assert_same(gpu.run_op("shrink", img, hshrink=hs, vshrink=vs)[0], oracle.shrink(img, hs, vs), "shrink")
+
+
+# ---------------------------------------------------------------- geometry (bit-exact by definition)
+@pytest.mark.parametrize("extend", range(7))
+@pytest.mark.parametrize("x,y,W,H", [(10, 5, 100, 60), (-7, -3, 40, 30), (0, 0, 64, 48), (30, 40, 50, 50),
+                                     (-100, 60, 300, 200)])
+def test_embed_matches_oracle(gpu, oracle, rng, extend, x, y, W, H):
+    for b in (3, 4):
+        img = rand_img(rng, 48, 64, b)
+        got = gpu.run_op("embed", img, x=x, y=y, width=W, height=H, extend=extend, background=(12, 200, 77))
+        assert_same(got[0], oracle.embed(img, x, y, W, H, extend, (12, 200, 77)), f"embed mode {extend} b{b}")
+
+
+@pytest.mark.parametrize("b", [1, 2, 3, 4])
+def test_extract_rot_flip(gpu, oracle, rng, b):
+    img = rand_img(rng, 37, 53, b)
+    assert_same(gpu.run_op("extract", img, left=5, top=7, width=31, height=20)[0],
+                oracle.extract(img, 5, 7, 31, 20), "extract")
+    for a in (0, 90, 180, 270):
+        assert_same(gpu.run_op("rot", img, angle=a)[0], oracle.rot(img, a), f"rot{a}")
+    for v in (0, 1):
+        assert_same(gpu.run_op("flip", img, vertical=v)[0], oracle.flip(img, v), f"flip{v}")
+    r = img
+    for _ in range(4):
+        r = gpu.run_op("rot", r, angle=90)[0]
+    assert_same(r, img, "rot90^4 == identity")
+
+
+# ---------------------------------------------------------------- gaussian blur
+@pytest.mark.parametrize("sigma", [0.8, 1.0, 3.0, 5.0, 12.5])
+@pytest.mark.parametrize("b", [3, 4])
+def test_gaussblur_matches_oracle(gpu, oracle, rng, sigma, b):
+    img = rand_img(rng, 45, 70, b)
+    assert_same(gpu.run_op("gaussblur", img, sigma=sigma, min_ampl=0.2)[0], oracle.gaussblur(img, sigma, 0.2),
+                f"blur {sigma}")
+
+
+# ---------------------------------------------------------------- watermark composite
+@pytest.mark.parametrize("bb,wb", [(3, 3), (3, 4), (4, 4), (4, 3), (1, 2), (2, 2)])
+@pytest.mark.parametrize("opacity", [0.5, 1.0, 0.2])
+def test_watermark_matches_oracle(gpu, oracle, rng, bb, wb, opacity):
+    base = rand_img(rng, 40, 60, bb)
+    wm = rand_img(rng, 16, 24, wb)
+    for left, top in ((3, 4), (50, 30), (0, 0)):
+        got = gpu.run_op("watermark", base, wm=wm, left=left, top=top, opacity=opacity)
+        assert_same(got[0], oracle.watermark(base, wm, left, top, opacity), f"wm {bb}/{wb} at {left},{top}")
+
+
+# ---------------------------------------------------------------- smartcrop
+@pytest.mark.parametrize("h,w,cw,ch", [(256, 341, 256, 256), (300, 400, 100, 80), (240, 180, 100, 100),
+                                       (512, 384, 200, 300)])
+def test_smartcrop_origin_identical(gpu, oracle, rng, h, w, cw, ch):
+    imgs = np.stack([smooth_img(rng, h, w, 3), rand_img(rng, h, w, 3)])
+    got = gpu.smartcrop_origins(imgs, cw, ch)
+    for i in range(len(imgs)):
+        assert tuple(got[i]) == oracle.smartcrop_origin(imgs[i], cw, ch), f"smartcrop img{i}"
+
+
+# ---------------------------------------------------------------- whole plans
+PLANS = [
+    # (opts, header (w, h, bands, type, orientation))
+    (dict(width=300, height=300, embed=1), (550, 740, 3, "png", 0)),
+    (dict(width=300, embed=1, crop=1), (550, 740, 3, "png", 0)),
+    (dict(width=300, height=200, crop=1, gravity=5), (640, 480, 3, "png", 0)),
+    (dict(width=256, height=256, crop=1, gravity=5), (1000, 750, 3, "png", 0)),
+    (dict(width=256, height=256), (1000, 750, 3, "png", 6)),
+    (dict(width=100, height=100, embed=1, extend=3), (320, 200, 4, "png", 0)),
+    (dict(rotate=90, flip=1, flop=1), (123, 77, 3, "png", 0)),
+    (dict(sigma=5.0), (200, 150, 4, "png", 0)),
+    (dict(top=10, left=20, area_width=100, area_height=50), (200, 150, 3, "png", 0)),
+    (dict(width=1024, embed=1), (2048, 2048, 4, "png", 0)),
+]
+
+
+@pytest.mark.parametrize("opts,hdr", PLANS)
+def test_plan_execution_matches_oracle(gpu, oracle, rng, opts, hdr):
+    w, h, b, typ, orient = hdr
+    p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(w, h, b, typ, orient))
+    e, rp = oracle.plan(opts, dict(w=w, h=h, bands=b, type=3, orientation=orient))
+    assert e == 0
+    imgs = np.stack([smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
+    got = gpu.execute(p, imgs)
+    for i in range(2):
+        assert_same(got[i], oracle.execute(rp, imgs[i]), f"plan {opts} img{i}")
+
+
+def test_watermark_plan(gpu, oracle, rng):
+    opts = dict(width=256, height=192, wm_enable=1, wm_left=16, wm_top=16, wm_opacity=0.5)
+    img = smooth_img(rng, 300, 400, 3)
+    wm = rand_img(rng, 128, 128, 4)
+    p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(400, 300, 3, "png", 0, wm_w=128, wm_h=128, wm_bands=4))
+    e, rp = oracle.plan(opts, dict(w=400, h=300, bands=3, type=3, wm_w=128, wm_h=128, wm_bands=4))
+    assert e == 0
+    assert_same(gpu.execute(p, img, wm)[0], oracle.execute(rp, img, wm), "thumbnail+watermark")
+
+
+def test_request_path_batches_and_matches(gpu, oracle, rng):
+    """mipx_submit/mipx_wait: pinned staging, queue, cross-request batching."""
+    eng = gpu.Engine(max_batch=8)
+    try:
+        p = gpu.plan_make(gpu.make_opts(width=160, height=120, embed=1), gpu.make_input(320, 240, 3, "png"))
+        e, rp = oracle.plan(dict(width=160, height=120, embed=1), dict(w=320, h=240, bands=3, type=3))
+        imgs = [rand_img(rng, 240, 320, 3) for _ in range(12)]
+        subs = [eng.submit(p, im) for im in imgs]
+        for (t, out), im in zip(subs, imgs):
+            eng.wait(t)
+            assert_same(out, oracle.execute(rp, im), "request path")
+    finally:
+        eng.shutdown()
+
+
+def test_golden_vectors_on_gpu(gpu):
+    """The committed fixtures (oracle outputs) are reproduced by the kernels."""
+    from conftest import load_golden
+    g = load_golden("ops.npz")
+    for key in g.files:
+        if not key.endswith("__in"):
+            continue
+        name = key[:-4]
+        src = g[key]
+        want = g[name + "__out"]
+        op, *args = name.split("__")
+        if op == "reduce":
+            got = gpu.run_op("reduce", src, hshrink=float(args[0]), vshrink=float(args[1]))[0]
+        elif op == "shrink":
+            got = gpu.run_op("shrink", src, hshrink=int(args[0]), vshrink=int(args[1]))[0]
+        elif op == "blur":
+            got = gpu.run_op("gaussblur", src, sigma=float(args[0]), min_ampl=0.2)[0]
+        else:
+            continue
+        assert_same(got, want, name)

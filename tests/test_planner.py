@@ -1,0 +1,212 @@
+"""Planner known-answer tests — pinned by the reference's OWN dimension tests.
+
+Every case below is an output size the reference asserts (image_test.go,
+server_test.go) for an imaginary operation on one of its fixtures.  The
+product planner (mipx_plan_make, host code, no GPU) and the oracle planner
+(ref_plan_make) must both produce it, and must agree step for step.
+"""
+import pytest
+
+import imaginary_amd as ia
+from imaginary_amd import imaginary as im
+
+# (label, fixture header, op wrapper, query, expected (w, h), reference line)
+LARGE = dict(w=1920, h=1080, type="jpeg", orientation=0)       # testdata/large.jpg
+IMAGINARY = dict(w=550, h=740, type="jpeg", orientation=1)     # testdata/imaginary.jpg
+
+KAT = [
+    ("resize 300x300", IMAGINARY, "Resize", {"width": 300, "height": 300}, (300, 300), "image_test.go:20"),
+    ("resize w300", IMAGINARY, "Resize", {"width": 300}, (300, 404), "image_test.go:36"),
+    ("resize w300 nocrop=false", IMAGINARY, "Resize", {"width": 300, "nocrop": "false"}, (300, 740),
+     "image_test.go:54"),
+    ("resize w300 nocrop=true", IMAGINARY, "Resize", {"width": 300, "nocrop": "true"}, (300, 404),
+     "image_test.go:72"),
+    ("fit 300x300", IMAGINARY, "Fit", {"width": 300, "height": 300}, (223, 300), "image_test.go:91"),
+    ("autorotate (orientation 1)", IMAGINARY, "Thumbnail", {"width": 550}, (550, 740), "image_test.go:105"),
+    ("pipeline crop 300x260", IMAGINARY, "Crop", {"width": 300, "height": 260}, (300, 260),
+     "image_test.go:136-141"),
+    ("crop w300", LARGE, "Crop", {"width": 300}, (300, 1080), "server_test.go:69"),
+    ("resize w300 nocrop=false", LARGE, "Resize", {"width": 300, "nocrop": "false"}, (300, 1080),
+     "server_test.go:102"),
+    ("enlarge 300x200", LARGE, "Enlarge", {"width": 300, "height": 200}, (300, 200), "server_test.go:135"),
+    ("extract 100,100 200x120", LARGE, "Extract",
+     {"top": 100, "left": 100, "areawidth": 200, "areaheight": 120}, (200, 120), "server_test.go:168"),
+    ("crop w300 type=auto", LARGE, "Crop", {"width": 300}, (300, 1080), "server_test.go:220"),
+    ("fit 300x300", LARGE, "Fit", {"width": 300, "height": 300}, (300, 169), "server_test.go:267"),
+    ("remote crop 200x200", LARGE, "Crop", {"width": 200, "height": 200}, (200, 200), "server_test.go:308"),
+    ("mount crop 200x200", LARGE, "Crop", {"width": 200, "height": 200}, (200, 200), "server_test.go:366"),
+]
+
+
+def _opts_for(opname, hdr, query):
+    """Run the image.go wrapper logic up to Process and capture the bimg options."""
+    o = im.build_params_from_query({k: str(v) for k, v in query.items()})
+    captured = {}
+
+    def fake_process(img, opts, **kw):
+        captured.update(opts)
+        return None
+
+    real = im.process
+    im.process = fake_process
+    try:
+        getattr(im, opname)(im.Decoded(pixels=__import__("numpy").zeros((1, 1, 3), "uint8"), type=hdr["type"],
+                                       orientation=hdr["orientation"], header_w=hdr["w"], header_h=hdr["h"]), o)
+    finally:
+        im.process = real
+    return captured
+
+
+def _product_plan(opts, hdr):
+    return ia.plan_make(ia.make_opts(**opts), ia.make_input(hdr["w"], hdr["h"], 3, hdr["type"], hdr["orientation"]))
+
+
+def _steps(p):
+    return [(p.steps[i].op, tuple(p.steps[i].a), tuple(round(x, 12) for x in p.steps[i].d),
+             p.steps[i].out_w, p.steps[i].out_h, p.steps[i].out_bands) for i in range(p.n_steps)]
+
+
+@pytest.mark.parametrize("label,hdr,op,query,want,ref", KAT, ids=[f"{k[0]}@{k[5]}" for k in KAT])
+def test_reference_dimension_kat(label, hdr, op, query, want, ref, oracle):
+    opts = _opts_for(op, hdr, query)
+    p = _product_plan(opts, hdr)
+    assert (p.out_w, p.out_h) == want, (label, ref, p.describe())
+    e, rp = oracle.plan(opts, dict(w=hdr["w"], h=hdr["h"], bands=3, type=1, orientation=hdr["orientation"]))
+    assert e == 0
+    assert (rp.out_w, rp.out_h) == want
+    assert _steps(p) == _steps(rp)
+    assert p.load_shrink == rp.load_shrink
+
+
+def test_c1_resize_width_300_plan():
+    """BASELINE config C1: POST /resize?width=300 on large.jpg -> JPEG shrink-on-load 4,
+    Lanczos3 reduce by 1.6 on 480x270 -> 300x169."""
+    opts = _opts_for("Resize", LARGE, {"width": 300})
+    p = _product_plan(opts, LARGE)
+    assert p.load_shrink == 4 and (p.in_w, p.in_h) == (480, 270)
+    d = p.describe()
+    assert d[0][0] == "reduce" and abs(d[0][2][0] - 1.6) < 1e-12 and d[0][3][:2] == (300, 169)
+    assert (p.out_w, p.out_h) == (300, 169)
+
+
+def test_c2_4k_to_1080p_plan():
+    """BASELINE config C2: decoded 3840x2160 -> 1920x1080 is one Lanczos3 reduce by 2 x 2."""
+    opts = _opts_for("Resize", dict(w=3840, h=2160, type="png", orientation=0), {"width": 1920, "height": 1080})
+    p = ia.plan_make(ia.make_opts(**opts), ia.make_input(3840, 2160, 3, "png"))
+    assert p.load_shrink == 1 and p.describe() == [("reduce", (0,) * 8, (2.0, 2.0, 0.0, 0.0), (1920, 1080, 3))]
+
+
+def test_c3_pipeline_plans():
+    """C3: resize w=1024 -> crop 768x512 -> blur sigma 5 on 2048^2 RGBA (PNG intermediates)."""
+    p1 = ia.plan_make(ia.make_opts(**_opts_for("Resize", dict(w=2048, h=2048, type="png", orientation=0),
+                                                  {"width": 1024})), ia.make_input(2048, 2048, 4, "png"))
+    assert [s[0] for s in p1.describe()] == ["reduce"] and (p1.out_w, p1.out_h) == (1024, 1024)
+    p2 = ia.plan_make(ia.make_opts(**_opts_for("Crop", dict(w=1024, h=1024, type="png", orientation=0),
+                                                  {"width": 768, "height": 512})), ia.make_input(1024, 1024, 4, "png"))
+    assert [s[0] for s in p2.describe()] == ["reduce", "extract"] and (p2.out_w, p2.out_h) == (768, 512)
+    p3 = ia.plan_make(ia.make_opts(**_opts_for("GaussianBlur", dict(w=768, h=512, type="png", orientation=0),
+                                                  {"sigma": 5})), ia.make_input(768, 512, 4, "png"))
+    assert p3.describe() == [("blur", (0,) * 8, (5.0, 0.2, 0.0, 0.0), (768, 512, 4))]
+
+
+FIT_KAT = [  # image_test.go:160-167
+    (1280, 1000, 710, 9999, 710, 555),
+    (1279, 1000, 710, 9999, 710, 555),
+    (900, 500, 312, 312, 312, 173),
+    (900, 500, 313, 313, 313, 174),
+    (1299, 2000, 710, 999, 649, 999),
+    (1500, 2000, 710, 999, 710, 947),
+]
+
+
+@pytest.mark.parametrize("iw,ih,fw,fh,ew,eh", FIT_KAT)
+def test_calculate_destination_fit_dimension(iw, ih, fw, fh, ew, eh, oracle):
+    assert ia.fit_dimension(iw, ih, fw, fh) == (ew, eh)
+    assert oracle.fit_dimension(iw, ih, fw, fh) == (ew, eh)
+
+
+@pytest.mark.parametrize("orientation,rot,flip", [(0, 0, 0), (1, 0, 0), (2, 0, 1), (3, 180, 0), (4, 180, 1),
+                                                   (5, 90, 1), (6, 90, 0), (7, 270, 1), (8, 270, 0)])
+def test_exif_autorotate_plan(orientation, rot, flip, oracle):
+    p = ia.plan_make(ia.make_opts(), ia.make_input(64, 48, 3, "jpeg", orientation))
+    ops = p.describe()
+    want = ([("rot", rot)] if rot else []) + ([("flip", 0)] if flip else [])
+    assert [(o[0], o[1][0]) for o in ops] == want
+    assert (p.out_w, p.out_h) == ((48, 64) if rot in (90, 270) else (64, 48))
+    e, rp = oracle.plan({}, dict(w=64, h=48, bands=3, type=1, orientation=orientation))
+    assert e == 0 and _steps(p) == _steps(rp)
+
+
+@pytest.mark.parametrize("rotate,angle", [(90, 90), (180, 180), (270, 270), (45, None), (360, 270), (100, 90)])
+def test_rotate_angle_normalisation(rotate, angle):
+    """bimg getAngle: remainder mod 90 dropped, capped at 270 (so 360 -> 270)."""
+    p = ia.plan_make(ia.make_opts(rotate=rotate), ia.make_input(64, 48, 3, "png"))
+    ops = p.describe()
+    if angle is None:
+        assert ops == []
+    else:
+        assert ops[0][0] == "rot" and ops[0][1][0] == angle
+
+
+def test_unsupported_ops_fall_back():
+    """Enlarge (vips_affine) and zoom are outside the engine: MIPX_EUNSUPPORTED."""
+    with pytest.raises(ia.MipxError) as e:
+        ia.plan_make(ia.make_opts(width=800, height=600, enlarge=1, crop=1), ia.make_input(400, 300, 3, "png"))
+    assert e.value.code == -2
+    with pytest.raises(ia.MipxError) as e:
+        ia.plan_make(ia.make_opts(zoom=2), ia.make_input(400, 300, 3, "png"))
+    assert e.value.code == -2
+
+
+def test_extract_out_of_bounds_is_einval():
+    with pytest.raises(ia.MipxError) as e:
+        ia.plan_make(ia.make_opts(top=100, left=100, area_width=400, area_height=10),
+                     ia.make_input(400, 300, 3, "png"))
+    assert e.value.code == -1
+
+
+def test_embed_modes_and_background_mapping(oracle):
+    for mode in range(7):
+        opts = dict(width=100, height=100, embed=1, extend=mode, background=(10, 20, 30))
+        p = ia.plan_make(ia.make_opts(**opts), ia.make_input(160, 40, 3, "png"))
+        e, rp = oracle.plan(opts, dict(w=160, h=40, bands=3, type=3))
+        assert e == 0 and _steps(p) == _steps(rp)
+        emb = [s for s in p.describe() if s[0] == "embed"]
+        assert emb and emb[0][1][4] == (5 if mode == 6 else mode)
+
+
+def test_gravity_crop_origins(oracle):
+    for g in range(5):
+        opts = dict(width=50, height=50, crop=1, gravity=g)
+        p = ia.plan_make(ia.make_opts(**opts), ia.make_input(120, 80, 3, "png"))
+        e, rp = oracle.plan(opts, dict(w=120, h=80, bands=3, type=3))
+        assert e == 0 and _steps(p) == _steps(rp)
+
+
+def test_random_plans_agree_with_oracle(oracle):
+    """Fuzz the option space: product and oracle planners agree on every field."""
+    import numpy as np
+    r = np.random.default_rng(7)
+    agree = 0
+    for _ in range(1500):
+        w, h = int(r.integers(1, 5000)), int(r.integers(1, 5000))
+        opts = dict(width=int(r.choice([0, r.integers(1, 3000)])), height=int(r.choice([0, r.integers(1, 3000)])),
+                    crop=int(r.integers(0, 2)), embed=int(r.integers(0, 2)), force=int(r.integers(0, 2)),
+                    gravity=int(r.integers(0, 6)), extend=int(r.integers(0, 7)),
+                    rotate=int(r.choice([0, 0, 90, 180, 270, 45])), flip=int(r.integers(0, 2)),
+                    flop=int(r.integers(0, 2)), sigma=float(r.choice([0, 0, 1.5, 5.0])))
+        typ = int(r.choice([1, 2, 3]))
+        orient = int(r.integers(0, 9))
+        inp = dict(w=w, h=h, bands=int(r.integers(1, 5)), type=typ, orientation=orient)
+        try:
+            p = ia.plan_make(ia.make_opts(**opts), ia.make_input(inp["w"], inp["h"], inp["bands"], typ, orient))
+            pe = 0
+        except ia.MipxError as ex:
+            pe, p = ex.code, None
+        e, rp = oracle.plan(opts, inp)
+        assert pe == e, (opts, inp)
+        if e == 0:
+            assert _steps(p) == _steps(rp), (opts, inp)
+            assert (p.out_w, p.out_h, p.load_shrink) == (rp.out_w, rp.out_h, rp.load_shrink)
+            agree += 1
+    assert agree > 500
