@@ -167,10 +167,14 @@ __global__ void __launch_bounds__(256) k_reduceh_generic(
 // ds_read_b128 and writes two output pixels per lane.  The intermediate never
 // touches HBM.
 // ===========================================================================
-constexpr int kTW = 64;          // output pixels per strip
 constexpr int kR = 12;           // output rows per LDS chunk (2 ring periods)
-constexpr int kNPX = 2 * kTW + 9;  // intermediate pixels a strip reads (2x0-5 .. 2x0+2TW+3)
 constexpr int kThreads = 128;
+// output pixels per strip: the vertical pass needs B * (2 TW + 9) / 4 + 1 dwords
+// per input row, one per lane, within kThreads lanes
+template <int B> constexpr int strip_width() { return B == 3 ? 64 : 56; }
+template <int B> constexpr int strip_pixels() { return 2 * strip_width<B>() + 9; }  // 2x0-5 .. 2x0+2TW+3
+static_assert((3 * strip_pixels<3>() + 3 + 3) / 4 <= kThreads, "RGB strip too wide");
+static_assert((4 * strip_pixels<4>() + 3 + 3) / 4 <= kThreads, "RGBA strip too wide");
 
 struct Reduce2Args {
     const u8 *in;
@@ -184,6 +188,8 @@ struct Reduce2Args {
 template <int B, bool EDGE>
 __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int strip, int band,
                                              float4 *lds) {
+    constexpr int kTW = strip_width<B>();
+    constexpr int kNPX = strip_pixels<B>();
     const int tid = threadIdx.x;
     const int x0 = strip * kTW;
     const int row_bytes = a.w * B;
@@ -293,13 +299,20 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
                                     (fixed_round_u(o0.z) << 16) | (fixed_round_u(o0.w) << 24);
                 const uint32_t w1 = fixed_round_u(o1.x) | (fixed_round_u(o1.y) << 8) |
                                     (fixed_round_u(o1.z) << 16) | (fixed_round_u(o1.w) << 24);
-                if (two) *reinterpret_cast<uint2 *>(q) = uint2{w0, w1};
-                else *reinterpret_cast<uint32_t *>(q) = w0;
+                uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
+                if (two && (reinterpret_cast<uintptr_t>(q) & 7u) == 0) *reinterpret_cast<uint2 *>(q) = uint2{w0, w1};
+                else {
+                    q32[0] = w0;
+                    if (two) q32[1] = w1;
+                }
             } else {  // B == 3: 6 bytes, 2-byte aligned
                 const uint32_t r0 = fixed_round_u(o0.x), g0 = fixed_round_u(o0.y), b0 = fixed_round_u(o0.z);
                 const uint32_t r1 = fixed_round_u(o1.x), g1 = fixed_round_u(o1.y), b1 = fixed_round_u(o1.z);
                 uint16_t *q16 = reinterpret_cast<uint16_t *>(q);
-                if (two) {
+                if ((reinterpret_cast<uintptr_t>(q) & 1u) != 0) {  // odd row start: byte stores
+                    q[0] = static_cast<u8>(r0), q[1] = static_cast<u8>(g0), q[2] = static_cast<u8>(b0);
+                    if (two) q[3] = static_cast<u8>(r1), q[4] = static_cast<u8>(g1), q[5] = static_cast<u8>(b1);
+                } else if (two) {
                     q16[0] = static_cast<uint16_t>(r0 | (g0 << 8));
                     q16[1] = static_cast<uint16_t>(b0 | (r1 << 8));
                     q16[2] = static_cast<uint16_t>(g1 | (b1 << 8));
@@ -315,7 +328,8 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 
 template <int B>
 __global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
-    __shared__ float4 lds[kR * kNPX];
+    constexpr int kTW = strip_width<B>();
+    __shared__ float4 lds[kR * strip_pixels<B>()];
     const uint32_t nb = gridDim.x;
     const uint32_t t = xcd_remap(blockIdx.x, nb);
     const int strip = t % a.n_strips;
@@ -757,7 +771,8 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     a.h = h;
     a.ow = out_size_reduce(w, 2.0);
     a.oh = out_size_reduce(h, 2.0);
-    a.n_strips = (a.ow + kTW - 1) / kTW;
+    const int tw = b == 3 ? strip_width<3>() : strip_width<4>();
+    a.n_strips = (a.ow + tw - 1) / tw;
     const int chunks = (a.oh + kR - 1) / kR;
     const int chunks_per_band = std::max(1, std::min(chunks, 15));
     a.band_rows = chunks_per_band * kR;
