@@ -157,24 +157,35 @@ __global__ void __launch_bounds__(256) k_reduceh_generic(
 // The host verifies that shape on the actual integer table before choosing
 // this kernel, so the arithmetic is exactly libvips' 13-tap sum.
 //
-// One workgroup = a strip of TW output pixels x a band of rows.  Vertical pass:
-// each lane owns one dword (4 byte-columns) of the input strip and walks down
-// the band, keeping the six odd input rows of the current window in a static
-// register ring (slot = odd-row index mod 6, loop unrolled by 12 so every
-// index is a constant); each input byte is loaded and converted once.  The
-// rounded uchar intermediate (libvips materialises it between reducev and
-// reduceh) lands in LDS as one float4 per pixel; horizontal pass reads it with
-// ds_read_b128 and writes two output pixels per lane.  The intermediate never
-// touches HBM.
+// One workgroup = a strip of TW output pixels x a band of rows.
+//  * Vertical pass: lane t owns dword t of the strip's input bytes (channel
+//    agnostic) and walks down the band with the six odd rows of the current
+//    window in a static register ring (slot = odd-row index mod 6, unrolled
+//    by 12); each input byte is loaded and converted once.  The rounded uchar
+//    intermediate (libvips materialises it between reducev and reduceh) is
+//    packed back to a dword and written to LDS in input byte order: one
+//    conflict-free ds_write_b32 per lane and row.
+//  * Horizontal pass: an item is K output pixels of one row; it reads the
+//    13-dword byte window it needs (ds_read_b64: lane stride 6 dwords for RGB,
+//    conflict-free; ds_read_b128 for RGBA, stride 4 dwords), converts each
+//    byte once and stores 12 (RGB) / 8 (RGBA) contiguous output bytes.
+// The intermediate never touches HBM, and the LDS image is 7.5 KB per
+// workgroup, so occupancy is set by registers, not LDS.
 // ===========================================================================
 constexpr int kR = 12;           // output rows per LDS chunk (2 ring periods)
 constexpr int kThreads = 128;
-// output pixels per strip: the vertical pass needs B * (2 TW + 9) / 4 + 1 dwords
-// per input row, one per lane, within kThreads lanes
-template <int B> constexpr int strip_width() { return B == 3 ? 64 : 56; }
-template <int B> constexpr int strip_pixels() { return 2 * strip_width<B>() + 9; }  // 2x0-5 .. 2x0+2TW+3
-static_assert((3 * strip_pixels<3>() + 3 + 3) / 4 <= kThreads, "RGB strip too wide");
-static_assert((4 * strip_pixels<4>() + 3 + 3) / 4 <= kThreads, "RGBA strip too wide");
+constexpr int kPitch = 160;      // LDS dwords per intermediate row (== 32 mod 64)
+
+template <int B>
+struct R2 {
+    static constexpr int TW = B == 3 ? 64 : 56;     // output pixels per strip
+    static constexpr int NPX = 2 * TW + 9;           // intermediate px 2x0-5 .. 2x0+2TW+3
+    static constexpr int K = B == 3 ? 4 : 2;         // output pixels per horizontal item
+    static constexpr int OFF0 = B == 3 ? 1 : 0;      // B*(2x0-5) - floor4(B*(2x0-5))
+    static constexpr int ND = (B * NPX + OFF0 + 3) / 4;  // dwords per row
+    static_assert(ND <= kThreads && ND <= kPitch, "strip too wide");
+    static_assert((B * 2 * K) % 8 == 0, "window start must be 8-byte aligned");
+};
 
 struct Reduce2Args {
     const u8 *in;
@@ -185,47 +196,40 @@ struct Reduce2Args {
     float c0, c1, c3, c5;
 };
 
+__device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
+    uint32_t v = __builtin_amdgcn_cvt_pk_u8_f32(fixed_round_f(a), 0, 0u);
+    v = __builtin_amdgcn_cvt_pk_u8_f32(fixed_round_f(b), 1, v);
+    v = __builtin_amdgcn_cvt_pk_u8_f32(fixed_round_f(c), 2, v);
+    return __builtin_amdgcn_cvt_pk_u8_f32(fixed_round_f(d), 3, v);
+}
+
 template <int B, bool EDGE>
 __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int strip, int band,
-                                             float4 *lds) {
-    constexpr int kTW = strip_width<B>();
-    constexpr int kNPX = strip_pixels<B>();
+                                             uint32_t *lds) {
+    using G = R2<B>;
+    constexpr int TW = G::TW, K = G::K;
     const int tid = threadIdx.x;
-    const int x0 = strip * kTW;
+    const int x0 = strip * TW;
     const int row_bytes = a.w * B;
     const u8 *src = a.in + img * a.in_img;
-    const int px0 = 2 * x0 - 5;                 // first intermediate pixel of the strip
-    const int bstart = B * px0;                 // may be negative
-    const int base = (bstart >= 0 ? bstart : bstart - 3) & ~3;  // floor to a dword
-    const int nd = (B * (2 * x0 + 2 * kTW + 4) - base + 3) >> 2;
+    const int px0 = 2 * x0 - 5;          // first intermediate pixel of the strip
+    const int base = (B * px0) & ~3;     // floor to a dword (two's complement)
     const int byte0 = base + 4 * tid;
-    const bool vlane = tid < nd && byte0 >= 0 && byte0 + 4 <= row_bytes;
-    // LDS float slot (pixel * 4 + channel) of each of this lane's 4 bytes; -1 = none
-    int slot[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int g = byte0 + k;
-        const int p = g >= 0 ? g / B : -1;
-        const int lp = p - px0;
-        slot[k] = (vlane && lp >= 0 && lp < kNPX) ? lp * 4 + (g - p * B) : -1;
-    }
-    float *ldsf = reinterpret_cast<float *>(lds);
-
+    const bool vlane = tid < G::ND && byte0 >= 0 && byte0 + 4 <= row_bytes;
     const int y0 = band * a.band_rows;
     const int y1 = min(y0 + a.band_rows, a.oh);
+    const float c0 = a.c0, c1 = a.c1, c3 = a.c3, c5 = a.c5;
+
     auto load_row = [&](int r) -> uint32_t {
         r = clampi(r, 0, a.h - 1);
-        return vlane ? *reinterpret_cast<const uint32_t *>(src + static_cast<size_t>(r) * row_bytes + byte0)
+        return vlane ? __builtin_nontemporal_load(
+                           reinterpret_cast<const uint32_t *>(src + static_cast<size_t>(r) * row_bytes + byte0))
                      : 0u;
     };
-    auto cvt4 = [](uint32_t v) {
-        return float4{ubyte_f<0>(v), ubyte_f<1>(v),
-                      ubyte_f<2>(v), ubyte_f<3>(v)};
-    };
+    auto cvt4 = [](uint32_t v) { return float4{ubyte_f<0>(v), ubyte_f<1>(v), ubyte_f<2>(v), ubyte_f<3>(v)}; };
 
-    // odd-row ring: slot s holds odd row 2m+1 with m = s (mod 6)
+    // odd-row ring: slot s holds odd row 2m+1 with m = s (mod 6); y0 % 12 == 0
     float4 ring[6];
-    // prologue: m = y0-3 .. y0+1 (y0 is a multiple of 12, so slots 3,4,5,0,1)
     ring[3] = cvt4(load_row(2 * (y0 - 3) + 1));
     ring[4] = cvt4(load_row(2 * (y0 - 2) + 1));
     ring[5] = cvt4(load_row(2 * (y0 - 1) + 1));
@@ -233,92 +237,114 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
     ring[1] = cvt4(load_row(2 * (y0 + 1) + 1));
     ring[2] = float4{0.f, 0.f, 0.f, 0.f};
 
-    uint32_t odd[kR], even[kR];
-#pragma unroll
-    for (int u = 0; u < kR; ++u) {
-        odd[u] = load_row(2 * (y0 + u + 2) + 1);
-        even[u] = load_row(2 * (y0 + u));
-    }
-
-    const float c0 = a.c0, c1 = a.c1, c3 = a.c3, c5 = a.c5;
     for (int yc = y0; yc < y1; yc += kR) {
-        // ---- vertical pass: kR intermediate rows into LDS ----
+        // ---- vertical pass: kR intermediate rows -> LDS (packed uchar) ----
+        uint32_t odd[kR], even[kR];
+#pragma unroll
+        for (int u = 0; u < kR; ++u) {
+            odd[u] = load_row(2 * (yc + u + 2) + 1);
+            even[u] = load_row(2 * (yc + u));
+        }
 #pragma unroll
         for (int u = 0; u < kR; ++u) {
             ring[(u + 2) % 6] = cvt4(odd[u]);
             const float4 e = cvt4(even[u]);
             const float4 m5 = ring[(u + 3) % 6], m3 = ring[(u + 4) % 6], m1 = ring[(u + 5) % 6];
             const float4 p1 = ring[u % 6], p3 = ring[(u + 1) % 6], p5 = ring[(u + 2) % 6];
-            float v[4];
-            v[0] = c0 * e.x + c1 * (m1.x + p1.x) + c3 * (m3.x + p3.x) + c5 * (m5.x + p5.x);
-            v[1] = c0 * e.y + c1 * (m1.y + p1.y) + c3 * (m3.y + p3.y) + c5 * (m5.y + p5.y);
-            v[2] = c0 * e.z + c1 * (m1.z + p1.z) + c3 * (m3.z + p3.z) + c5 * (m5.z + p5.z);
-            v[3] = c0 * e.w + c1 * (m1.w + p1.w) + c3 * (m3.w + p3.w) + c5 * (m5.w + p5.w);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (slot[k] >= 0) ldsf[u * kNPX * 4 + slot[k]] = fixed_round_f(v[k]);
+            const float v0 = c0 * e.x + c1 * (m1.x + p1.x) + c3 * (m3.x + p3.x) + c5 * (m5.x + p5.x);
+            const float v1 = c0 * e.y + c1 * (m1.y + p1.y) + c3 * (m3.y + p3.y) + c5 * (m5.y + p5.y);
+            const float v2 = c0 * e.z + c1 * (m1.z + p1.z) + c3 * (m3.z + p3.z) + c5 * (m5.z + p5.z);
+            const float v3 = c0 * e.w + c1 * (m1.w + p1.w) + c3 * (m3.w + p3.w) + c5 * (m5.w + p5.w);
+            if (tid < G::ND) lds[u * kPitch + tid] = pack4(v0, v1, v2, v3);
         }
         __syncthreads();
-        // prefetch the next chunk's rows; they fly during the horizontal pass
-        if (yc + kR < y1) {
-#pragma unroll
-            for (int u = 0; u < kR; ++u) {
-                odd[u] = load_row(2 * (yc + kR + u + 2) + 1);
-                even[u] = load_row(2 * (yc + kR + u));
-            }
-        }
-        // ---- horizontal pass: 2 output pixels per item ----
-        for (int it = tid; it < kR * (kTW / 2); it += kThreads) {
-            const int u = it / (kTW / 2);
-            const int jp = it - u * (kTW / 2);
-            const int x = x0 + 2 * jp;
+        // ---- horizontal pass: K output pixels per item ----
+        constexpr int items_per_row = TW / K;
+        for (int it = tid; it < kR * items_per_row; it += kThreads) {
+            const int u = it / items_per_row;
+            const int j = it - u * items_per_row;
+            const int x = x0 + K * j;
             const int y = yc + u;
             if (y >= a.oh || x >= a.ow) continue;
-            const float4 *rowp = lds + u * kNPX;
-            float4 v[13];
+            const uint32_t *row = lds + u * kPitch;
+            const u8 *rowb = reinterpret_cast<const u8 *>(row);
+            // px[t][c]: intermediate pixel 2x - 5 + t, channel c (t = 0 .. 2K+8)
+            float px[2 * K + 9][B];
+            if (!EDGE) {
+                constexpr int W0 = (B * 2 * K) / 4;  // window start (dwords) per item
+                uint32_t win[13];
+                if (B == 3) {
+                    const uint2 *r2 = reinterpret_cast<const uint2 *>(row + W0 * j);
 #pragma unroll
-            for (int k = 0; k <= 12; ++k) {
-                if (k == 1 || k == 3 || k == 9 || k == 11) continue;
-                int lp = 4 * jp + k;
-                if (EDGE) lp = clampi(lp + px0, 0, a.w - 1) - px0;
-                v[k] = rowp[lp];
-            }
-            float4 o0, o1;
-            o0.x = c0 * v[5].x + c1 * (v[4].x + v[6].x) + c3 * (v[2].x + v[8].x) + c5 * (v[0].x + v[10].x);
-            o0.y = c0 * v[5].y + c1 * (v[4].y + v[6].y) + c3 * (v[2].y + v[8].y) + c5 * (v[0].y + v[10].y);
-            o0.z = c0 * v[5].z + c1 * (v[4].z + v[6].z) + c3 * (v[2].z + v[8].z) + c5 * (v[0].z + v[10].z);
-            o0.w = c0 * v[5].w + c1 * (v[4].w + v[6].w) + c3 * (v[2].w + v[8].w) + c5 * (v[0].w + v[10].w);
-            o1.x = c0 * v[7].x + c1 * (v[6].x + v[8].x) + c3 * (v[4].x + v[10].x) + c5 * (v[2].x + v[12].x);
-            o1.y = c0 * v[7].y + c1 * (v[6].y + v[8].y) + c3 * (v[4].y + v[10].y) + c5 * (v[2].y + v[12].y);
-            o1.z = c0 * v[7].z + c1 * (v[6].z + v[8].z) + c3 * (v[4].z + v[10].z) + c5 * (v[2].z + v[12].z);
-            o1.w = c0 * v[7].w + c1 * (v[6].w + v[8].w) + c3 * (v[4].w + v[10].w) + c5 * (v[2].w + v[12].w);
-            u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
-            const bool two = x + 1 < a.ow;
-            if (B == 4) {
-                const uint32_t w0 = fixed_round_u(o0.x) | (fixed_round_u(o0.y) << 8) |
-                                    (fixed_round_u(o0.z) << 16) | (fixed_round_u(o0.w) << 24);
-                const uint32_t w1 = fixed_round_u(o1.x) | (fixed_round_u(o1.y) << 8) |
-                                    (fixed_round_u(o1.z) << 16) | (fixed_round_u(o1.w) << 24);
-                uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
-                if (two && (reinterpret_cast<uintptr_t>(q) & 7u) == 0) *reinterpret_cast<uint2 *>(q) = uint2{w0, w1};
-                else {
-                    q32[0] = w0;
-                    if (two) q32[1] = w1;
-                }
-            } else {  // B == 3: 6 bytes, 2-byte aligned
-                const uint32_t r0 = fixed_round_u(o0.x), g0 = fixed_round_u(o0.y), b0 = fixed_round_u(o0.z);
-                const uint32_t r1 = fixed_round_u(o1.x), g1 = fixed_round_u(o1.y), b1 = fixed_round_u(o1.z);
-                uint16_t *q16 = reinterpret_cast<uint16_t *>(q);
-                if ((reinterpret_cast<uintptr_t>(q) & 1u) != 0) {  // odd row start: byte stores
-                    q[0] = static_cast<u8>(r0), q[1] = static_cast<u8>(g0), q[2] = static_cast<u8>(b0);
-                    if (two) q[3] = static_cast<u8>(r1), q[4] = static_cast<u8>(g1), q[5] = static_cast<u8>(b1);
-                } else if (two) {
-                    q16[0] = static_cast<uint16_t>(r0 | (g0 << 8));
-                    q16[1] = static_cast<uint16_t>(b0 | (r1 << 8));
-                    q16[2] = static_cast<uint16_t>(g1 | (b1 << 8));
+                    for (int q = 0; q < 6; ++q) {
+                        const uint2 d = r2[q];
+                        win[2 * q] = d.x;
+                        win[2 * q + 1] = d.y;
+                    }
+                    win[12] = row[W0 * j + 12];
                 } else {
-                    q16[0] = static_cast<uint16_t>(r0 | (g0 << 8));
-                    q[2] = static_cast<u8>(b0);
+                    const uint4 *r4 = reinterpret_cast<const uint4 *>(row + W0 * j);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const uint4 d = r4[q];
+                        win[4 * q] = d.x, win[4 * q + 1] = d.y, win[4 * q + 2] = d.z, win[4 * q + 3] = d.w;
+                    }
+                    win[12] = row[W0 * j + 12];
+                }
+#pragma unroll
+                for (int t = 0; t < 2 * K + 9; ++t)
+#pragma unroll
+                    for (int c = 0; c < B; ++c) {
+                        const int lb = B * t + c + G::OFF0;
+                        const uint32_t d = win[lb >> 2];
+                        switch (lb & 3) {
+                            case 0: px[t][c] = ubyte_f<0>(d); break;
+                            case 1: px[t][c] = ubyte_f<1>(d); break;
+                            case 2: px[t][c] = ubyte_f<2>(d); break;
+                            default: px[t][c] = ubyte_f<3>(d); break;
+                        }
+                    }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 2 * K + 9; ++t) {
+                    const int p = clampi(2 * x - 5 + t, 0, a.w - 1);
+                    const int lb = B * (p - px0) + G::OFF0;
+#pragma unroll
+                    for (int c = 0; c < B; ++c) px[t][c] = static_cast<float>(rowb[lb + c]);
+                }
+            }
+            // output pixel k uses px[2k + 5 + o], o in {-5,-3,-1,0,1,3,5}
+            float o[K][B];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int c = 0; c < B; ++c) {
+                    const int m = 2 * k + 5;
+                    o[k][c] = c0 * px[m][c] + c1 * (px[m - 1][c] + px[m + 1][c]) +
+                              c3 * (px[m - 3][c] + px[m + 3][c]) + c5 * (px[m - 5][c] + px[m + 5][c]);
+                }
+            u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
+            const bool full = x + K <= a.ow;
+            if (B == 3) {
+                const uint32_t d0 = pack4(o[0][0], o[0][1], o[0][2], o[1][0]);
+                const uint32_t d1 = pack4(o[1][1], o[1][2], o[2][0], o[2][1]);
+                const uint32_t d2 = pack4(o[2][2], o[3][0], o[3][1], o[3][2]);
+                if (full && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+                    *reinterpret_cast<uint3 *>(q) = uint3{d0, d1, d2};
+                } else {
+                    const uint32_t dd[3] = {d0, d1, d2};
+                    const int nb = (full ? K : a.ow - x) * B;
+                    for (int i = 0; i < nb; ++i) q[i] = static_cast<u8>(dd[i >> 2] >> (8 * (i & 3)));
+                }
+            } else {
+                const uint32_t d0 = pack4(o[0][0], o[0][1], o[0][2], o[0][3]);
+                const uint32_t d1 = pack4(o[1][0], o[1][1], o[1][2], o[1][3]);
+                uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
+                if (full && (reinterpret_cast<uintptr_t>(q) & 7u) == 0) {
+                    *reinterpret_cast<uint2 *>(q) = uint2{d0, d1};
+                } else {
+                    q32[0] = d0;
+                    if (full) q32[1] = d1;
                 }
             }
         }
@@ -328,16 +354,14 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 
 template <int B>
 __global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
-    constexpr int kTW = strip_width<B>();
-    __shared__ float4 lds[kR * strip_pixels<B>()];
-    const uint32_t nb = gridDim.x;
-    const uint32_t t = xcd_remap(blockIdx.x, nb);
+    __shared__ uint32_t lds[kR * kPitch];
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = t % a.n_strips;
     const int rest = t / a.n_strips;
     const int band = rest % a.n_bands;
     const int img = rest / a.n_bands;
-    const int x0 = strip * kTW;
-    const bool edge = (2 * x0 - 5 < 0) || (2 * x0 + 2 * kTW + 3 > a.w - 1);
+    const int x0 = strip * R2<B>::TW;
+    const bool edge = (2 * x0 - 5 < 0) || (2 * x0 + 2 * R2<B>::TW + 3 > a.w - 1);
     if (edge) reduce2_tile<B, true>(a, img, strip, band, lds);
     else reduce2_tile<B, false>(a, img, strip, band, lds);
 }
@@ -771,7 +795,7 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     a.h = h;
     a.ow = out_size_reduce(w, 2.0);
     a.oh = out_size_reduce(h, 2.0);
-    const int tw = b == 3 ? strip_width<3>() : strip_width<4>();
+    const int tw = b == 3 ? R2<3>::TW : R2<4>::TW;
     a.n_strips = (a.ow + tw - 1) / tw;
     const int chunks = (a.oh + kR - 1) / kR;
     const int chunks_per_band = std::max(1, std::min(chunks, 15));
