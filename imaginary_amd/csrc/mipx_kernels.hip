@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -178,7 +179,7 @@ constexpr int kPitch = 160;      // LDS dwords per intermediate row (== 32 mod 6
 
 template <int B>
 struct R2 {
-    static constexpr int TW = B == 3 ? 64 : 56;     // output pixels per strip
+    static constexpr int TW = B == 3 ? 80 : 56;     // output pixels per strip
     static constexpr int NPX = 2 * TW + 9;           // intermediate px 2x0-5 .. 2x0+2TW+3
     static constexpr int K = B == 3 ? 4 : 2;         // output pixels per horizontal item
     static constexpr int OFF0 = B == 3 ? 1 : 0;      // B*(2x0-5) - floor4(B*(2x0-5))
@@ -193,14 +194,41 @@ struct Reduce2Args {
     int w, h, ow, oh;
     int n_strips, n_bands, band_rows;  // band_rows multiple of kR
     long long in_img, out_img;
-    float c0, c1, c3, c5;
+    // taps pre-scaled by 1/4096 (exact: powers of two); the bias 2^-13 turns the
+    // exact chain into RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5) at the cvt
+    float c0, c1, c3, c5, bias;
 };
 
-__device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
-    uint32_t v = __builtin_amdgcn_cvt_pk_u8_f32(fixed_round_f(a), 0, 0u);
-    v = __builtin_amdgcn_cvt_pk_u8_f32(fixed_round_f(b), 1, v);
-    v = __builtin_amdgcn_cvt_pk_u8_f32(fixed_round_f(c), 2, v);
-    return __builtin_amdgcn_cvt_pk_u8_f32(fixed_round_f(d), 3, v);
+// byte k of a dword as float, opaque to instcombine so that a row converted
+// once is reused by every output it feeds (otherwise (float)a + (float)b is
+// folded into (float)(a + b): one convert per use instead of per byte)
+template <int K>
+__device__ __forceinline__ float ubyte_once(uint32_t v) {
+    float f = ubyte_f<K>(v);
+    asm("" : "+v"(f));
+    return f;
+}
+__device__ __forceinline__ float4 cvt4_once(uint32_t v) {
+    return float4{ubyte_once<0>(v), ubyte_once<1>(v), ubyte_once<2>(v), ubyte_once<3>(v)};
+}
+
+// c0 e + c1 (m1 + p1) + c3 (m3 + p3) + c5 (m5 + p5) with pre-scaled taps and the
+// bias: every partial is exact on a 1/8192 grid below 2^9, so the result is
+// exactly sum/4096 + 2^-13
+__device__ __forceinline__ float tap7(float c0, float c1, float c3, float c5, float bias, float e, float m1,
+                                      float p1, float m3, float p3, float m5, float p5) {
+    float acc = __builtin_fmaf(c0, e, bias);
+    acc = __builtin_fmaf(c1, m1 + p1, acc);
+    acc = __builtin_fmaf(c3, m3 + p3, acc);
+    return __builtin_fmaf(c5, m5 + p5, acc);
+}
+// v_cvt_pk_u8_f32 rounds to nearest-even and saturates to 0..255; on the
+// 1/4096 grid RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5) (no ties occur)
+__device__ __forceinline__ uint32_t pack4b(float a, float b, float c, float d) {
+    uint32_t v = __builtin_amdgcn_cvt_pk_u8_f32(a, 0, 0u);
+    v = __builtin_amdgcn_cvt_pk_u8_f32(b, 1, v);
+    v = __builtin_amdgcn_cvt_pk_u8_f32(c, 2, v);
+    return __builtin_amdgcn_cvt_pk_u8_f32(d, 3, v);
 }
 
 template <int B, bool EDGE>
@@ -211,30 +239,31 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
     const int tid = threadIdx.x;
     const int x0 = strip * TW;
     const int row_bytes = a.w * B;
-    const u8 *src = a.in + img * a.in_img;
     const int px0 = 2 * x0 - 5;          // first intermediate pixel of the strip
     const int base = (B * px0) & ~3;     // floor to a dword (two's complement)
     const int byte0 = base + 4 * tid;
     const bool vlane = tid < G::ND && byte0 >= 0 && byte0 + 4 <= row_bytes;
+    // raw buffer loads: per-lane byte offset in voffset, row offset in soffset;
+    // lanes outside the row get an out-of-range voffset and read 0
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<u8 *>(a.in + img * a.in_img), 0, static_cast<int>(a.in_img), 0x00020000);
+    const uint32_t voff = vlane ? static_cast<uint32_t>(byte0) : 0x80000000u;
     const int y0 = band * a.band_rows;
     const int y1 = min(y0 + a.band_rows, a.oh);
-    const float c0 = a.c0, c1 = a.c1, c3 = a.c3, c5 = a.c5;
+    const float c0 = a.c0, c1 = a.c1, c3 = a.c3, c5 = a.c5, bias = a.bias;
 
     auto load_row = [&](int r) -> uint32_t {
         r = clampi(r, 0, a.h - 1);
-        return vlane ? __builtin_nontemporal_load(
-                           reinterpret_cast<const uint32_t *>(src + static_cast<size_t>(r) * row_bytes + byte0))
-                     : 0u;
+        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * row_bytes, 0));
     };
-    auto cvt4 = [](uint32_t v) { return float4{ubyte_f<0>(v), ubyte_f<1>(v), ubyte_f<2>(v), ubyte_f<3>(v)}; };
 
     // odd-row ring: slot s holds odd row 2m+1 with m = s (mod 6); y0 % 12 == 0
     float4 ring[6];
-    ring[3] = cvt4(load_row(2 * (y0 - 3) + 1));
-    ring[4] = cvt4(load_row(2 * (y0 - 2) + 1));
-    ring[5] = cvt4(load_row(2 * (y0 - 1) + 1));
-    ring[0] = cvt4(load_row(2 * y0 + 1));
-    ring[1] = cvt4(load_row(2 * (y0 + 1) + 1));
+    ring[3] = cvt4_once(load_row(2 * (y0 - 3) + 1));
+    ring[4] = cvt4_once(load_row(2 * (y0 - 2) + 1));
+    ring[5] = cvt4_once(load_row(2 * (y0 - 1) + 1));
+    ring[0] = cvt4_once(load_row(2 * y0 + 1));
+    ring[1] = cvt4_once(load_row(2 * (y0 + 1) + 1));
     ring[2] = float4{0.f, 0.f, 0.f, 0.f};
 
     for (int yc = y0; yc < y1; yc += kR) {
@@ -247,15 +276,15 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
         }
 #pragma unroll
         for (int u = 0; u < kR; ++u) {
-            ring[(u + 2) % 6] = cvt4(odd[u]);
-            const float4 e = cvt4(even[u]);
+            ring[(u + 2) % 6] = cvt4_once(odd[u]);
+            const float4 e = cvt4_once(even[u]);
             const float4 m5 = ring[(u + 3) % 6], m3 = ring[(u + 4) % 6], m1 = ring[(u + 5) % 6];
             const float4 p1 = ring[u % 6], p3 = ring[(u + 1) % 6], p5 = ring[(u + 2) % 6];
-            const float v0 = c0 * e.x + c1 * (m1.x + p1.x) + c3 * (m3.x + p3.x) + c5 * (m5.x + p5.x);
-            const float v1 = c0 * e.y + c1 * (m1.y + p1.y) + c3 * (m3.y + p3.y) + c5 * (m5.y + p5.y);
-            const float v2 = c0 * e.z + c1 * (m1.z + p1.z) + c3 * (m3.z + p3.z) + c5 * (m5.z + p5.z);
-            const float v3 = c0 * e.w + c1 * (m1.w + p1.w) + c3 * (m3.w + p3.w) + c5 * (m5.w + p5.w);
-            if (tid < G::ND) lds[u * kPitch + tid] = pack4(v0, v1, v2, v3);
+            const uint32_t d = pack4b(tap7(c0, c1, c3, c5, bias, e.x, m1.x, p1.x, m3.x, p3.x, m5.x, p5.x),
+                                      tap7(c0, c1, c3, c5, bias, e.y, m1.y, p1.y, m3.y, p3.y, m5.y, p5.y),
+                                      tap7(c0, c1, c3, c5, bias, e.z, m1.z, p1.z, m3.z, p3.z, m5.z, p5.z),
+                                      tap7(c0, c1, c3, c5, bias, e.w, m1.w, p1.w, m3.w, p3.w, m5.w, p5.w));
+            if (G::ND >= kThreads || tid < G::ND) lds[u * kPitch + tid] = d;
         }
         __syncthreads();
         // ---- horizontal pass: K output pixels per item ----
@@ -277,17 +306,17 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
                     const uint2 *r2 = reinterpret_cast<const uint2 *>(row + W0 * j);
 #pragma unroll
                     for (int q = 0; q < 6; ++q) {
-                        const uint2 d = r2[q];
-                        win[2 * q] = d.x;
-                        win[2 * q + 1] = d.y;
+                        const uint2 dd = r2[q];
+                        win[2 * q] = dd.x;
+                        win[2 * q + 1] = dd.y;
                     }
                     win[12] = row[W0 * j + 12];
                 } else {
                     const uint4 *r4 = reinterpret_cast<const uint4 *>(row + W0 * j);
 #pragma unroll
                     for (int q = 0; q < 3; ++q) {
-                        const uint4 d = r4[q];
-                        win[4 * q] = d.x, win[4 * q + 1] = d.y, win[4 * q + 2] = d.z, win[4 * q + 3] = d.w;
+                        const uint4 dd = r4[q];
+                        win[4 * q] = dd.x, win[4 * q + 1] = dd.y, win[4 * q + 2] = dd.z, win[4 * q + 3] = dd.w;
                     }
                     win[12] = row[W0 * j + 12];
                 }
@@ -296,12 +325,12 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 #pragma unroll
                     for (int c = 0; c < B; ++c) {
                         const int lb = B * t + c + G::OFF0;
-                        const uint32_t d = win[lb >> 2];
+                        const uint32_t dd = win[lb >> 2];
                         switch (lb & 3) {
-                            case 0: px[t][c] = ubyte_f<0>(d); break;
-                            case 1: px[t][c] = ubyte_f<1>(d); break;
-                            case 2: px[t][c] = ubyte_f<2>(d); break;
-                            default: px[t][c] = ubyte_f<3>(d); break;
+                            case 0: px[t][c] = ubyte_once<0>(dd); break;
+                            case 1: px[t][c] = ubyte_once<1>(dd); break;
+                            case 2: px[t][c] = ubyte_once<2>(dd); break;
+                            default: px[t][c] = ubyte_once<3>(dd); break;
                         }
                     }
             } else {
@@ -310,7 +339,11 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
                     const int p = clampi(2 * x - 5 + t, 0, a.w - 1);
                     const int lb = B * (p - px0) + G::OFF0;
 #pragma unroll
-                    for (int c = 0; c < B; ++c) px[t][c] = static_cast<float>(rowb[lb + c]);
+                    for (int c = 0; c < B; ++c) {
+                        float f = static_cast<float>(rowb[lb + c]);
+                        asm("" : "+v"(f));
+                        px[t][c] = f;
+                    }
                 }
             }
             // output pixel k uses px[2k + 5 + o], o in {-5,-3,-1,0,1,3,5}
@@ -320,15 +353,15 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 #pragma unroll
                 for (int c = 0; c < B; ++c) {
                     const int m = 2 * k + 5;
-                    o[k][c] = c0 * px[m][c] + c1 * (px[m - 1][c] + px[m + 1][c]) +
-                              c3 * (px[m - 3][c] + px[m + 3][c]) + c5 * (px[m - 5][c] + px[m + 5][c]);
+                    o[k][c] = tap7(c0, c1, c3, c5, bias, px[m][c], px[m - 1][c], px[m + 1][c], px[m - 3][c],
+                                   px[m + 3][c], px[m - 5][c], px[m + 5][c]);
                 }
             u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
             const bool full = x + K <= a.ow;
             if (B == 3) {
-                const uint32_t d0 = pack4(o[0][0], o[0][1], o[0][2], o[1][0]);
-                const uint32_t d1 = pack4(o[1][1], o[1][2], o[2][0], o[2][1]);
-                const uint32_t d2 = pack4(o[2][2], o[3][0], o[3][1], o[3][2]);
+                const uint32_t d0 = pack4b(o[0][0], o[0][1], o[0][2], o[1][0]);
+                const uint32_t d1 = pack4b(o[1][1], o[1][2], o[2][0], o[2][1]);
+                const uint32_t d2 = pack4b(o[2][2], o[3][0], o[3][1], o[3][2]);
                 if (full && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
                     *reinterpret_cast<uint3 *>(q) = uint3{d0, d1, d2};
                 } else {
@@ -337,8 +370,8 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
                     for (int i = 0; i < nb; ++i) q[i] = static_cast<u8>(dd[i >> 2] >> (8 * (i & 3)));
                 }
             } else {
-                const uint32_t d0 = pack4(o[0][0], o[0][1], o[0][2], o[0][3]);
-                const uint32_t d1 = pack4(o[1][0], o[1][1], o[1][2], o[1][3]);
+                const uint32_t d0 = pack4b(o[0][0], o[0][1], o[0][2], o[0][3]);
+                const uint32_t d1 = pack4b(o[1][0], o[1][1], o[1][2], o[1][3]);
                 uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
                 if (full && (reinterpret_cast<uintptr_t>(q) & 7u) == 0) {
                     *reinterpret_cast<uint2 *>(q) = uint2{d0, d1};
@@ -803,10 +836,11 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     a.n_bands = (a.oh + a.band_rows - 1) / a.band_rows;
     a.in_img = img_bytes(w, h, b);
     a.out_img = img_bytes(a.ow, a.oh, b);
-    a.c0 = c[0];
-    a.c1 = c[1];
-    a.c3 = c[2];
-    a.c5 = c[3];
+    a.c0 = c[0] / 4096.0f;
+    a.c1 = c[1] / 4096.0f;
+    a.c3 = c[2] / 4096.0f;
+    a.c5 = c[3] / 4096.0f;
+    a.bias = 1.0f / 8192.0f;
     const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
     dim3 grid(static_cast<unsigned>(tiles));
