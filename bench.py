@@ -60,14 +60,45 @@ def cpu_baseline(args, sample):
                       f"(reducev+reduceh Lanczos3 2x2), {threads} OpenMP threads, {dt:.2f} s wall"}
 
 
-def main():
-    args = parse()
+def dist_env():
+    """(world, rank, local_rank) from the torchrun environment; gloo group for N > 1.
+    The group only carries the barrier and the max-reduce of the timing: the
+    shards are independent, there is no data-path collective."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    return world, rank, local
+
+
+def timed_region(step, steps, warmup, sync, world):
+    """W untimed warmup steps, then exactly `steps` steps bracketed by barrier +
+    device sync on both sides; returns the MAX wall time over ranks (seconds)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    sync()
+    t = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_env()
     torch.cuda.set_device(local)
     import imaginary_amd as ia
     from imaginary_amd._abi import check, lib
@@ -93,29 +124,22 @@ def main():
         check(lib.mipx_execute_dev(C.byref(plan), n, d_in.data_ptr(), d_out.data_ptr(), None,
                                    d_ws.data_ptr(), wsb, sp), "mipx_execute_dev")
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    count = {"i": 0}
+
+    def timed_step():  # HIP events on the kernel's own stream bracket exactly the K timed steps
+        if count["i"] == 0:
+            ev0.record(stream)
         step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+        count["i"] += 1
+        if count["i"] == args.steps:
+            ev1.record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    wall_max = timed_region(timed_step, args.steps, 0, torch.cuda.synchronize, world)
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel launch per step, on `stream`
-    t = torch.tensor([wall], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
 
     verify = None
     if not args.no_verify and rank == 0:

@@ -231,7 +231,7 @@ __device__ __forceinline__ uint32_t pack4b(float a, float b, float c, float d) {
     return __builtin_amdgcn_cvt_pk_u8_f32(d, 3, v);
 }
 
-template <int B, bool EDGE>
+template <int B, int R, bool PF>
 __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int strip, int band,
                                              uint32_t *lds) {
     using G = R2<B>;
@@ -251,13 +251,21 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
     const int y0 = band * a.band_rows;
     const int y1 = min(y0 + a.band_rows, a.oh);
     const float c0 = a.c0, c1 = a.c1, c3 = a.c3, c5 = a.c5, bias = a.bias;
+    // strip pixels outside the image (COPY edge): LDS pixels [0, nl) copy pixel 0,
+    // [fr, fr_end] copy pixel w-1; filled after each vertical pass
+    const int nl = px0 < 0 ? -px0 : 0;
+    const int x_last = min(x0 + TW, a.ow) - 1;
+    const int fr = a.w - px0;                                   // LDS index of pixel w
+    const int fr_end = min(2 * x_last + 5 - px0, G::NPX - 1);   // last LDS pixel read
+    const int nr = fr_end >= fr ? fr_end - fr + 1 : 0;
+    const bool edge = nl > 0 || nr > 0;
 
     auto load_row = [&](int r) -> uint32_t {
         r = clampi(r, 0, a.h - 1);
         return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * row_bytes, 0));
     };
 
-    // odd-row ring: slot s holds odd row 2m+1 with m = s (mod 6); y0 % 12 == 0
+    // odd-row ring: slot s holds odd row 2m+1 with m = s (mod 6); y0 % 6 == 0
     float4 ring[6];
     ring[3] = cvt4_once(load_row(2 * (y0 - 3) + 1));
     ring[4] = cvt4_once(load_row(2 * (y0 - 2) + 1));
@@ -266,96 +274,108 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
     ring[1] = cvt4_once(load_row(2 * (y0 + 1) + 1));
     ring[2] = float4{0.f, 0.f, 0.f, 0.f};
 
-    for (int yc = y0; yc < y1; yc += kR) {
-        // ---- vertical pass: kR intermediate rows -> LDS (packed uchar) ----
-        uint32_t odd[kR], even[kR];
+    uint32_t odd[R], even[R];
+    if (PF) {
 #pragma unroll
-        for (int u = 0; u < kR; ++u) {
-            odd[u] = load_row(2 * (yc + u + 2) + 1);
-            even[u] = load_row(2 * (yc + u));
+        for (int u = 0; u < R; ++u) {
+            odd[u] = load_row(2 * (y0 + u + 2) + 1);
+            even[u] = load_row(2 * (y0 + u));
         }
+    }
+    int buf = 0;
+    for (int yc = y0; yc < y1; yc += R, buf ^= 1) {
+        uint32_t *L = lds + buf * (R * kPitch);
+        // ---- vertical pass: R intermediate rows -> LDS (packed uchar) ----
+        if (!PF) {
 #pragma unroll
-        for (int u = 0; u < kR; ++u) {
+            for (int u = 0; u < R; ++u) {
+                odd[u] = load_row(2 * (yc + u + 2) + 1);
+                even[u] = load_row(2 * (yc + u));
+            }
+        }
+        const bool more = yc + R < y1;
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
             ring[(u + 2) % 6] = cvt4_once(odd[u]);
             const float4 e = cvt4_once(even[u]);
+            if (PF && more) {  // rotate: this register now fetches the next chunk's row
+                odd[u] = load_row(2 * (yc + R + u + 2) + 1);
+                even[u] = load_row(2 * (yc + R + u));
+            }
             const float4 m5 = ring[(u + 3) % 6], m3 = ring[(u + 4) % 6], m1 = ring[(u + 5) % 6];
             const float4 p1 = ring[u % 6], p3 = ring[(u + 1) % 6], p5 = ring[(u + 2) % 6];
             const uint32_t d = pack4b(tap7(c0, c1, c3, c5, bias, e.x, m1.x, p1.x, m3.x, p3.x, m5.x, p5.x),
                                       tap7(c0, c1, c3, c5, bias, e.y, m1.y, p1.y, m3.y, p3.y, m5.y, p5.y),
                                       tap7(c0, c1, c3, c5, bias, e.z, m1.z, p1.z, m3.z, p3.z, m5.z, p5.z),
                                       tap7(c0, c1, c3, c5, bias, e.w, m1.w, p1.w, m3.w, p3.w, m5.w, p5.w));
-            if (G::ND >= kThreads || tid < G::ND) lds[u * kPitch + tid] = d;
+            if (G::ND >= kThreads || tid < G::ND) L[u * kPitch + tid] = d;
+        }
+        if (edge) {  // replicate the edge pixels (EXTEND_COPY) inside the LDS image
+            __syncthreads();
+            u8 *Lb = reinterpret_cast<u8 *>(L);
+            const int nfill = nl + nr;
+            for (int i = tid; i < R * nfill * B; i += kThreads) {
+                const int u = i / (nfill * B);
+                const int rem = i - u * nfill * B;
+                const int f = rem / B, c = rem - f * B;
+                const int dst = f < nl ? f : fr + (f - nl);
+                const int srcp = f < nl ? nl : fr - 1;
+                Lb[u * kPitch * 4 + B * dst + G::OFF0 + c] = Lb[u * kPitch * 4 + B * srcp + G::OFF0 + c];
+            }
         }
         __syncthreads();
-        // ---- horizontal pass: K output pixels per item ----
+        // ---- horizontal pass: K output pixels per item, one channel at a time ----
         constexpr int items_per_row = TW / K;
-        for (int it = tid; it < kR * items_per_row; it += kThreads) {
+        for (int it = tid; it < R * items_per_row; it += kThreads) {
             const int u = it / items_per_row;
             const int j = it - u * items_per_row;
             const int x = x0 + K * j;
             const int y = yc + u;
             if (y >= a.oh || x >= a.ow) continue;
-            const uint32_t *row = lds + u * kPitch;
-            const u8 *rowb = reinterpret_cast<const u8 *>(row);
-            // px[t][c]: intermediate pixel 2x - 5 + t, channel c (t = 0 .. 2K+8)
-            float px[2 * K + 9][B];
-            if (!EDGE) {
-                constexpr int W0 = (B * 2 * K) / 4;  // window start (dwords) per item
-                uint32_t win[13];
-                if (B == 3) {
-                    const uint2 *r2 = reinterpret_cast<const uint2 *>(row + W0 * j);
+            const uint32_t *row = L + u * kPitch;
+            constexpr int W0 = (B * 2 * K) / 4;  // window start (dwords) per item
+            uint32_t win[13];
+            if (B == 3) {
+                const uint2 *r2 = reinterpret_cast<const uint2 *>(row + W0 * j);
 #pragma unroll
-                    for (int q = 0; q < 6; ++q) {
-                        const uint2 dd = r2[q];
-                        win[2 * q] = dd.x;
-                        win[2 * q + 1] = dd.y;
-                    }
-                    win[12] = row[W0 * j + 12];
-                } else {
-                    const uint4 *r4 = reinterpret_cast<const uint4 *>(row + W0 * j);
-#pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        const uint4 dd = r4[q];
-                        win[4 * q] = dd.x, win[4 * q + 1] = dd.y, win[4 * q + 2] = dd.z, win[4 * q + 3] = dd.w;
-                    }
-                    win[12] = row[W0 * j + 12];
+                for (int q = 0; q < 6; ++q) {
+                    const uint2 dd = r2[q];
+                    win[2 * q] = dd.x;
+                    win[2 * q + 1] = dd.y;
                 }
-#pragma unroll
-                for (int t = 0; t < 2 * K + 9; ++t)
-#pragma unroll
-                    for (int c = 0; c < B; ++c) {
-                        const int lb = B * t + c + G::OFF0;
-                        const uint32_t dd = win[lb >> 2];
-                        switch (lb & 3) {
-                            case 0: px[t][c] = ubyte_once<0>(dd); break;
-                            case 1: px[t][c] = ubyte_once<1>(dd); break;
-                            case 2: px[t][c] = ubyte_once<2>(dd); break;
-                            default: px[t][c] = ubyte_once<3>(dd); break;
-                        }
-                    }
+                win[12] = row[W0 * j + 12];
             } else {
+                const uint4 *r4 = reinterpret_cast<const uint4 *>(row + W0 * j);
 #pragma unroll
-                for (int t = 0; t < 2 * K + 9; ++t) {
-                    const int p = clampi(2 * x - 5 + t, 0, a.w - 1);
-                    const int lb = B * (p - px0) + G::OFF0;
-#pragma unroll
-                    for (int c = 0; c < B; ++c) {
-                        float f = static_cast<float>(rowb[lb + c]);
-                        asm("" : "+v"(f));
-                        px[t][c] = f;
-                    }
+                for (int q = 0; q < 3; ++q) {
+                    const uint4 dd = r4[q];
+                    win[4 * q] = dd.x, win[4 * q + 1] = dd.y, win[4 * q + 2] = dd.z, win[4 * q + 3] = dd.w;
                 }
+                win[12] = row[W0 * j + 12];
             }
-            // output pixel k uses px[2k + 5 + o], o in {-5,-3,-1,0,1,3,5}
             float o[K][B];
 #pragma unroll
-            for (int k = 0; k < K; ++k)
+            for (int c = 0; c < B; ++c) {
+                // px[t]: intermediate pixel 2x - 5 + t of channel c
+                float px[2 * K + 9];
 #pragma unroll
-                for (int c = 0; c < B; ++c) {
-                    const int m = 2 * k + 5;
-                    o[k][c] = tap7(c0, c1, c3, c5, bias, px[m][c], px[m - 1][c], px[m + 1][c], px[m - 3][c],
-                                   px[m + 3][c], px[m - 5][c], px[m + 5][c]);
+                for (int t = 0; t < 2 * K + 9; ++t) {
+                    const int lb = B * t + c + G::OFF0;
+                    const uint32_t dd = win[lb >> 2];
+                    switch (lb & 3) {
+                        case 0: px[t] = ubyte_once<0>(dd); break;
+                        case 1: px[t] = ubyte_once<1>(dd); break;
+                        case 2: px[t] = ubyte_once<2>(dd); break;
+                        default: px[t] = ubyte_once<3>(dd); break;
+                    }
                 }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int m = 2 * k + 5;
+                    o[k][c] = tap7(c0, c1, c3, c5, bias, px[m], px[m - 1], px[m + 1], px[m - 3], px[m + 3],
+                                   px[m - 5], px[m + 5]);
+                }
+            }
             u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
             const bool full = x + K <= a.ow;
             if (B == 3) {
@@ -381,22 +401,24 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
                 }
             }
         }
-        __syncthreads();
+        // double-buffered LDS: the next vertical pass writes the other buffer, whose
+        // readers all finished before this chunk's barrier
     }
 }
 
-template <int B>
+// Variant bits (A/B in one process via MIPX_R2_VARIANT; default = best measured):
+// bit 0: R = 6 (else 12), bit 1: register prefetch of the next chunk.
+template <int B, int VAR>
 __global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
-    __shared__ uint32_t lds[kR * kPitch];
+    constexpr int R = (VAR & 1) ? 6 : 12;
+    constexpr bool PF = (VAR & 2) != 0;
+    __shared__ uint32_t lds[2 * R * kPitch];
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = t % a.n_strips;
     const int rest = t / a.n_strips;
     const int band = rest % a.n_bands;
     const int img = rest / a.n_bands;
-    const int x0 = strip * R2<B>::TW;
-    const bool edge = (2 * x0 - 5 < 0) || (2 * x0 + 2 * R2<B>::TW + 3 > a.w - 1);
-    if (edge) reduce2_tile<B, true>(a, img, strip, band, lds);
-    else reduce2_tile<B, false>(a, img, strip, band, lds);
+    reduce2_tile<B, R, PF>(a, img, strip, band, lds);
 }
 
 // ===========================================================================
@@ -818,6 +840,16 @@ bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
     return shape_ok;
 }
 
+// MIPX_R2_VARIANT overrides the default variant of k_reduce2x2 for A/B runs
+// (scripts/ab_reduce.py); read per launch so one process can interleave them.
+constexpr int kR2Default = 2;  // R = 12 + register prefetch: measured best (profiles/r01/v5_variants_ab.log)
+int reduce2_variant() {
+    const char *e = std::getenv("MIPX_R2_VARIANT");
+    if (!e || !*e) return kR2Default;
+    const int v = std::atoi(e);
+    return (v >= 0 && v <= 3) ? v : kR2Default;
+}
+
 int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_t st) {
     float c[4];
     if (!reduce2_taps(c)) return MIPX_EINVAL;
@@ -844,8 +876,17 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
     dim3 grid(static_cast<unsigned>(tiles));
-    if (b == 3) hipLaunchKernelGGL(k_reduce2x2<3>, grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL(k_reduce2x2<4>, grid, dim3(kThreads), 0, st, a);
+    const int var = reduce2_variant();
+#define MIPX_R2(V)                                                                           \
+    case V:                                                                                  \
+        if (b == 3) hipLaunchKernelGGL((k_reduce2x2<3, V>), grid, dim3(kThreads), 0, st, a); \
+        else hipLaunchKernelGGL((k_reduce2x2<4, V>), grid, dim3(kThreads), 0, st, a);        \
+        break;
+    switch (var) {
+        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3)
+        default: return MIPX_EINVAL;
+    }
+#undef MIPX_R2
     return launch_check("k_reduce2x2");
 }
 
