@@ -60,6 +60,23 @@ def cpu_baseline(args, sample):
                       f"(reducev+reduceh Lanczos3 2x2), {threads} OpenMP threads, {dt:.2f} s wall"}
 
 
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic_v5.json")
+
+
+def pmc_traffic(kernel_name_hint):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes of this kernel
+    (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections calibrated in
+    profiles/r01/calib_*.csv); None when no matching summary exists."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+    except OSError:
+        return None, None
+    if t.get("kernel") != kernel_name_hint:
+        return None, None
+    return t["traffic_bytes"], os.path.relpath(TRAFFIC_JSON, ROOT)
+
+
 def dist_env():
     """(world, rank, local_rank) from the torchrun environment; gloo group for N > 1.
     The group only carries the barrier and the max-reduce of the timing: the
@@ -156,6 +173,8 @@ def main():
         value = images / wall_max
         alg_bytes = n * (in_img + out_img)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        variant = os.environ.get("MIPX_R2_VARIANT", "2")
+        traffic, traffic_src = pmc_traffic(f"k_reduce2x2<3, {variant}>")
         line = {
             "metric": "images/sec (4K RGB->1080p Lanczos3 batch) + achieved HBM GB/s, 1/2/4/8 GPUs",
             "value": round(value, 1),
@@ -174,7 +193,8 @@ def main():
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world} (independent shards)"},
             "achieved_hbm_gbs": round(achieved, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
             "verified_vs_oracle": verify,
         }

@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""bench_configs.py — the other BASELINE.json configs, device-resident, one JSON
+line each (bench.py keeps the headline C2 line).
+
+  C3  /pipeline resize(w=1024) -> crop(768x512) -> blur(sigma=5), 2048^2 RGBA, batch 512
+  C4  smartcrop 256x256 + thumbnail 256x256 + 128^2 RGBA watermark on 12 MP
+      (4000x3000 and 3000x4000 decoded), batch 64
+  C5  mixed request stream (resize/fit/rotate/embed/blur over 1080p/4K/12MP),
+      4096 requests drawn with seed 5, grouped by identical plan
+
+Every config runs the bimg plans produced by mipx_plan_make through
+mipx_execute_dev; one image of each group is checked bit-exact against the
+oracle first.  Algorithmic bytes = inputs + final outputs.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402  (before libmipx: one HIP runtime)
+
+import imaginary_amd as ia  # noqa: E402
+from imaginary_amd._abi import check, lib  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+class Group:
+    """n images sharing one plan, resident on the device."""
+
+    def __init__(self, plan, n, dev, seed, wm=None):
+        self.plan, self.n = plan, n
+        ib = plan.in_w * plan.in_h * plan.in_bands
+        ob = plan.out_w * plan.out_h * plan.out_bands
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        self.x = torch.randint(0, 256, (n, ib), dtype=torch.uint8, device=dev, generator=g)
+        self.y = torch.empty((n, ob), dtype=torch.uint8, device=dev)
+        self.wsb = lib.mipx_workspace_bytes(C.byref(plan), n)
+        self.ws = torch.empty(max(self.wsb, 1), dtype=torch.uint8, device=dev)
+        self.wm = None if wm is None else torch.from_numpy(np.ascontiguousarray(wm)).to(dev)
+        self.in_bytes, self.out_bytes = n * ib, n * ob
+
+    def run(self, sp):
+        check(lib.mipx_execute_dev(C.byref(self.plan), self.n, self.x.data_ptr(), self.y.data_ptr(),
+                                   None if self.wm is None else self.wm.data_ptr(), self.ws.data_ptr(),
+                                   self.wsb, sp), "mipx_execute_dev")
+
+
+def plan_for(opts, w, h, b, typ="png", wm_shape=None):
+    inp = ia.make_input(w, h, b, typ)
+    if wm_shape is not None:
+        inp.wm_h, inp.wm_w, inp.wm_bands = wm_shape
+    return ia.plan_make(ia.make_opts(**opts), inp)
+
+
+def verify(group, ref_opts, wm=None):
+    from oracle import oracle as o
+    p = group.plan
+    e, rp = o.plan(ref_opts, dict(w=p.in_w, h=p.in_h, bands=p.in_bands, type=3,
+                                  **({} if wm is None else dict(wm_w=wm.shape[1], wm_h=wm.shape[0],
+                                                                wm_bands=wm.shape[2]))))
+    assert e == 0
+    src = group.x[0].cpu().numpy().reshape(p.in_h, p.in_w, p.in_bands)
+    got = group.y[0].cpu().numpy().reshape(p.out_h, p.out_w, p.out_bands)
+    return bool(np.array_equal(got, o.execute(rp, src, wm)))
+
+
+def time_groups(run_all, steps, warmup, stream):
+    for _ in range(warmup):
+        run_all()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        run_all()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, e0.elapsed_time(e1) / steps
+
+
+def line(name, workload, images, wall_s, dev_ms, alg_bytes, verified, extra=None):
+    d = {"config": name, "workload": workload, "images_per_sec": round(images / wall_s, 1),
+         "ms_per_step": round(wall_s * 1e3, 3), "device_ms_per_step": round(dev_ms, 3),
+         "achieved_gbs": round(alg_bytes / (dev_ms * 1e-3) / 1e9, 1),
+         "hbm_frac": round(alg_bytes / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+         "alg_bytes_per_step": alg_bytes, "verified_vs_oracle": verified}
+    if extra:
+        d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def c3(args, dev, sp, stream):
+    n = args.c3_batch
+    stages = [("resize", dict(width=1024, embed=1)), ("crop", dict(width=768, height=512, crop=1)),
+              ("blur", dict(sigma=5.0))]
+    groups, w, h = [], 2048, 2048
+    for i, (name, opts) in enumerate(stages):
+        p = plan_for(opts, w, h, 4)
+        groups.append((Group(p, n, dev, 3 + i), opts))
+        w, h = p.out_w, p.out_h
+
+    def run_all():  # PNG intermediates are lossless: stages chain on the device
+        for gi, (g, _) in enumerate(groups):
+            if gi > 0:
+                g.x = groups[gi - 1][0].y
+            g.run(sp)
+
+    run_all()
+    torch.cuda.synchronize()
+    ok = all(verify(g, opts) for g, opts in groups)
+    wall, dev_ms = time_groups(run_all, args.steps, args.warmup, stream)
+    alg = groups[0][0].in_bytes + groups[-1][0].out_bytes
+    line("C3", "pipeline resize(w=1024)+crop(768x512)+blur(sigma=5), 2048^2 RGBA", n, wall, dev_ms, alg, ok,
+         {"batch": n, "stages": [g.plan.describe() for g, _ in groups]})
+
+
+def c4(args, dev, sp, stream):
+    n = args.c4_batch // 2
+    rng = np.random.default_rng(4)
+    wm = rng.integers(0, 256, (128, 128, 4), dtype=np.uint8)
+    groups = []
+    for (w, h) in ((4000, 3000), (3000, 4000)):
+        for opts in (dict(width=256, height=256, crop=1, gravity=5),      # SmartCrop
+                     dict(width=256, height=256, wm_enable=1, wm_left=16, wm_top=16, wm_opacity=0.5)):
+            p = plan_for(opts, w, h, 3, wm_shape=(128, 128, 4) if opts.get("wm_enable") else None)
+            groups.append((Group(p, n, dev, 4 + len(groups), wm if opts.get("wm_enable") else None), opts))
+
+    def run_all():
+        for g, _ in groups:
+            g.run(sp)
+
+    run_all()
+    torch.cuda.synchronize()
+    ok = all(verify(g, opts, wm if opts.get("wm_enable") else None) for g, opts in groups)
+    wall, dev_ms = time_groups(run_all, args.steps, args.warmup, stream)
+    alg = sum(g.in_bytes + g.out_bytes + (wm.nbytes if g.wm is not None else 0) for g, _ in groups)
+    line("C4", "smartcrop 256^2 + thumbnail 256^2 + watermark, 12 MP 4000x3000 / 3000x4000",
+         2 * n * 2, wall, dev_ms, alg, ok, {"requests": 4 * n, "plans": [g.plan.describe() for g, _ in groups]})
+
+
+def c5_requests(count, seed=5):
+    r = np.random.default_rng(seed)
+    sizes = [(1920, 1080), (3840, 2160), (4000, 3000)]
+    reqs = []
+    for _ in range(count):
+        w, h = sizes[r.integers(0, 3)]
+        u = r.random()
+        if u < 0.40:
+            opts = dict(width=int(r.choice([300, 640, 1280])), embed=1)
+        elif u < 0.60:
+            fw, fh = ia.fit_dimension(w, h, 800, 800)
+            opts = dict(width=fw, height=fh, embed=1)
+        elif u < 0.75:
+            opts = dict(rotate=int(r.choice([90, 180, 270])))
+        elif u < 0.90:
+            s = max(w, h)
+            opts = dict(width=s, height=s, embed=1, extend=int(r.choice([0, 1, 2, 3, 4, 5])))
+        else:
+            opts = dict(sigma=float(r.choice([1.0, 3.0, 5.0])))
+        reqs.append(((w, h), opts))
+    return reqs
+
+
+def c5(args, dev, sp, stream):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    reqs = c5_requests(args.c5_requests)[rank::world]  # shard requests across ranks
+    buckets = {}
+    for (w, h), opts in reqs:
+        key = (w, h, json.dumps(opts, sort_keys=True))
+        buckets.setdefault(key, [0, opts, w, h])[0] += 1
+    groups = []
+    for (w, h, _), (cnt, opts, _, _) in sorted(buckets.items()):
+        groups.append((Group(plan_for(opts, w, h, 3), cnt, dev, 5 + len(groups)), opts))
+
+    def run_all():
+        for g, _ in groups:
+            g.run(sp)
+
+    run_all()
+    torch.cuda.synchronize()
+    ok = all(verify(g, opts) for g, opts in groups[:: max(1, len(groups) // 8)])
+    wall, dev_ms = time_groups(run_all, args.steps, args.warmup, stream)
+    alg = sum(g.in_bytes + g.out_bytes for g, _ in groups)
+    line("C5", f"mixed stream {len(reqs)} requests (rank {rank}/{world}), {len(groups)} plan groups",
+         len(reqs), wall, dev_ms, alg, ok, {"groups": len(groups)})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C3,C4,C5")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--c3-batch", type=int, default=512)
+    ap.add_argument("--c4-batch", type=int, default=64)
+    ap.add_argument("--c5-requests", type=int, default=512 * int(os.environ.get("WORLD_SIZE", "1")),
+                    help="total requests, sharded across ranks (4096 at 8 GPUs)")
+    args = ap.parse_args()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    check(lib.mipx_set_device(local), "mipx_set_device")
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    sp = C.c_void_p(stream.cuda_stream)
+    for c in args.configs.split(","):
+        {"C3": c3, "C4": c4, "C5": c5}[c](args, dev, sp, stream)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,266 @@
+// k_geometry.hip — libvips vips_embed / vips_extract_area / vips_rot /
+// vips_flip on gfx950: bit-exact byte moves.
+//
+//  * k_remap<B, EMBED|FLIPH|FLIPV|ROT180>: one lane per output pixel; embed
+//    implements every VipsExtend mode (embed.c: COPY clamps, REPEAT tiles with
+//    period W, MIRROR tiles the 2x2 [in, flip(in)] mosaic with period 2W,
+//    BLACK / WHITE / BACKGROUND fill).  With `origins` set it is an extract at a
+//    device-computed (left, top) — smartcrop needs no host round trip.
+//  * k_rot90t<B, CW>: 90 / 270 through a 32 x 32 pixel LDS tile, so both the
+//    read and the write side are row-coalesced.
+//  * k_extract_rows: row copies, dword lanes when rows and offset allow.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "device_common.h"
+
+namespace mipx {
+namespace {
+
+using namespace dev;
+
+enum RemapKind { kEmbed = 0, kFlipH, kFlipV, kRot180 };
+
+struct RemapArgs {
+    const u8 *in;
+    u8 *out;
+    int w, h, ow, oh;
+    int x, y, extend;
+    u8 fill[4];
+    long long in_img, out_img;
+    const int *origins;  // extract with per-image (left, top) from the device (smartcrop)
+};
+
+__device__ __forceinline__ uint32_t load_px(const u8 *p, int B) {
+    uint32_t v = p[0];
+    if (B > 1) v |= static_cast<uint32_t>(p[1]) << 8;
+    if (B > 2) v |= static_cast<uint32_t>(p[2]) << 16;
+    if (B > 3) v |= static_cast<uint32_t>(p[3]) << 24;
+    return v;
+}
+__device__ __forceinline__ void store_px(u8 *q, uint32_t v, int B) {
+    q[0] = static_cast<u8>(v);
+    if (B > 1) q[1] = static_cast<u8>(v >> 8);
+    if (B > 2) q[2] = static_cast<u8>(v >> 16);
+    if (B > 3) q[3] = static_cast<u8>(v >> 24);
+}
+
+template <int B, int KIND>
+__global__ void __launch_bounds__(256) k_remap(RemapArgs a) {
+    const int X = blockIdx.x * blockDim.x + threadIdx.x;
+    const int Y = blockIdx.y;
+    const int img = blockIdx.z;
+    if (X >= a.ow) return;
+    int sx = X, sy = Y;
+    bool use_fill = false;
+    if (KIND == kEmbed) {
+        int ox = a.x, oy = a.y;
+        if (a.origins) {  // extract at a device-computed origin == embed at (-l, -t)
+            ox = -a.origins[2 * img];
+            oy = -a.origins[2 * img + 1];
+        }
+        sx = X - ox;
+        sy = Y - oy;
+        if (sx < 0 || sx >= a.w || sy < 0 || sy >= a.h) {
+            switch (a.extend) {
+                case MIPX_EXTEND_COPY:
+                    sx = clampi(sx, 0, a.w - 1);
+                    sy = clampi(sy, 0, a.h - 1);
+                    break;
+                case MIPX_EXTEND_REPEAT:
+                    sx = pmod(sx, a.w);
+                    sy = pmod(sy, a.h);
+                    break;
+                case MIPX_EXTEND_MIRROR: {
+                    const int u = pmod(sx, 2 * a.w), v = pmod(sy, 2 * a.h);
+                    sx = u < a.w ? u : 2 * a.w - 1 - u;
+                    sy = v < a.h ? v : 2 * a.h - 1 - v;
+                    break;
+                }
+                default: use_fill = true;
+            }
+        }
+    } else if (KIND == kFlipH) {
+        sx = a.w - 1 - X;
+    } else if (KIND == kFlipV) {
+        sy = a.h - 1 - Y;
+    } else {  // kRot180
+        sx = a.w - 1 - X;
+        sy = a.h - 1 - Y;
+    }
+    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(Y) * a.ow + X) * B;
+    uint32_t v;
+    if (use_fill) {
+        v = a.fill[0] | (a.fill[1] << 8) | (a.fill[2] << 16) | (static_cast<uint32_t>(a.fill[3]) << 24);
+    } else {
+        const u8 *p = a.in + img * a.in_img + (static_cast<size_t>(sy) * a.w + sx) * B;
+        v = B == 4 ? *reinterpret_cast<const uint32_t *>(p) : load_px(p, B);
+    }
+    if (B == 4) *reinterpret_cast<uint32_t *>(q) = v;
+    else store_px(q, v, B);
+}
+
+// 90 (CW) / 270 rotation: out(x, y) = in(y, H-1-x) for CW, in(W-1-y, x) for CCW.
+// A block moves one 32 x 32 input tile; rows of the tile are read and rows of
+// the transposed tile written, each coalesced.
+template <int B, bool CW>
+__global__ void __launch_bounds__(256) k_rot90t(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
+                                                 long long img_bytes_) {
+    __shared__ uint32_t tile[32][33];
+    const int img = blockIdx.z;
+    const int tx0 = blockIdx.x * 32, ty0 = blockIdx.y * 32;  // input tile origin
+    const u8 *src = in + img * img_bytes_;
+    u8 *dst = out + img * img_bytes_;
+    for (int i = threadIdx.x; i < 32 * 32; i += 256) {
+        const int r = i >> 5, c = i & 31;
+        const int x = tx0 + c, y = ty0 + r;
+        if (x < w && y < h) {
+            const u8 *p = src + (static_cast<size_t>(y) * w + x) * B;
+            tile[r][c] = B == 4 ? *reinterpret_cast<const uint32_t *>(p) : load_px(p, B);
+        }
+    }
+    __syncthreads();
+    // output is h wide, w tall; output row X_out = input column
+    for (int i = threadIdx.x; i < 32 * 32; i += 256) {
+        const int r = i >> 5, c = i & 31;  // r: output row within tile, c: output column within tile
+        int ox, oy, ix, iy;
+        if (CW) {   // out(ox, oy) = in(x = oy, y = h-1-ox)
+            oy = tx0 + r;
+            ix = oy;
+            iy = ty0 + (31 - c);
+            ox = h - 1 - iy;
+        } else {    // out(ox, oy) = in(x = w-1-oy, y = ox)
+            ix = tx0 + (31 - r);
+            oy = w - 1 - ix;
+            iy = ty0 + c;
+            ox = iy;
+        }
+        if (ix < w && iy < h && ix >= tx0 && iy >= ty0) {
+            const uint32_t v = tile[iy - ty0][ix - tx0];
+            u8 *q = dst + (static_cast<size_t>(oy) * h + ox) * B;
+            if (B == 4) *reinterpret_cast<uint32_t *>(q) = v;
+            else store_px(q, v, B);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_extract_rows(const u8 *__restrict__ in, u8 *__restrict__ out,
+                                                      int in_row_bytes, int out_row_bytes, int left_bytes, int top,
+                                                      long long in_img, long long out_img, int dword) {
+    const int y = blockIdx.y;
+    const int img = blockIdx.z;
+    const u8 *src = in + img * in_img + static_cast<size_t>(top + y) * in_row_bytes + left_bytes;
+    u8 *dst = out + img * out_img + static_cast<size_t>(y) * out_row_bytes;
+    if (dword) {
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
+        uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+        for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < out_row_bytes / 4; j += gridDim.x * blockDim.x)
+            d[j] = s[j];
+    } else {
+        for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < out_row_bytes; j += gridDim.x * blockDim.x)
+            dst[j] = src[j];
+    }
+}
+
+int remap_launch(int kind, const RemapArgs &a, int b, int n, hipStream_t st) {
+    dim3 grid((a.ow + 255) / 256, a.oh, n);
+#define MIPX_REMAP(KIND) \
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_remap<B_, KIND>), grid, dim3(256), 0, st, a))
+    switch (kind) {
+        case kEmbed: MIPX_REMAP(kEmbed); break;
+        case kFlipH: MIPX_REMAP(kFlipH); break;
+        case kFlipV: MIPX_REMAP(kFlipV); break;
+        case kRot180: MIPX_REMAP(kRot180); break;
+        default: return MIPX_EINVAL;
+    }
+#undef MIPX_REMAP
+    return launch_check("k_remap");
+}
+
+bool aligned4(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
+
+}  // namespace
+
+int embed_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x, int y, int ow, int oh, int extend,
+                 const int *bg, const int *d_origins, hipStream_t st) {
+    RemapArgs a{};
+    a.in = in;
+    a.out = out;
+    a.w = w;
+    a.h = h;
+    a.ow = ow;
+    a.oh = oh;
+    a.x = x;
+    a.y = y;
+    if (extend == MIPX_EXTEND_LAST) extend = MIPX_EXTEND_BACKGROUND;  // bimg vipsEmbed: extend > 5
+    a.extend = extend;
+    for (int z = 0; z < 4; ++z) a.fill[z] = 0;
+    if (extend == MIPX_EXTEND_WHITE)
+        for (int z = 0; z < 4; ++z) a.fill[z] = 255;
+    if (extend == MIPX_EXTEND_BACKGROUND) {
+        int b3[3] = {0, 0, 0};
+        if (bg) b3[0] = bg[0], b3[1] = bg[1], b3[2] = bg[2];
+        for (int z = 0; z < 4; ++z) a.fill[z] = static_cast<uint8_t>(std::min(255, std::max(0, b3[z < 3 ? z : 2])));
+        if (b == 4) a.fill[3] = 255;
+        if (b <= 2) a.fill[0] = static_cast<uint8_t>(std::min(255, std::max(0, b3[0]))), a.fill[1] = 255;
+    }
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = img_bytes(ow, oh, b);
+    a.origins = d_origins;
+    if (b == 4 && !(aligned4(in) && aligned4(out))) return MIPX_EINVAL;
+    return remap_launch(kEmbed, a, b, n, st);
+}
+
+int flip_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int vertical, hipStream_t st) {
+    RemapArgs a{};
+    a.in = in;
+    a.out = out;
+    a.w = w;
+    a.h = h;
+    a.ow = w;
+    a.oh = h;
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = a.in_img;
+    if (b == 4 && !(aligned4(in) && aligned4(out))) return MIPX_EINVAL;
+    return remap_launch(vertical ? kFlipV : kFlipH, a, b, n, st);
+}
+
+int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hipStream_t st) {
+    angle = ((angle % 360) + 360) % 360;
+    if (b == 4 && !(aligned4(in) && aligned4(out))) return MIPX_EINVAL;
+    if (angle == 0) {
+        MIPX_HIP(hipMemcpyAsync(out, in, static_cast<size_t>(img_bytes(w, h, b)) * n, hipMemcpyDeviceToDevice, st));
+        return MIPX_OK;
+    }
+    if (angle == 180) {
+        RemapArgs a{};
+        a.in = in;
+        a.out = out;
+        a.w = a.ow = w;
+        a.h = a.oh = h;
+        a.in_img = a.out_img = img_bytes(w, h, b);
+        return remap_launch(kRot180, a, b, n, st);
+    }
+    if (angle != 90 && angle != 270) return MIPX_EINVAL;
+    dim3 grid((w + 31) / 32, (h + 31) / 32, n);
+    const long long ib = img_bytes(w, h, b);
+    if (angle == 90) {
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90t<B_, true>), grid, dim3(256), 0, st, in, out, w, h, ib));
+    } else {
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90t<B_, false>), grid, dim3(256), 0, st, in, out, w, h, ib));
+    }
+    return launch_check("k_rot90t");
+}
+
+int extract_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, int top, int ow, int oh,
+                   hipStream_t st) {
+    const int in_row = w * b, out_row = ow * b, lb = left * b;
+    const int dword = (in_row % 4 == 0) && (out_row % 4 == 0) && (lb % 4 == 0) && aligned4(in) && aligned4(out);
+    dim3 grid(std::max(1, std::min((out_row / (dword ? 4 : 1) + 255) / 256, 64)), oh, n);
+    hipLaunchKernelGGL(k_extract_rows, grid, dim3(256), 0, st, in, out, in_row, out_row, lb, top, img_bytes(w, h, b),
+                       img_bytes(ow, oh, b), dword);
+    return launch_check("k_extract_rows");
+}
+
+}  // namespace mipx

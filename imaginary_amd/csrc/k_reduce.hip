@@ -1,0 +1,607 @@
+// k_reduce.hip — libvips vips_reduce (Lanczos3) on gfx950.
+//
+// reduce.c runs reducev then reduceh with a uchar intermediate; every tap is a
+// 12-bit integer (matrixi, truncated) and each uchar result is
+// (sum + 2048) >> 12 clipped (reduceh.cpp / reducev.cpp / templates.h,
+// restated in oracle/vips_ref.c).  Sums stay exact in fp32 (< 2^24), so the
+// kernels are bit-identical to the integer C path.
+//
+//  * k_reduce2x2     fused reducev -> reduceh for shrink 2 x 2 (north star C2)
+//  * k_reducev_gen   any vshrink: per output row one phase (uniform per block)
+//  * k_reduceh_lds   any hshrink: input row span and tap table staged in LDS
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <vector>
+
+#include "device_common.h"
+
+namespace mipx {
+namespace {
+
+using namespace dev;
+
+// ===========================================================================
+// generic vertical pass: a block = 256 dword columns of one output row (the
+// 1D grid is XCD-remapped so consecutive output rows of one image, which
+// share input rows, run on one XCD); taps are uniform (SGPR) per block.
+// ===========================================================================
+struct RedV {
+    const u8 *in;
+    u8 *out;
+    int row_bytes, h, oh, col_blocks, pad, taps;
+    double shrink;
+    const float *tab;
+    long long in_img, out_img;
+};
+
+template <bool DWORD>
+__global__ void __launch_bounds__(256) k_reducev_gen(RedV a) {
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int cb = t % a.col_blocks;
+    const int rest = t / a.col_blocks;
+    const int y = rest % a.oh;
+    const int img = rest / a.oh;
+    const int j = (cb * 256 + threadIdx.x) * 4;
+    if (j >= a.row_bytes) return;
+    const double Y = y * a.shrink;
+    const int iy = static_cast<int>(Y);
+    const int ty = ((static_cast<int>(Y * 256.0) & 255) + 1) >> 1;
+    const float *c = a.tab + ty * a.taps;
+    const u8 *src = a.in + img * a.in_img;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int nb = min(4, a.row_bytes - j);
+    if (DWORD) {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
+        for (int i = 0; i < a.taps; ++i) {
+            const int r = clampi(iy + i - a.pad, 0, a.h - 1);
+            const uint32_t v = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, j, r * a.row_bytes, 0));
+            const float ci = c[i];
+            acc[0] = __builtin_fmaf(ci, ubyte_f<0>(v), acc[0]);
+            acc[1] = __builtin_fmaf(ci, ubyte_f<1>(v), acc[1]);
+            acc[2] = __builtin_fmaf(ci, ubyte_f<2>(v), acc[2]);
+            acc[3] = __builtin_fmaf(ci, ubyte_f<3>(v), acc[3]);
+        }
+        uint32_t o = fixed_round_u(acc[0]) | (fixed_round_u(acc[1]) << 8) | (fixed_round_u(acc[2]) << 16) |
+                     (fixed_round_u(acc[3]) << 24);
+        *reinterpret_cast<uint32_t *>(a.out + img * a.out_img + static_cast<size_t>(y) * a.row_bytes + j) = o;
+    } else {
+        for (int i = 0; i < a.taps; ++i) {
+            const int r = clampi(iy + i - a.pad, 0, a.h - 1);
+            const u8 *p = src + static_cast<size_t>(r) * a.row_bytes + j;
+            const float ci = c[i];
+            for (int k = 0; k < nb; ++k) acc[k] = __builtin_fmaf(ci, static_cast<float>(p[k]), acc[k]);
+        }
+        u8 *q = a.out + img * a.out_img + static_cast<size_t>(y) * a.row_bytes + j;
+        for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(fixed_round_u(acc[k]));
+    }
+}
+
+// ===========================================================================
+// generic horizontal pass: a block = 256 output pixels of one row.  The input
+// pixels the block's taps touch (COPY-clamped) are staged once in LDS as one
+// packed u32 per pixel, the 129-phase tap table beside them; each lane then
+// reads its taps from LDS.
+// ===========================================================================
+struct RedH {
+    const u8 *in;
+    u8 *out;
+    int w, h, ow, x_blocks, pad, taps, span_max;
+    double shrink;
+    const float *tab;
+    long long in_img, out_img;
+};
+
+template <int B>
+__global__ void __launch_bounds__(256) k_reduceh_lds(RedH a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    float *ctab = reinterpret_cast<float *>(smem);
+    uint32_t *spx = smem + (kTransformScale + 1) * a.taps;
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int y = rest % a.h;
+    const int img = rest / a.h;
+    const int x0 = xb * 256;
+    const int x_last = min(x0 + 255, a.ow - 1);
+    const int lo = static_cast<int>(x0 * a.shrink) - a.pad;
+    const int hi = static_cast<int>(x_last * a.shrink) + a.taps - 1 - a.pad;
+    const int span = hi - lo + 1;
+    for (int i = threadIdx.x; i < (kTransformScale + 1) * a.taps; i += 256) ctab[i] = a.tab[i];
+    const u8 *row = a.in + img * a.in_img + static_cast<size_t>(y) * a.w * B;
+    for (int p = threadIdx.x; p < span; p += 256) {
+        const u8 *s = row + clampi(lo + p, 0, a.w - 1) * B;
+        uint32_t v;
+        if (B == 4) {
+            v = *reinterpret_cast<const uint32_t *>(s);
+        } else {
+            v = s[0];
+            if (B > 1) v |= static_cast<uint32_t>(s[1]) << 8;
+            if (B > 2) v |= static_cast<uint32_t>(s[2]) << 16;
+        }
+        spx[p] = v;
+    }
+    __syncthreads();
+    const int x = x0 + threadIdx.x;
+    if (x > x_last) return;
+    const double X = x * a.shrink;
+    const int ix = static_cast<int>(X);
+    const int tx = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
+    const float *c = ctab + tx * a.taps;
+    const uint32_t *sp = spx + (ix - a.pad - lo);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < a.taps; ++i) {
+        const uint32_t v = sp[i];
+        const float ci = c[i];
+        acc[0] = __builtin_fmaf(ci, ubyte_f<0>(v), acc[0]);
+        if (B > 1) acc[1] = __builtin_fmaf(ci, ubyte_f<1>(v), acc[1]);
+        if (B > 2) acc[2] = __builtin_fmaf(ci, ubyte_f<2>(v), acc[2]);
+        if (B > 3) acc[3] = __builtin_fmaf(ci, ubyte_f<3>(v), acc[3]);
+    }
+    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
+    if (B == 4) {
+        *reinterpret_cast<uint32_t *>(q) = fixed_round_u(acc[0]) | (fixed_round_u(acc[1]) << 8) |
+                                           (fixed_round_u(acc[2]) << 16) | (fixed_round_u(acc[3]) << 24);
+    } else {
+#pragma unroll
+        for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_u(acc[z]));
+    }
+}
+
+// horizontal pass without LDS staging, for shrinks whose span exceeds the LDS
+// budget: taps gathered through L1
+template <int B>
+__global__ void __launch_bounds__(256) k_reduceh_gather(RedH a) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int img = blockIdx.z;
+    if (x >= a.ow) return;
+    const double X = x * a.shrink;
+    const int ix = static_cast<int>(X);
+    const int tx = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
+    const float *c = a.tab + tx * a.taps;
+    const u8 *row = a.in + img * a.in_img + static_cast<size_t>(y) * a.w * B;
+    float acc[B];
+#pragma unroll
+    for (int z = 0; z < B; ++z) acc[z] = 0.f;
+    for (int i = 0; i < a.taps; ++i) {
+        const u8 *p = row + clampi(ix + i - a.pad, 0, a.w - 1) * B;
+        const float ci = c[i];
+#pragma unroll
+        for (int z = 0; z < B; ++z) acc[z] = __builtin_fmaf(ci, static_cast<float>(p[z]), acc[z]);
+    }
+    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
+#pragma unroll
+    for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_u(acc[z]));
+}
+
+// ===========================================================================
+// Lanczos3 reduce by exactly 2 x 2, fused reducev -> reduceh (the north-star
+// kernel: 4K -> 1080p).
+//
+// At shrink 2 with the corner convention every output samples phase 0, whose
+// 13-tap mask has zeros at the odd integer positions of the Lanczos lobe and is
+// symmetric, so output o = c0 * p[2o] + c1 * (p[2o-1] + p[2o+1])
+//                      + c3 * (p[2o-3] + p[2o+3]) + c5 * (p[2o-5] + p[2o+5]).
+// The host verifies that shape on the actual integer table before choosing
+// this kernel, so the arithmetic is exactly libvips' 13-tap sum.
+//
+// One workgroup = a strip of TW output pixels x a band of rows.
+//  * Vertical pass: lane t owns dword t of the strip's input bytes (channel
+//    agnostic) and walks down the band with the six odd rows of the current
+//    window in a static register ring (slot = odd-row index mod 6, unrolled
+//    by 12); each input byte is loaded and converted once.  The rounded uchar
+//    intermediate (libvips materialises it between reducev and reduceh) is
+//    packed back to a dword and written to LDS in input byte order: one
+//    conflict-free ds_write_b32 per lane and row.
+//  * Horizontal pass: an item is K output pixels of one row; it reads the
+//    13-dword byte window it needs (ds_read_b64: lane stride 6 dwords for RGB,
+//    conflict-free; ds_read_b128 for RGBA, stride 4 dwords), converts each
+//    byte once and stores 12 (RGB) / 8 (RGBA) contiguous output bytes.
+// The intermediate never touches HBM, and the LDS image is 7.5 KB per
+// workgroup, so occupancy is set by registers, not LDS.
+// ===========================================================================
+constexpr int kR = 12;           // output rows per LDS chunk (2 ring periods)
+constexpr int kThreads = 128;
+constexpr int kPitch = 160;      // LDS dwords per intermediate row (== 32 mod 64)
+
+template <int B>
+struct R2 {
+    static constexpr int TW = B == 3 ? 80 : 56;     // output pixels per strip
+    static constexpr int NPX = 2 * TW + 9;           // intermediate px 2x0-5 .. 2x0+2TW+3
+    static constexpr int K = B == 3 ? 4 : 2;         // output pixels per horizontal item
+    static constexpr int OFF0 = B == 3 ? 1 : 0;      // B*(2x0-5) - floor4(B*(2x0-5))
+    static constexpr int ND = (B * NPX + OFF0 + 3) / 4;  // dwords per row
+    static_assert(ND <= kThreads && ND <= kPitch, "strip too wide");
+    static_assert((B * 2 * K) % 8 == 0, "window start must be 8-byte aligned");
+};
+
+struct Reduce2Args {
+    const u8 *in;
+    u8 *out;
+    int w, h, ow, oh;
+    int n_strips, n_bands, band_rows;  // band_rows multiple of kR
+    long long in_img, out_img;
+    // taps pre-scaled by 1/4096 (exact: powers of two); the bias 2^-13 turns the
+    // exact chain into RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5) at the cvt
+    float c0, c1, c3, c5, bias;
+    int remap;       // XCD-aware tile order (MIPX_R2_REMAP=0 disables, for A/B)
+    int band_major;  // tile order inside an XCD range (MIPX_R2_ORDER=1: bands fastest)
+};
+
+__device__ __forceinline__ float4 cvt4_once(uint32_t v) {
+    return float4{ubyte_once<0>(v), ubyte_once<1>(v), ubyte_once<2>(v), ubyte_once<3>(v)};
+}
+
+// c0 e + c1 (m1 + p1) + c3 (m3 + p3) + c5 (m5 + p5) with pre-scaled taps and the
+// bias: every partial is exact on a 1/8192 grid below 2^9, so the result is
+// exactly sum/4096 + 2^-13
+__device__ __forceinline__ float tap7(float c0, float c1, float c3, float c5, float bias, float e, float m1,
+                                      float p1, float m3, float p3, float m5, float p5) {
+    float acc = __builtin_fmaf(c0, e, bias);
+    acc = __builtin_fmaf(c1, m1 + p1, acc);
+    acc = __builtin_fmaf(c3, m3 + p3, acc);
+    return __builtin_fmaf(c5, m5 + p5, acc);
+}
+// v_cvt_pk_u8_f32 rounds to nearest-even and saturates to 0..255; on the
+// 1/4096 grid RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5) (no ties occur)
+__device__ __forceinline__ uint32_t pack4b(float a, float b, float c, float d) {
+    uint32_t v = __builtin_amdgcn_cvt_pk_u8_f32(a, 0, 0u);
+    v = __builtin_amdgcn_cvt_pk_u8_f32(b, 1, v);
+    v = __builtin_amdgcn_cvt_pk_u8_f32(c, 2, v);
+    return __builtin_amdgcn_cvt_pk_u8_f32(d, 3, v);
+}
+
+template <int B, int R, bool PF>
+__device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int strip, int band,
+                                             uint32_t *lds) {
+    using G = R2<B>;
+    constexpr int TW = G::TW, K = G::K;
+    const int tid = threadIdx.x;
+    const int x0 = strip * TW;
+    const int row_bytes = a.w * B;
+    const int px0 = 2 * x0 - 5;          // first intermediate pixel of the strip
+    const int base = (B * px0) & ~3;     // floor to a dword (two's complement)
+    const int byte0 = base + 4 * tid;
+    const bool vlane = tid < G::ND && byte0 >= 0 && byte0 + 4 <= row_bytes;
+    // raw buffer loads: per-lane byte offset in voffset, row offset in soffset;
+    // lanes outside the row get an out-of-range voffset and read 0
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<u8 *>(a.in + img * a.in_img), 0, static_cast<int>(a.in_img), 0x00020000);
+    const uint32_t voff = vlane ? static_cast<uint32_t>(byte0) : 0x80000000u;
+    const int y0 = band * a.band_rows;
+    const int y1 = min(y0 + a.band_rows, a.oh);
+    const float c0 = a.c0, c1 = a.c1, c3 = a.c3, c5 = a.c5, bias = a.bias;
+    // strip pixels outside the image (COPY edge): LDS pixels [0, nl) copy pixel 0,
+    // [fr, fr_end] copy pixel w-1; filled after each vertical pass
+    const int nl = px0 < 0 ? -px0 : 0;
+    const int x_last = min(x0 + TW, a.ow) - 1;
+    const int fr = a.w - px0;                                   // LDS index of pixel w
+    const int fr_end = min(2 * x_last + 5 - px0, G::NPX - 1);   // last LDS pixel read
+    const int nr = fr_end >= fr ? fr_end - fr + 1 : 0;
+    const bool edge = nl > 0 || nr > 0;
+
+    auto load_row = [&](int r) -> uint32_t {
+        r = clampi(r, 0, a.h - 1);
+        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * row_bytes, 0));
+    };
+
+    // odd-row ring: slot s holds odd row 2m+1 with m = s (mod 6); y0 % 6 == 0
+    float4 ring[6];
+    ring[3] = cvt4_once(load_row(2 * (y0 - 3) + 1));
+    ring[4] = cvt4_once(load_row(2 * (y0 - 2) + 1));
+    ring[5] = cvt4_once(load_row(2 * (y0 - 1) + 1));
+    ring[0] = cvt4_once(load_row(2 * y0 + 1));
+    ring[1] = cvt4_once(load_row(2 * (y0 + 1) + 1));
+    ring[2] = float4{0.f, 0.f, 0.f, 0.f};
+
+    uint32_t odd[R], even[R];
+    if (PF) {
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            odd[u] = load_row(2 * (y0 + u + 2) + 1);
+            even[u] = load_row(2 * (y0 + u));
+        }
+    }
+    int buf = 0;
+    for (int yc = y0; yc < y1; yc += R, buf ^= 1) {
+        uint32_t *L = lds + buf * (R * kPitch);
+        // ---- vertical pass: R intermediate rows -> LDS (packed uchar) ----
+        if (!PF) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                odd[u] = load_row(2 * (yc + u + 2) + 1);
+                even[u] = load_row(2 * (yc + u));
+            }
+        }
+        const bool more = yc + R < y1;
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            ring[(u + 2) % 6] = cvt4_once(odd[u]);
+            const float4 e = cvt4_once(even[u]);
+            if (PF && more) {  // rotate: this register now fetches the next chunk's row
+                odd[u] = load_row(2 * (yc + R + u + 2) + 1);
+                even[u] = load_row(2 * (yc + R + u));
+            }
+            const float4 m5 = ring[(u + 3) % 6], m3 = ring[(u + 4) % 6], m1 = ring[(u + 5) % 6];
+            const float4 p1 = ring[u % 6], p3 = ring[(u + 1) % 6], p5 = ring[(u + 2) % 6];
+            const uint32_t d = pack4b(tap7(c0, c1, c3, c5, bias, e.x, m1.x, p1.x, m3.x, p3.x, m5.x, p5.x),
+                                      tap7(c0, c1, c3, c5, bias, e.y, m1.y, p1.y, m3.y, p3.y, m5.y, p5.y),
+                                      tap7(c0, c1, c3, c5, bias, e.z, m1.z, p1.z, m3.z, p3.z, m5.z, p5.z),
+                                      tap7(c0, c1, c3, c5, bias, e.w, m1.w, p1.w, m3.w, p3.w, m5.w, p5.w));
+            if (G::ND >= kThreads || tid < G::ND) L[u * kPitch + tid] = d;
+        }
+        if (edge) {  // replicate the edge pixels (EXTEND_COPY) inside the LDS image
+            __syncthreads();
+            u8 *Lb = reinterpret_cast<u8 *>(L);
+            const int nfill = nl + nr;
+            for (int i = tid; i < R * nfill * B; i += kThreads) {
+                const int u = i / (nfill * B);
+                const int rem = i - u * nfill * B;
+                const int f = rem / B, c = rem - f * B;
+                const int dst = f < nl ? f : fr + (f - nl);
+                const int srcp = f < nl ? nl : fr - 1;
+                Lb[u * kPitch * 4 + B * dst + G::OFF0 + c] = Lb[u * kPitch * 4 + B * srcp + G::OFF0 + c];
+            }
+        }
+        __syncthreads();
+        // ---- horizontal pass: K output pixels per item, one channel at a time ----
+        constexpr int items_per_row = TW / K;
+        for (int it = tid; it < R * items_per_row; it += kThreads) {
+            const int u = it / items_per_row;
+            const int j = it - u * items_per_row;
+            const int x = x0 + K * j;
+            const int y = yc + u;
+            if (y >= a.oh || x >= a.ow) continue;
+            const uint32_t *row = L + u * kPitch;
+            constexpr int W0 = (B * 2 * K) / 4;  // window start (dwords) per item
+            uint32_t win[13];
+            if (B == 3) {
+                const uint2 *r2 = reinterpret_cast<const uint2 *>(row + W0 * j);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {
+                    const uint2 dd = r2[q];
+                    win[2 * q] = dd.x;
+                    win[2 * q + 1] = dd.y;
+                }
+                win[12] = row[W0 * j + 12];
+            } else {
+                const uint4 *r4 = reinterpret_cast<const uint4 *>(row + W0 * j);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const uint4 dd = r4[q];
+                    win[4 * q] = dd.x, win[4 * q + 1] = dd.y, win[4 * q + 2] = dd.z, win[4 * q + 3] = dd.w;
+                }
+                win[12] = row[W0 * j + 12];
+            }
+            float o[K][B];
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                // px[t]: intermediate pixel 2x - 5 + t of channel c
+                float px[2 * K + 9];
+#pragma unroll
+                for (int t = 0; t < 2 * K + 9; ++t) {
+                    const int lb = B * t + c + G::OFF0;
+                    const uint32_t dd = win[lb >> 2];
+                    switch (lb & 3) {
+                        case 0: px[t] = ubyte_once<0>(dd); break;
+                        case 1: px[t] = ubyte_once<1>(dd); break;
+                        case 2: px[t] = ubyte_once<2>(dd); break;
+                        default: px[t] = ubyte_once<3>(dd); break;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int m = 2 * k + 5;
+                    o[k][c] = tap7(c0, c1, c3, c5, bias, px[m], px[m - 1], px[m + 1], px[m - 3], px[m + 3],
+                                   px[m - 5], px[m + 5]);
+                }
+            }
+            u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
+            const bool full = x + K <= a.ow;
+            if (B == 3) {
+                const uint32_t d0 = pack4b(o[0][0], o[0][1], o[0][2], o[1][0]);
+                const uint32_t d1 = pack4b(o[1][1], o[1][2], o[2][0], o[2][1]);
+                const uint32_t d2 = pack4b(o[2][2], o[3][0], o[3][1], o[3][2]);
+                if (full && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+                    *reinterpret_cast<uint3 *>(q) = uint3{d0, d1, d2};
+                } else {
+                    const uint32_t dd[3] = {d0, d1, d2};
+                    const int nb = (full ? K : a.ow - x) * B;
+                    for (int i = 0; i < nb; ++i) q[i] = static_cast<u8>(dd[i >> 2] >> (8 * (i & 3)));
+                }
+            } else {
+                const uint32_t d0 = pack4b(o[0][0], o[0][1], o[0][2], o[0][3]);
+                const uint32_t d1 = pack4b(o[1][0], o[1][1], o[1][2], o[1][3]);
+                uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
+                if (full && (reinterpret_cast<uintptr_t>(q) & 7u) == 0) {
+                    *reinterpret_cast<uint2 *>(q) = uint2{d0, d1};
+                } else {
+                    q32[0] = d0;
+                    if (full) q32[1] = d1;
+                }
+            }
+        }
+        // double-buffered LDS: the next vertical pass writes the other buffer, whose
+        // readers all finished before this chunk's barrier
+    }
+}
+
+// Variant bits (A/B in one process via MIPX_R2_VARIANT; default = best measured):
+// bit 0: R = 6 (else 12), bit 1: register prefetch of the next chunk.
+template <int B, int VAR>
+__global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
+    constexpr int R = (VAR & 1) ? 6 : 12;
+    constexpr bool PF = (VAR & 2) != 0;
+    __shared__ uint32_t lds[2 * R * kPitch];
+    const uint32_t t = a.remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+    int strip, band, img;
+    if (a.band_major) {  // tiles ordered (img, strip, band): vertical neighbours adjacent
+        band = t % a.n_bands;
+        const int rest = t / a.n_bands;
+        strip = rest % a.n_strips;
+        img = rest / a.n_strips;
+    } else {             // (img, band, strip): horizontal neighbours adjacent
+        strip = t % a.n_strips;
+        const int rest = t / a.n_strips;
+        band = rest % a.n_bands;
+        img = rest / a.n_bands;
+    }
+    reduce2_tile<B, R, PF>(a, img, strip, band, lds);
+}
+
+
+}  // namespace
+
+// ===========================================================================
+// launchers
+// ===========================================================================
+int reducev_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double vshrink, hipStream_t st) {
+    int taps = 0;
+    const float *tab = device_reduce_table(vshrink, &taps);
+    if (!tab) return MIPX_EDEVICE;
+    RedV a{};
+    a.in = in;
+    a.out = out;
+    a.row_bytes = w * b;
+    a.h = h;
+    a.oh = out_size_reduce(h, vshrink);
+    a.col_blocks = (a.row_bytes / 4 + 1 + 255) / 256;
+    a.pad = taps / 2 - 1;
+    a.taps = taps;
+    a.shrink = vshrink;
+    a.tab = tab;
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = img_bytes(w, a.oh, b);
+    const long long blocks = static_cast<long long>(a.col_blocks) * a.oh * n;
+    if (!grid_ok(blocks)) return MIPX_EINVAL;
+    const bool dword = (a.row_bytes % 4) == 0 && (reinterpret_cast<uintptr_t>(in) % 4) == 0 &&
+                       (reinterpret_cast<uintptr_t>(out) % 4) == 0 && a.in_img < 0x7fffffffLL;
+    if (dword) hipLaunchKernelGGL(k_reducev_gen<true>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_reducev_gen<false>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, a);
+    return launch_check("k_reducev_gen");
+}
+
+int reduceh_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hshrink, hipStream_t st) {
+    int taps = 0;
+    const float *tab = device_reduce_table(hshrink, &taps);
+    if (!tab) return MIPX_EDEVICE;
+    RedH a{};
+    a.in = in;
+    a.out = out;
+    a.w = w;
+    a.h = h;
+    a.ow = out_size_reduce(w, hshrink);
+    a.x_blocks = (a.ow + 255) / 256;
+    a.pad = taps / 2 - 1;
+    a.taps = taps;
+    a.shrink = hshrink;
+    a.tab = tab;
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = img_bytes(a.ow, h, b);
+    a.span_max = static_cast<int>(std::ceil(255 * hshrink)) + taps + 2;
+    const size_t lds = (static_cast<size_t>(kTransformScale + 1) * taps + a.span_max) * 4;
+    const bool aligned4 = b != 4 || ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 4) == 0;
+    if (lds <= 48 * 1024 && aligned4) {
+        const long long blocks = static_cast<long long>(a.x_blocks) * h * n;
+        if (!grid_ok(blocks)) return MIPX_EINVAL;
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduceh_lds<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256),
+                                                  lds, st, a));
+        return launch_check("k_reduceh_lds");
+    }
+    dim3 grid((a.ow + 255) / 256, h, n);
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduceh_gather<B_>, grid, dim3(256), 0, st, a));
+    return launch_check("k_reduceh_gather");
+}
+
+// Is the phase-0 mask of shrink 2 the 7-nonzero symmetric shape the fused
+// kernel hard-wires?  Returns the four distinct taps.
+bool reduce2_taps(float c[4]) {
+    std::vector<int> t;
+    reduce_table(2.0, t);
+    const int n = reduce_points(2.0);
+    if (n != 13) return false;
+    const int *r = t.data();  // phase 0
+    static const int zero[] = {1, 3, 7, 9, 11, 12};
+    for (int z : zero)
+        if (r[z] != 0) return false;
+    if (r[4] != r[6] || r[2] != r[8] || r[0] != r[10]) return false;
+    c[0] = static_cast<float>(r[5]);
+    c[1] = static_cast<float>(r[4]);
+    c[2] = static_cast<float>(r[2]);
+    c[3] = static_cast<float>(r[0]);
+    return true;
+}
+
+// Fused path applies to shrink exactly 2 x 2 on 3- or 4-band images whose rows
+// are dword aligned.
+bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
+    if (hs != 2.0 || vs != 2.0) return false;
+    if (b != 3 && b != 4) return false;
+    if ((w * b) % 4 != 0 || (reinterpret_cast<uintptr_t>(in) % 4) != 0) return false;
+    if (w < 8 || h < 8) return false;
+    static const bool shape_ok = [] { float c[4]; return reduce2_taps(c); }();
+    return shape_ok;
+}
+
+// MIPX_R2_VARIANT overrides the default variant of k_reduce2x2 for A/B runs
+// (scripts/ab_reduce.py); read per launch so one process can interleave them.
+constexpr int kR2Default = 2;  // R = 12 + register prefetch: measured best (profiles/r01/v5_variants_ab.log)
+int reduce2_variant() {
+    const char *e = std::getenv("MIPX_R2_VARIANT");
+    if (!e || !*e) return kR2Default;
+    const int v = std::atoi(e);
+    return (v >= 0 && v <= 3) ? v : kR2Default;
+}
+
+int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_t st) {
+    float c[4];
+    if (!reduce2_taps(c)) return MIPX_EINVAL;
+    Reduce2Args a{};
+    a.in = in;
+    a.out = out;
+    a.w = w;
+    a.h = h;
+    a.ow = out_size_reduce(w, 2.0);
+    a.oh = out_size_reduce(h, 2.0);
+    const int tw = b == 3 ? R2<3>::TW : R2<4>::TW;
+    a.n_strips = (a.ow + tw - 1) / tw;
+    const int chunks = (a.oh + kR - 1) / kR;
+    // rows per workgroup: 2 chunks of 12 (measured best, profiles/r01/geom_ab.log; MIPX_R2_BAND overrides)
+    const char *eb = std::getenv("MIPX_R2_BAND");
+    const int cpb = (eb && *eb) ? std::max(1, std::atoi(eb)) : 2;
+    const int chunks_per_band = std::max(1, std::min(chunks, cpb));
+    a.band_rows = chunks_per_band * kR;
+    a.n_bands = (a.oh + a.band_rows - 1) / a.band_rows;
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = img_bytes(a.ow, a.oh, b);
+    a.c0 = c[0] / 4096.0f;
+    a.c1 = c[1] / 4096.0f;
+    a.c3 = c[2] / 4096.0f;
+    a.c5 = c[3] / 4096.0f;
+    a.bias = 1.0f / 8192.0f;
+    const char *er = std::getenv("MIPX_R2_REMAP");
+    a.remap = (er && *er) ? std::atoi(er) : 1;
+    const char *eo = std::getenv("MIPX_R2_ORDER");
+    a.band_major = (eo && *eo) ? std::atoi(eo) : 0;
+    const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
+    if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
+    dim3 grid(static_cast<unsigned>(tiles));
+    const int var = reduce2_variant();
+#define MIPX_R2(V)                                                                           \
+    case V:                                                                                  \
+        if (b == 3) hipLaunchKernelGGL((k_reduce2x2<3, V>), grid, dim3(kThreads), 0, st, a); \
+        else hipLaunchKernelGGL((k_reduce2x2<4, V>), grid, dim3(kThreads), 0, st, a);        \
+        break;
+    switch (var) {
+        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3)
+        default: return MIPX_EINVAL;
+    }
+#undef MIPX_R2
+    return launch_check("k_reduce2x2");
+}
+
+
+}  // namespace mipx

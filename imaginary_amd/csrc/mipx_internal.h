@@ -55,10 +55,35 @@ const float *device_reduce_table(double shrink, int *n_taps);
 const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt]
 void free_device_tables();
 
-// ---- kernels (mipx_kernels.hip) ------------------------------------------------
+// ---- kernel launchers (k_*.hip); batches of n images packed back to back -----
+// k_reduce.hip
+int reducev_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double vshrink, hipStream_t st);
+int reduceh_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hshrink, hipStream_t st);
+bool reduce2_eligible(const uint8_t *in, int w, int h, int b, double hs, double vs);
+int reduce2_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, hipStream_t st);
+// k_shrink.hip
+int shrink_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int hs, int vs, hipStream_t st);
+// k_geometry.hip
+int embed_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int x, int y, int ow, int oh,
+                 int extend, const int *bg, const int *d_origins, hipStream_t st);
+int flip_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int vertical, hipStream_t st);
+int rot_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int angle, hipStream_t st);
+int extract_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int left, int top, int ow, int oh,
+                   hipStream_t st);
+// k_blur.hip (ws: n * w * h * b bytes for the uchar intermediate)
+int blur_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double sigma, double min_ampl,
+                void *ws, size_t ws_bytes, hipStream_t st);
+// k_composite.hip
+int watermark_launch(const uint8_t *base, const uint8_t *wm, uint8_t *out, int n, int w, int h, int bands, int ww,
+                     int wh, int wb, int left, int top, float opacity, hipStream_t st);
+// k_smartcrop.hip
+size_t smartcrop_workspace_bytes(int n, int w, int h, int bands);
+int smartcrop_origins(const uint8_t *in, int *origins, int n, int w, int h, int b, int cw, int ch, void *ws,
+                      size_t ws_bytes, hipStream_t st);
+int smartcrop_extract(const uint8_t *in, uint8_t *out, int n, int w, int h, int bands, int cw, int ch, void *ws,
+                      size_t ws_bytes, hipStream_t st);
+// mipx_ops.cpp
 size_t op_workspace_bytes(int op, int n, int w, int h, int bands, double p0, double p1);
-int smartcrop_extract(const uint8_t *in, uint8_t *out, int n, int w, int h, int bands,
-                      int cw, int ch, void *ws, size_t ws_bytes, hipStream_t st);
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -43,6 +43,8 @@ REDUCE_CASES = [
     (270, 480, 3, 1.6, 1.6), (300, 200, 3, 2.4666666666666666, 2.4666666666666666),
     (101, 131, 4, 1.3333333333333333, 1.3333333333333333), (60, 90, 3, 3.7, 1.2), (33, 17, 3, 1.0, 2.5),
     (64, 64, 3, 2.5, 1.0), (128, 96, 3, 7.3, 7.3),
+    # large shrink: the horizontal pass falls back from LDS staging to gathers
+    (300, 420, 3, 14.2, 14.2), (90, 700, 4, 20.0, 3.0),
 ]
 
 
@@ -82,7 +84,8 @@ def test_reduce_4k_to_1080p_full_size(gpu, oracle, rng):
 
 # ---------------------------------------------------------------- box shrink
 @pytest.mark.parametrize("h,w,b,hs,vs", [(64, 64, 3, 2, 2), (100, 75, 3, 8, 8), (31, 47, 4, 3, 5),
-                                         (3000 // 10, 4000 // 10, 3, 11, 11), (9, 9, 1, 4, 4), (20, 20, 2, 1, 3)])
+                                         (3000 // 10, 4000 // 10, 3, 11, 11), (9, 9, 1, 4, 4), (20, 20, 2, 1, 3),
+                                         (37, 1001, 3, 7, 3), (40, 3000, 4, 33, 2), (16, 4096, 1, 200, 8)])
 def test_shrink_matches_oracle(gpu, oracle, rng, h, w, b, hs, vs):
     img = rand_img(rng, h, w, b)
     assert_same(gpu.run_op("shrink", img, hshrink=hs, vshrink=vs)[0], oracle.shrink(img, hs, vs), "shrink")
@@ -114,11 +117,21 @@ def test_extract_rot_flip(gpu, oracle, rng, b):
     assert_same(r, img, "rot90^4 == identity")
 
 
+@pytest.mark.parametrize("h,w,b", [(33, 65, 3), (64, 96, 4), (100, 31, 1), (70, 71, 2), (128, 256, 4)])
+def test_rot_tiles_and_aligned_extract(gpu, oracle, rng, h, w, b):
+    img = rand_img(rng, h, w, b)
+    for a in (90, 180, 270):
+        assert_same(gpu.run_op("rot", img, angle=a)[0], oracle.rot(img, a), f"rot{a} {h}x{w}x{b}")
+    for left, top, ew, eh in ((4, 3, w - 8, h - 5), (0, 0, w, h), (w // 2, h // 3, w // 2, h // 2)):
+        assert_same(gpu.run_op("extract", img, left=left, top=top, width=ew, height=eh)[0],
+                    oracle.extract(img, left, top, ew, eh), f"extract {left},{top}")
+
+
 # ---------------------------------------------------------------- gaussian blur
 @pytest.mark.parametrize("sigma", [0.8, 1.0, 3.0, 5.0, 12.5])
-@pytest.mark.parametrize("b", [3, 4])
+@pytest.mark.parametrize("b", [1, 3, 4])
 def test_gaussblur_matches_oracle(gpu, oracle, rng, sigma, b):
-    img = rand_img(rng, 45, 70, b)
+    img = rand_img(rng, 45, 301 if b == 1 else 70, b)
     assert_same(gpu.run_op("gaussblur", img, sigma=sigma, min_ampl=0.2)[0], oracle.gaussblur(img, sigma, 0.2),
                 f"blur {sigma}")
 
