@@ -60,7 +60,7 @@ def cpu_baseline(args, sample):
                       f"(reducev+reduceh Lanczos3 2x2), {threads} OpenMP threads, {dt:.2f} s wall"}
 
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic_v5.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic_v6.json")
 
 
 def pmc_traffic(kernel_name_hint):

@@ -115,6 +115,7 @@ _SIG = {
                               C.POINTER(MipxImg), C.POINTER(C.c_uint64)]),
     "mipx_wait": (C.c_int, [C.c_uint64, C.c_int]),
     "mipx_process": (C.c_int, [C.POINTER(MipxPlan), C.POINTER(MipxImg), C.POINTER(MipxImg), C.POINTER(MipxImg)]),
+    "mipx_stats": (C.c_int, [C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "mipx_workspace_bytes": (C.c_size_t, [C.POINTER(MipxPlan), _I]),
     "mipx_execute_dev": (C.c_int, [C.POINTER(MipxPlan), _I, _U8P, _U8P, _U8P, _P, C.c_size_t, _P]),
     "mipx_op_reduce": (C.c_int, [_U8P, _U8P, _I, _I, _I, _I, C.c_double, C.c_double, _P, C.c_size_t, _P]),

@@ -208,38 +208,124 @@ int execute_plan(const mipx_plan *p, int n, const uint8_t *d_in, uint8_t *d_out,
 }
 
 // ---- request path ----------------------------------------------------------------
+//
+// Per device: a worker thread forms batches and ENQUEUES them, a completer
+// thread retires them.  Each batch occupies one of kSlots buffer slots and
+// flows over three non-blocking streams chained by events:
+//
+//   s_h2d : pinned request inputs -> slot.d_in                 (ev_h2d)
+//   s_exec: wait ev_h2d, run the plan  slot.d_in -> slot.d_out (ev_exec)
+//   s_d2h : wait ev_exec, slot.d_out -> pinned slot.h_out      (ev_done)
+//
+// so batch k+1's upload overlaps batch k's kernels and batch k's download
+// overlaps batch k+1's kernels.  A slot is reused only after the completer
+// has seen its ev_done, so no buffer is overwritten while in flight.
 namespace {
+
+constexpr int kSlots = 2;
+
+// Pinned host blocks reused across requests: hipHostMalloc / hipHostFree of a
+// 25 MB block costs far more than the copy into it.
+class PinnedPool {
+   public:
+    static size_t size_class(size_t n) {  // 1/16-power-of-two classes, >= 64 KiB
+        const size_t floor_c = size_t(64) << 10;
+        if (n <= floor_c) return floor_c;
+        size_t p = 1;
+        while (p < n) p <<= 1;
+        const size_t step = p / 16;
+        return (n + step - 1) / step * step;
+    }
+    uint8_t *get(size_t n, size_t *cap) {
+        *cap = size_class(n);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto it = free_.find(*cap);
+            if (it != free_.end()) {
+                uint8_t *p = it->second;
+                free_.erase(it);
+                cached_ -= *cap;
+                return p;
+            }
+        }
+        void *p = nullptr;
+        if (hipHostMalloc(&p, *cap, hipHostMallocPortable) != hipSuccess) return nullptr;
+        return static_cast<uint8_t *>(p);
+    }
+    void put(uint8_t *p, size_t cap) {
+        if (!p) return;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (cached_ + cap <= limit_) {
+                free_.emplace(cap, p);
+                cached_ += cap;
+                return;
+            }
+        }
+        (void)hipHostFree(p);
+    }
+    void set_limit(size_t l) {
+        std::lock_guard<std::mutex> lk(mu_);
+        limit_ = l;
+    }
+    void clear() {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (auto &kv : free_) (void)hipHostFree(kv.second);
+        free_.clear();
+        cached_ = 0;
+    }
+
+   private:
+    std::mutex mu_;
+    std::multimap<size_t, uint8_t *> free_;
+    size_t cached_ = 0, limit_ = size_t(1) << 30;
+};
+PinnedPool &pool() {
+    static PinnedPool *p = new PinnedPool();  // leaked on purpose: outlives static dtors
+    return *p;
+}
 
 struct Job {
     uint64_t ticket = 0;
     mipx_plan plan{};
     std::vector<uint8_t> plan_key;   // bytes compared for batching
-    uint8_t *pin_in = nullptr;       // pinned copy of the packed input
-    size_t in_bytes = 0;
+    uint8_t *pin_in = nullptr;       // pinned copy of the packed input (pool block)
+    size_t in_bytes = 0, in_cap = 0;
     uint8_t *pin_wm = nullptr;
-    size_t wm_bytes = 0;
+    size_t wm_bytes = 0, wm_cap = 0;
     mipx_img out{};
     size_t out_bytes = 0;
     int status = 1;                  // 1 = pending
-    bool waited = false;
     std::mutex mu;
     std::condition_variable cv;
 };
 
-struct Device {
-    int id = 0;
-    hipStream_t stream = nullptr;
-    std::thread worker;
-    std::mutex mu;
-    std::condition_variable cv;
-    std::deque<std::shared_ptr<Job>> q;
-    std::atomic<int64_t> pending_bytes{0};
-    bool stop = false;
-    // device buffers grown on demand (worker thread only)
+struct Slot {
     uint8_t *d_in = nullptr, *d_out = nullptr, *d_wm = nullptr, *d_ws = nullptr;
     size_t in_cap = 0, out_cap = 0, wm_cap = 0, ws_cap = 0;
     uint8_t *h_out = nullptr;  // pinned output staging
     size_t h_out_cap = 0;
+    hipEvent_t ev_h2d = nullptr, ev_exec = nullptr, ev_done = nullptr;
+    bool busy = false;
+    int status = 0;
+    std::vector<std::shared_ptr<Job>> batch;
+};
+
+struct Device {
+    int id = 0;
+    hipStream_t s_h2d = nullptr, s_exec = nullptr, s_d2h = nullptr;
+    std::thread worker, completer;
+    std::mutex mu;  // request queue
+    std::condition_variable cv;
+    std::deque<std::shared_ptr<Job>> q;
+    std::atomic<int64_t> pending_bytes{0};
+    bool stop = false;
+    std::mutex fmu;  // slots + in-flight FIFO
+    std::condition_variable fcv;
+    std::deque<int> inflight;
+    bool worker_done = false;
+    Slot slots[kSlots];
+    std::atomic<uint64_t> batches{0}, requests{0};
 };
 
 struct Runtime {
@@ -284,38 +370,70 @@ void finish(const std::shared_ptr<Job> &j, int status) {
     j->cv.notify_all();
 }
 
-int run_batch(Device &d, std::vector<std::shared_ptr<Job>> &batch) {
+// Enqueue one batch on the slot's three-stream chain; never synchronises.
+int launch_batch(Device &d, Slot &s) {
+    auto &batch = s.batch;
     const mipx_plan &p = batch[0]->plan;
     const int n = static_cast<int>(batch.size());
     const size_t in1 = batch[0]->in_bytes, out1 = batch[0]->out_bytes;
     int e;
-    if ((e = grow(&d.d_in, &d.in_cap, in1 * n))) return e;
-    if ((e = grow(&d.d_out, &d.out_cap, out1 * n))) return e;
-    if ((e = grow_host(&d.h_out, &d.h_out_cap, out1 * n))) return e;
+    if ((e = grow(&s.d_in, &s.in_cap, in1 * n))) return e;
+    if ((e = grow(&s.d_out, &s.out_cap, out1 * n))) return e;
+    if ((e = grow_host(&s.h_out, &s.h_out_cap, out1 * n))) return e;
     ExecLayout L;
     if ((e = plan_layout(&p, n, &L))) return e;
-    if ((e = grow(&d.d_ws, &d.ws_cap, L.total() + 256))) return e;
+    if ((e = grow(&s.d_ws, &s.ws_cap, L.total() + 256))) return e;
     for (int i = 0; i < n; ++i)
-        MIPX_HIP(hipMemcpyAsync(d.d_in + in1 * i, batch[i]->pin_in, in1, hipMemcpyHostToDevice, d.stream));
+        MIPX_HIP(hipMemcpyAsync(s.d_in + in1 * i, batch[i]->pin_in, in1, hipMemcpyHostToDevice, d.s_h2d));
     const uint8_t *wm = nullptr;
     if (batch[0]->pin_wm) {  // watermark is per request; batches share a byte-identical one
-        if ((e = grow(&d.d_wm, &d.wm_cap, batch[0]->wm_bytes))) return e;
-        MIPX_HIP(hipMemcpyAsync(d.d_wm, batch[0]->pin_wm, batch[0]->wm_bytes, hipMemcpyHostToDevice, d.stream));
-        wm = d.d_wm;
+        if ((e = grow(&s.d_wm, &s.wm_cap, batch[0]->wm_bytes))) return e;
+        MIPX_HIP(hipMemcpyAsync(s.d_wm, batch[0]->pin_wm, batch[0]->wm_bytes, hipMemcpyHostToDevice, d.s_h2d));
+        wm = s.d_wm;
     }
-    if ((e = execute_plan(&p, n, d.d_in, d.d_out, wm, d.d_ws, d.ws_cap, d.stream))) return e;
-    MIPX_HIP(hipMemcpyAsync(d.h_out, d.d_out, out1 * n, hipMemcpyDeviceToHost, d.stream));
-    MIPX_HIP(hipStreamSynchronize(d.stream));
-    for (int i = 0; i < n; ++i) {
-        const mipx_img &o = batch[i]->out;
-        const size_t row = static_cast<size_t>(o.w) * o.bands;
-        const size_t stride = o.stride ? static_cast<size_t>(o.stride) : row;
-        const uint8_t *src = d.h_out + out1 * i;
-        if (stride == row) std::memcpy(o.data, src, out1);
-        else
-            for (int y = 0; y < o.h; ++y) std::memcpy(o.data + y * stride, src + y * row, row);
-    }
+    MIPX_HIP(hipEventRecord(s.ev_h2d, d.s_h2d));
+    MIPX_HIP(hipStreamWaitEvent(d.s_exec, s.ev_h2d, 0));
+    if ((e = execute_plan(&p, n, s.d_in, s.d_out, wm, s.d_ws, s.ws_cap, d.s_exec))) return e;
+    MIPX_HIP(hipEventRecord(s.ev_exec, d.s_exec));
+    MIPX_HIP(hipStreamWaitEvent(d.s_d2h, s.ev_exec, 0));
+    MIPX_HIP(hipMemcpyAsync(s.h_out, s.d_out, out1 * n, hipMemcpyDeviceToHost, d.s_d2h));
+    MIPX_HIP(hipEventRecord(s.ev_done, d.s_d2h));
     return MIPX_OK;
+}
+
+// Wait for a slot's batch, scatter its outputs to the callers, release it.
+void retire_batch(Device &d, Slot &s) {
+    int e = s.status;
+    if (e == MIPX_OK) {
+        const hipError_t he = hipEventSynchronize(s.ev_done);
+        if (he != hipSuccess) e = hip_fail(he, "hipEventSynchronize(batch)");
+    } else {  // a failed enqueue may have left work behind on any of the streams
+        (void)hipStreamSynchronize(d.s_h2d);
+        (void)hipStreamSynchronize(d.s_exec);
+        (void)hipStreamSynchronize(d.s_d2h);
+    }
+    const size_t out1 = s.batch[0]->out_bytes;
+    for (size_t i = 0; i < s.batch.size(); ++i) {
+        auto &j = s.batch[i];
+        if (e == MIPX_OK) {
+            const mipx_img &o = j->out;
+            const size_t row = static_cast<size_t>(o.w) * o.bands;
+            const size_t stride = o.stride ? static_cast<size_t>(o.stride) : row;
+            const uint8_t *src = s.h_out + out1 * i;
+            if (stride == row) std::memcpy(o.data, src, out1);
+            else
+                for (int y = 0; y < o.h; ++y) std::memcpy(o.data + y * stride, src + y * row, row);
+        }
+        d.pending_bytes -= static_cast<int64_t>(j->in_bytes);
+        pool().put(j->pin_in, j->in_cap);
+        j->pin_in = nullptr;
+        pool().put(j->pin_wm, j->wm_cap);
+        j->pin_wm = nullptr;
+        finish(j, e);
+    }
+    d.batches += 1;
+    d.requests += s.batch.size();
+    s.batch.clear();
 }
 
 bool same_batch(const Job &a, const Job &b) {
@@ -332,7 +450,7 @@ void worker_main(Device *d) {
         {
             std::unique_lock<std::mutex> lk(d->mu);
             d->cv.wait(lk, [&] { return d->stop || !d->q.empty(); });
-            if (d->stop && d->q.empty()) return;
+            if (d->stop && d->q.empty()) break;
             if (r.batch_wait_us > 0 && static_cast<int>(d->q.size()) < r.max_batch)
                 d->cv.wait_for(lk, std::chrono::microseconds(r.batch_wait_us),
                                [&] { return d->stop || static_cast<int>(d->q.size()) >= r.max_batch; });
@@ -347,26 +465,100 @@ void worker_main(Device *d) {
                 }
             }
         }
-        const int e = run_batch(*d, batch);
-        for (auto &j : batch) {
-            d->pending_bytes -= static_cast<int64_t>(j->in_bytes);
-            (void)hipHostFree(j->pin_in);
-            j->pin_in = nullptr;
-            if (j->pin_wm) (void)hipHostFree(j->pin_wm);
-            j->pin_wm = nullptr;
-            finish(j, e);
+        int si = -1;
+        {
+            std::unique_lock<std::mutex> lk(d->fmu);
+            d->fcv.wait(lk, [&] {
+                for (const Slot &s : d->slots)
+                    if (!s.busy) return true;
+                return false;
+            });
+            for (int i = 0; i < kSlots && si < 0; ++i)
+                if (!d->slots[i].busy) si = i;
+            d->slots[si].busy = true;
         }
+        Slot &s = d->slots[si];
+        s.batch = std::move(batch);
+        s.status = launch_batch(*d, s);
+        {
+            std::lock_guard<std::mutex> lk(d->fmu);
+            d->inflight.push_back(si);
+        }
+        d->fcv.notify_all();
+    }
+    {
+        std::lock_guard<std::mutex> lk(d->fmu);
+        d->worker_done = true;
+    }
+    d->fcv.notify_all();
+}
+
+// Retires batches in submission order; exits once the worker is done and
+// nothing is in flight.
+void completer_main(Device *d) {
+    (void)hipSetDevice(d->id);
+    for (;;) {
+        int si;
+        {
+            std::unique_lock<std::mutex> lk(d->fmu);
+            d->fcv.wait(lk, [&] { return !d->inflight.empty() || d->worker_done; });
+            if (d->inflight.empty()) return;
+            si = d->inflight.front();
+        }
+        retire_batch(*d, d->slots[si]);
+        {
+            std::lock_guard<std::mutex> lk(d->fmu);
+            d->inflight.pop_front();
+            d->slots[si].busy = false;
+        }
+        d->fcv.notify_all();
     }
 }
 
-int pack_pinned(const mipx_img *img, uint8_t **dst, size_t *bytes) {
+int pack_pinned(const mipx_img *img, uint8_t **dst, size_t *bytes, size_t *cap) {
     const size_t row = static_cast<size_t>(img->w) * img->bands;
     const size_t stride = img->stride ? static_cast<size_t>(img->stride) : row;
     *bytes = row * img->h;
-    MIPX_HIP(hipHostMalloc(reinterpret_cast<void **>(dst), *bytes, hipHostMallocDefault));
+    *dst = pool().get(*bytes, cap);
+    if (!*dst) {
+        set_error("pinned staging: hipHostMalloc(%zu) failed", *cap);
+        return MIPX_ENOMEM;
+    }
     if (stride == row) std::memcpy(*dst, img->data, *bytes);
     else
         for (int y = 0; y < img->h; ++y) std::memcpy(*dst + y * row, img->data + y * stride, row);
+    return MIPX_OK;
+}
+
+void destroy_device(Device &d) {
+    (void)hipSetDevice(d.id);
+    for (Slot &s : d.slots) {
+        (void)hipFree(s.d_in);
+        (void)hipFree(s.d_out);
+        (void)hipFree(s.d_wm);
+        (void)hipFree(s.d_ws);
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.ev_h2d) (void)hipEventDestroy(s.ev_h2d);
+        if (s.ev_exec) (void)hipEventDestroy(s.ev_exec);
+        if (s.ev_done) (void)hipEventDestroy(s.ev_done);
+        s = Slot();
+    }
+    if (d.s_h2d) (void)hipStreamDestroy(d.s_h2d);
+    if (d.s_exec) (void)hipStreamDestroy(d.s_exec);
+    if (d.s_d2h) (void)hipStreamDestroy(d.s_d2h);
+    d.s_h2d = d.s_exec = d.s_d2h = nullptr;
+}
+
+int create_device(Device &d) {
+    MIPX_HIP(hipSetDevice(d.id));
+    MIPX_HIP(hipStreamCreateWithFlags(&d.s_h2d, hipStreamNonBlocking));
+    MIPX_HIP(hipStreamCreateWithFlags(&d.s_exec, hipStreamNonBlocking));
+    MIPX_HIP(hipStreamCreateWithFlags(&d.s_d2h, hipStreamNonBlocking));
+    for (Slot &s : d.slots) {
+        MIPX_HIP(hipEventCreateWithFlags(&s.ev_h2d, hipEventDisableTiming));
+        MIPX_HIP(hipEventCreateWithFlags(&s.ev_exec, hipEventDisableTiming));
+        MIPX_HIP(hipEventCreateWithFlags(&s.ev_done, hipEventDisableTiming));
+    }
     return MIPX_OK;
 }
 
@@ -422,16 +614,25 @@ int mipx_init(const mipx_cfg *cfg) {
         for (int i = 0; i < ndev; ++i) ids.push_back(i);
     }
     if (ids.empty()) return MIPX_ENODEV;
-    if (cfg && cfg->max_batch > 0) r.max_batch = cfg->max_batch;
-    if (cfg && cfg->batch_wait_us > 0) r.batch_wait_us = cfg->batch_wait_us;
+    r.max_batch = (cfg && cfg->max_batch > 0) ? cfg->max_batch : 64;
+    r.batch_wait_us = (cfg && cfg->batch_wait_us > 0) ? cfg->batch_wait_us : 0;
+    pool().set_limit((cfg && cfg->staging_bytes > 0) ? static_cast<size_t>(cfg->staging_bytes) : size_t(1) << 30);
     for (int id : ids) {
         auto d = std::make_unique<Device>();
         d->id = id;
-        MIPX_HIP(hipSetDevice(id));
-        MIPX_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        const int e = create_device(*d);
+        if (e) {
+            destroy_device(*d);
+            for (auto &o : r.devs) destroy_device(*o);
+            r.devs.clear();
+            return e;
+        }
         r.devs.push_back(std::move(d));
     }
-    for (auto &d : r.devs) d->worker = std::thread(worker_main, d.get());
+    for (auto &d : r.devs) {
+        d->worker = std::thread(worker_main, d.get());
+        d->completer = std::thread(completer_main, d.get());
+    }
     r.up = true;
     return MIPX_OK;
 }
@@ -447,19 +648,28 @@ void mipx_shutdown(void) {
         }
         d->cv.notify_all();
     }
-    for (auto &d : r.devs) {
+    for (auto &d : r.devs) {  // the worker drains the queue; the completer retires it
         if (d->worker.joinable()) d->worker.join();
-        (void)hipSetDevice(d->id);
-        (void)hipFree(d->d_in);
-        (void)hipFree(d->d_out);
-        (void)hipFree(d->d_wm);
-        (void)hipFree(d->d_ws);
-        if (d->h_out) (void)hipHostFree(d->h_out);
-        (void)hipStreamDestroy(d->stream);
+        if (d->completer.joinable()) d->completer.join();
+        destroy_device(*d);
     }
     r.devs.clear();
+    pool().clear();
     free_device_tables();
     r.up = false;
+}
+
+int mipx_stats(int device, uint64_t *batches, uint64_t *requests) {
+    Runtime &r = rt();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (!r.up) return MIPX_ENOTINIT;
+    for (auto &d : r.devs)
+        if (d->id == device) {
+            if (batches) *batches = d->batches.load();
+            if (requests) *requests = d->requests.load();
+            return MIPX_OK;
+        }
+    return MIPX_EINVAL;
 }
 
 int mipx_submit(int device, const mipx_plan *plan, const mipx_img *in, const mipx_img *wm, mipx_img *out,
@@ -496,12 +706,12 @@ int mipx_submit(int device, const mipx_plan *plan, const mipx_img *in, const mip
     j->plan = *plan;
     const uint8_t *pk = reinterpret_cast<const uint8_t *>(plan);
     j->plan_key.assign(pk, pk + sizeof(mipx_plan));
-    int e = pack_pinned(in, &j->pin_in, &j->in_bytes);
+    int e = pack_pinned(in, &j->pin_in, &j->in_bytes, &j->in_cap);
     if (e) return e;
     if (needs_wm) {
-        e = pack_pinned(wm, &j->pin_wm, &j->wm_bytes);
+        e = pack_pinned(wm, &j->pin_wm, &j->wm_bytes, &j->wm_cap);
         if (e) {
-            (void)hipHostFree(j->pin_in);
+            pool().put(j->pin_in, j->in_cap);
             return e;
         }
     }

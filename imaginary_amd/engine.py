@@ -119,7 +119,9 @@ class Engine:
         check(lib.mipx_init(C.byref(cfg)), "mipx_init")
 
     def submit(self, plan: MipxPlan, img: np.ndarray, wm: Optional[np.ndarray] = None, device: int = -1):
-        img = np.ascontiguousarray(img, dtype=np.uint8)
+        if not (img.dtype == np.uint8 and img.ndim == 3 and img.strides[2] == 1
+                and img.strides[1] == img.shape[2]):
+            img = np.ascontiguousarray(img, dtype=np.uint8)  # rows may keep a wider stride
         out = np.empty((plan.out_h, plan.out_w, plan.out_bands), np.uint8)
         ti = C.c_uint64()
         wmi = C.byref(_img(np.ascontiguousarray(wm, dtype=np.uint8))) if wm is not None else None
@@ -134,6 +136,12 @@ class Engine:
         t, out = self.submit(plan, img, wm)
         self.wait(t)
         return out
+
+    def stats(self, device: int = 0):
+        """(batches launched, requests retired) on `device` since mipx_init."""
+        b, r = C.c_uint64(), C.c_uint64()
+        check(lib.mipx_stats(device, C.byref(b), C.byref(r)), "mipx_stats")
+        return b.value, r.value
 
     def shutdown(self):
         lib.mipx_shutdown()

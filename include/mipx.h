@@ -128,7 +128,7 @@ typedef struct mipx_img {
 typedef struct mipx_cfg {
     int32_t n_devices;              /* 0 = every visible device */
     int32_t device_ids[16];
-    int64_t staging_bytes;          /* pinned staging per device; 0 = default (256 MiB) */
+    int64_t staging_bytes;          /* pinned staging kept cached for reuse; 0 = default (1 GiB) */
     int32_t max_batch;              /* requests fused into one launch; 0 = default (64) */
     int32_t batch_wait_us;          /* bounded wait for more requests; 0 = none */
 } mipx_cfg;
@@ -154,6 +154,8 @@ int mipx_submit(int device, const mipx_plan *plan, const mipx_img *in, const mip
 int mipx_wait(uint64_t ticket, int timeout_ms);      /* timeout < 0 = forever */
 int mipx_process(const mipx_plan *plan, const mipx_img *in, const mipx_img *wm,
                  mipx_img *out);                     /* submit + wait */
+/* Batches launched and requests retired so far on `device` (batching telemetry). */
+int mipx_stats(int device, uint64_t *batches, uint64_t *requests);
 
 /* ---- device-resident batch API ---- */
 size_t mipx_workspace_bytes(const mipx_plan *plan, int32_t n);

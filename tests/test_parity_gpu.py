@@ -210,6 +210,45 @@ def test_request_path_batches_and_matches(gpu, oracle, rng):
         eng.shutdown()
 
 
+def test_request_path_concurrent_mixed_plans(gpu, oracle, rng):
+    """Many submitting threads, two interleaved plans, strided host buffers: every
+    result matches the oracle, batches fuse requests, the three-stream pipeline
+    retires everything."""
+    from concurrent.futures import ThreadPoolExecutor
+    eng = gpu.Engine(max_batch=16, batch_wait_us=2000)
+    try:
+        specs = [(dict(width=160, height=120, embed=1), (320, 240, 3)),
+                 (dict(sigma=2.0), (100, 80, 4)),
+                 (dict(width=50, height=50, crop=1, gravity=5), (200, 150, 3))]
+        plans = []
+        for opts, (w, h, b) in specs:
+            p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(w, h, b, "png"))
+            e, rp = oracle.plan(opts, dict(w=w, h=h, bands=b, type=3))
+            assert e == 0
+            plans.append((p, rp, (h, w, b)))
+        jobs = []
+        for i in range(60):
+            p, rp, (h, w, b) = plans[i % len(plans)]
+            wide = rand_img(rng, h, w + 7, b)          # a row stride wider than the image
+            jobs.append((p, rp, wide[:, :w]))
+
+        def one(job):
+            p, rp, img = job
+            t, out = eng.submit(p, img)
+            eng.wait(t)
+            return out, oracle.execute(rp, np.ascontiguousarray(img))
+
+        with ThreadPoolExecutor(6) as ex:
+            results = list(ex.map(one, jobs))
+        for k, (got, want) in enumerate(results):
+            assert_same(got, want, f"request {k}")
+        batches, requests = eng.stats(0)
+        assert requests == len(jobs)
+        assert batches < len(jobs)
+    finally:
+        eng.shutdown()
+
+
 def test_golden_vectors_on_gpu(gpu):
     """The committed fixtures (oracle outputs) are reproduced by the kernels."""
     from conftest import load_golden
