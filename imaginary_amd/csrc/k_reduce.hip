@@ -231,9 +231,14 @@ struct Reduce2Args {
     int band_major;  // tile order inside an XCD range (MIPX_R2_ORDER=1: bands fastest)
 };
 
-__device__ __forceinline__ float4 cvt4_once(uint32_t v) {
-    return float4{ubyte_once<0>(v), ubyte_once<1>(v), ubyte_once<2>(v), ubyte_once<3>(v)};
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v cvt4_once(uint32_t v) {
+    return f4v{ubyte_once<0>(v), ubyte_once<1>(v), ubyte_once<2>(v), ubyte_once<3>(v)};
 }
+__device__ __forceinline__ f2v lo2(f4v v) { return __builtin_shufflevector(v, v, 0, 1); }
+__device__ __forceinline__ f2v hi2(f4v v) { return __builtin_shufflevector(v, v, 2, 3); }
 
 // c0 e + c1 (m1 + p1) + c3 (m3 + p3) + c5 (m5 + p5) with pre-scaled taps and the
 // bias: every partial is exact on a 1/8192 grid below 2^9, so the result is
@@ -245,6 +250,15 @@ __device__ __forceinline__ float tap7(float c0, float c1, float c3, float c5, fl
     acc = __builtin_fmaf(c3, m3 + p3, acc);
     return __builtin_fmaf(c5, m5 + p5, acc);
 }
+// the same chain on two columns at once (v_pk_fma_f32 / v_pk_add_f32): each lane
+// of the pair sees exactly the scalar operation sequence, so results are identical
+__device__ __forceinline__ f2v tap7v(f2v c0, f2v c1, f2v c3, f2v c5, f2v bias, f2v e, f2v m1, f2v p1, f2v m3,
+                                     f2v p3, f2v m5, f2v p5) {
+    f2v acc = __builtin_elementwise_fma(c0, e, bias);
+    acc = __builtin_elementwise_fma(c1, m1 + p1, acc);
+    acc = __builtin_elementwise_fma(c3, m3 + p3, acc);
+    return __builtin_elementwise_fma(c5, m5 + p5, acc);
+}
 // v_cvt_pk_u8_f32 rounds to nearest-even and saturates to 0..255; on the
 // 1/4096 grid RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5) (no ties occur)
 __device__ __forceinline__ uint32_t pack4b(float a, float b, float c, float d) {
@@ -254,7 +268,7 @@ __device__ __forceinline__ uint32_t pack4b(float a, float b, float c, float d) {
     return __builtin_amdgcn_cvt_pk_u8_f32(d, 3, v);
 }
 
-template <int B, int R, bool PF>
+template <int B, int R, bool PF, bool PK, bool MEM, int LAUX, bool NTS>
 __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int strip, int band,
                                              uint32_t *lds) {
     using G = R2<B>;
@@ -285,17 +299,17 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 
     auto load_row = [&](int r) -> uint32_t {
         r = clampi(r, 0, a.h - 1);
-        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * row_bytes, 0));
+        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * row_bytes, LAUX));
     };
 
     // odd-row ring: slot s holds odd row 2m+1 with m = s (mod 6); y0 % 6 == 0
-    float4 ring[6];
+    f4v ring[6];
     ring[3] = cvt4_once(load_row(2 * (y0 - 3) + 1));
     ring[4] = cvt4_once(load_row(2 * (y0 - 2) + 1));
     ring[5] = cvt4_once(load_row(2 * (y0 - 1) + 1));
     ring[0] = cvt4_once(load_row(2 * y0 + 1));
     ring[1] = cvt4_once(load_row(2 * (y0 + 1) + 1));
-    ring[2] = float4{0.f, 0.f, 0.f, 0.f};
+    ring[2] = f4v{0.f, 0.f, 0.f, 0.f};
 
     uint32_t odd[R], even[R];
     if (PF) {
@@ -319,18 +333,36 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
         const bool more = yc + R < y1;
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-            ring[(u + 2) % 6] = cvt4_once(odd[u]);
-            const float4 e = cvt4_once(even[u]);
-            if (PF && more) {  // rotate: this register now fetches the next chunk's row
-                odd[u] = load_row(2 * (yc + R + u + 2) + 1);
-                even[u] = load_row(2 * (yc + R + u));
+            uint32_t d;
+            if (MEM) {  // diagnostic: same loads / LDS / stores, no arithmetic
+                d = odd[u] + even[u];
+                if (PF && more) {
+                    odd[u] = load_row(2 * (yc + R + u + 2) + 1);
+                    even[u] = load_row(2 * (yc + R + u));
+                }
+            } else {
+                ring[(u + 2) % 6] = cvt4_once(odd[u]);
+                const f4v e = cvt4_once(even[u]);
+                if (PF && more) {  // rotate: this register now fetches the next chunk's row
+                    odd[u] = load_row(2 * (yc + R + u + 2) + 1);
+                    even[u] = load_row(2 * (yc + R + u));
+                }
+                const f4v m5 = ring[(u + 3) % 6], m3 = ring[(u + 4) % 6], m1 = ring[(u + 5) % 6];
+                const f4v p1 = ring[u % 6], p3 = ring[(u + 1) % 6], p5 = ring[(u + 2) % 6];
+                if (PK) {
+                    const f2v C0 = {c0, c0}, C1 = {c1, c1}, C3 = {c3, c3}, C5 = {c5, c5}, BI = {bias, bias};
+                    const f2v a = tap7v(C0, C1, C3, C5, BI, lo2(e), lo2(m1), lo2(p1), lo2(m3), lo2(p3), lo2(m5),
+                                        lo2(p5));
+                    const f2v b = tap7v(C0, C1, C3, C5, BI, hi2(e), hi2(m1), hi2(p1), hi2(m3), hi2(p3), hi2(m5),
+                                        hi2(p5));
+                    d = pack4b(a.x, a.y, b.x, b.y);
+                } else {
+                    d = pack4b(tap7(c0, c1, c3, c5, bias, e.x, m1.x, p1.x, m3.x, p3.x, m5.x, p5.x),
+                               tap7(c0, c1, c3, c5, bias, e.y, m1.y, p1.y, m3.y, p3.y, m5.y, p5.y),
+                               tap7(c0, c1, c3, c5, bias, e.z, m1.z, p1.z, m3.z, p3.z, m5.z, p5.z),
+                               tap7(c0, c1, c3, c5, bias, e.w, m1.w, p1.w, m3.w, p3.w, m5.w, p5.w));
+                }
             }
-            const float4 m5 = ring[(u + 3) % 6], m3 = ring[(u + 4) % 6], m1 = ring[(u + 5) % 6];
-            const float4 p1 = ring[u % 6], p3 = ring[(u + 1) % 6], p5 = ring[(u + 2) % 6];
-            const uint32_t d = pack4b(tap7(c0, c1, c3, c5, bias, e.x, m1.x, p1.x, m3.x, p3.x, m5.x, p5.x),
-                                      tap7(c0, c1, c3, c5, bias, e.y, m1.y, p1.y, m3.y, p3.y, m5.y, p5.y),
-                                      tap7(c0, c1, c3, c5, bias, e.z, m1.z, p1.z, m3.z, p3.z, m5.z, p5.z),
-                                      tap7(c0, c1, c3, c5, bias, e.w, m1.w, p1.w, m3.w, p3.w, m5.w, p5.w));
             if (G::ND >= kThreads || tid < G::ND) L[u * kPitch + tid] = d;
         }
         if (edge) {  // replicate the edge pixels (EXTEND_COPY) inside the LDS image
@@ -377,6 +409,12 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
                 win[12] = row[W0 * j + 12];
             }
             float o[K][B];
+            if (MEM) {  // diagnostic: skip the arithmetic, keep the LDS reads and stores
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+#pragma unroll
+                    for (int c = 0; c < B; ++c) o[k][c] = __uint_as_float(win[(k * B + c) % 13] & 0x437f0000u);
+            } else
 #pragma unroll
             for (int c = 0; c < B; ++c) {
                 // px[t]: intermediate pixel 2x - 5 + t of channel c
@@ -406,7 +444,12 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
                 const uint32_t d1 = pack4b(o[1][1], o[1][2], o[2][0], o[2][1]);
                 const uint32_t d2 = pack4b(o[2][2], o[3][0], o[3][1], o[3][2]);
                 if (full && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
-                    *reinterpret_cast<uint3 *>(q) = uint3{d0, d1, d2};
+                    if (NTS) {
+                        typedef uint32_t u3v __attribute__((ext_vector_type(3)));
+                        __builtin_nontemporal_store(u3v{d0, d1, d2}, reinterpret_cast<u3v *>(q));
+                    } else {
+                        *reinterpret_cast<uint3 *>(q) = uint3{d0, d1, d2};
+                    }
                 } else {
                     const uint32_t dd[3] = {d0, d1, d2};
                     const int nb = (full ? K : a.ow - x) * B;
@@ -430,11 +473,19 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 }
 
 // Variant bits (A/B in one process via MIPX_R2_VARIANT; default = best measured):
-// bit 0: R = 6 (else 12), bit 1: register prefetch of the next chunk.
+// bit 0: R = 6 (else 12), bit 1: register prefetch of the next chunk,
+// bit 2: packed-FP32 vertical taps, bit 3: memory-only diagnostic (not exact),
+// bit 4: non-temporal loads, bit 5: non-temporal stores.  Measured in
+// profiles/r01/v7_variants_ab.log: the memory-only build is no faster than the
+// full one (the arithmetic is hidden), packed math and nt hints lose.
 template <int B, int VAR>
 __global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
     constexpr int R = (VAR & 1) ? 6 : 12;
     constexpr bool PF = (VAR & 2) != 0;
+    constexpr bool PK = (VAR & 4) != 0;
+    constexpr bool MEM = (VAR & 8) != 0;
+    constexpr int LAUX = (VAR & 16) ? 2 : 0;  // bit 4: non-temporal loads (cache policy nt)
+    constexpr bool NTS = (VAR & 32) != 0;     // bit 5: non-temporal stores
     __shared__ uint32_t lds[2 * R * kPitch];
     const uint32_t t = a.remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     int strip, band, img;
@@ -449,7 +500,7 @@ __global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
         band = rest % a.n_bands;
         img = rest / a.n_bands;
     }
-    reduce2_tile<B, R, PF>(a, img, strip, band, lds);
+    reduce2_tile<B, R, PF, PK, MEM, LAUX, NTS>(a, img, strip, band, lds);
 }
 
 
@@ -553,7 +604,10 @@ int reduce2_variant() {
     const char *e = std::getenv("MIPX_R2_VARIANT");
     if (!e || !*e) return kR2Default;
     const int v = std::atoi(e);
-    return (v >= 0 && v <= 3) ? v : kR2Default;
+    switch (v) {
+        case 0: case 1: case 2: case 3: case 6: case 10: return v;
+        default: return kR2Default;
+    }
 }
 
 int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_t st) {
@@ -596,7 +650,7 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
         else hipLaunchKernelGGL((k_reduce2x2<4, V>), grid, dim3(kThreads), 0, st, a);        \
         break;
     switch (var) {
-        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3)
+        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3) MIPX_R2(6) MIPX_R2(10)
         default: return MIPX_EINVAL;
     }
 #undef MIPX_R2
