@@ -7,8 +7,7 @@
 // kernels are bit-identical to the integer C path.
 //
 //  * k_reduce2x2     fused reducev -> reduceh for shrink 2 x 2 (north star C2)
-//  * k_reducev_gen   any vshrink: per output row one phase (uniform per block)
-//  * k_reduceh_lds   any hshrink: input row span and tap table staged in LDS
+//  * any other shrink: the generic separable passes of k_sep.hip
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,160 +21,6 @@ namespace mipx {
 namespace {
 
 using namespace dev;
-
-// ===========================================================================
-// generic vertical pass: a block = 256 dword columns of one output row (the
-// 1D grid is XCD-remapped so consecutive output rows of one image, which
-// share input rows, run on one XCD); taps are uniform (SGPR) per block.
-// ===========================================================================
-struct RedV {
-    const u8 *in;
-    u8 *out;
-    int row_bytes, h, oh, col_blocks, pad, taps;
-    double shrink;
-    const float *tab;
-    long long in_img, out_img;
-};
-
-template <bool DWORD>
-__global__ void __launch_bounds__(256) k_reducev_gen(RedV a) {
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int cb = t % a.col_blocks;
-    const int rest = t / a.col_blocks;
-    const int y = rest % a.oh;
-    const int img = rest / a.oh;
-    const int j = (cb * 256 + threadIdx.x) * 4;
-    if (j >= a.row_bytes) return;
-    const double Y = y * a.shrink;
-    const int iy = static_cast<int>(Y);
-    const int ty = ((static_cast<int>(Y * 256.0) & 255) + 1) >> 1;
-    const float *c = a.tab + ty * a.taps;
-    const u8 *src = a.in + img * a.in_img;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const int nb = min(4, a.row_bytes - j);
-    if (DWORD) {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
-        for (int i = 0; i < a.taps; ++i) {
-            const int r = clampi(iy + i - a.pad, 0, a.h - 1);
-            const uint32_t v = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, j, r * a.row_bytes, 0));
-            const float ci = c[i];
-            acc[0] = __builtin_fmaf(ci, ubyte_f<0>(v), acc[0]);
-            acc[1] = __builtin_fmaf(ci, ubyte_f<1>(v), acc[1]);
-            acc[2] = __builtin_fmaf(ci, ubyte_f<2>(v), acc[2]);
-            acc[3] = __builtin_fmaf(ci, ubyte_f<3>(v), acc[3]);
-        }
-        uint32_t o = fixed_round_u(acc[0]) | (fixed_round_u(acc[1]) << 8) | (fixed_round_u(acc[2]) << 16) |
-                     (fixed_round_u(acc[3]) << 24);
-        *reinterpret_cast<uint32_t *>(a.out + img * a.out_img + static_cast<size_t>(y) * a.row_bytes + j) = o;
-    } else {
-        for (int i = 0; i < a.taps; ++i) {
-            const int r = clampi(iy + i - a.pad, 0, a.h - 1);
-            const u8 *p = src + static_cast<size_t>(r) * a.row_bytes + j;
-            const float ci = c[i];
-            for (int k = 0; k < nb; ++k) acc[k] = __builtin_fmaf(ci, static_cast<float>(p[k]), acc[k]);
-        }
-        u8 *q = a.out + img * a.out_img + static_cast<size_t>(y) * a.row_bytes + j;
-        for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(fixed_round_u(acc[k]));
-    }
-}
-
-// ===========================================================================
-// generic horizontal pass: a block = 256 output pixels of one row.  The input
-// pixels the block's taps touch (COPY-clamped) are staged once in LDS as one
-// packed u32 per pixel, the 129-phase tap table beside them; each lane then
-// reads its taps from LDS.
-// ===========================================================================
-struct RedH {
-    const u8 *in;
-    u8 *out;
-    int w, h, ow, x_blocks, pad, taps, span_max;
-    double shrink;
-    const float *tab;
-    long long in_img, out_img;
-};
-
-template <int B>
-__global__ void __launch_bounds__(256) k_reduceh_lds(RedH a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    float *ctab = reinterpret_cast<float *>(smem);
-    uint32_t *spx = smem + (kTransformScale + 1) * a.taps;
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int xb = t % a.x_blocks;
-    const int rest = t / a.x_blocks;
-    const int y = rest % a.h;
-    const int img = rest / a.h;
-    const int x0 = xb * 256;
-    const int x_last = min(x0 + 255, a.ow - 1);
-    const int lo = static_cast<int>(x0 * a.shrink) - a.pad;
-    const int hi = static_cast<int>(x_last * a.shrink) + a.taps - 1 - a.pad;
-    const int span = hi - lo + 1;
-    for (int i = threadIdx.x; i < (kTransformScale + 1) * a.taps; i += 256) ctab[i] = a.tab[i];
-    const u8 *row = a.in + img * a.in_img + static_cast<size_t>(y) * a.w * B;
-    for (int p = threadIdx.x; p < span; p += 256) {
-        const u8 *s = row + clampi(lo + p, 0, a.w - 1) * B;
-        uint32_t v;
-        if (B == 4) {
-            v = *reinterpret_cast<const uint32_t *>(s);
-        } else {
-            v = s[0];
-            if (B > 1) v |= static_cast<uint32_t>(s[1]) << 8;
-            if (B > 2) v |= static_cast<uint32_t>(s[2]) << 16;
-        }
-        spx[p] = v;
-    }
-    __syncthreads();
-    const int x = x0 + threadIdx.x;
-    if (x > x_last) return;
-    const double X = x * a.shrink;
-    const int ix = static_cast<int>(X);
-    const int tx = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
-    const float *c = ctab + tx * a.taps;
-    const uint32_t *sp = spx + (ix - a.pad - lo);
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < a.taps; ++i) {
-        const uint32_t v = sp[i];
-        const float ci = c[i];
-        acc[0] = __builtin_fmaf(ci, ubyte_f<0>(v), acc[0]);
-        if (B > 1) acc[1] = __builtin_fmaf(ci, ubyte_f<1>(v), acc[1]);
-        if (B > 2) acc[2] = __builtin_fmaf(ci, ubyte_f<2>(v), acc[2]);
-        if (B > 3) acc[3] = __builtin_fmaf(ci, ubyte_f<3>(v), acc[3]);
-    }
-    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
-    if (B == 4) {
-        *reinterpret_cast<uint32_t *>(q) = fixed_round_u(acc[0]) | (fixed_round_u(acc[1]) << 8) |
-                                           (fixed_round_u(acc[2]) << 16) | (fixed_round_u(acc[3]) << 24);
-    } else {
-#pragma unroll
-        for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_u(acc[z]));
-    }
-}
-
-// horizontal pass without LDS staging, for shrinks whose span exceeds the LDS
-// budget: taps gathered through L1
-template <int B>
-__global__ void __launch_bounds__(256) k_reduceh_gather(RedH a) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    const int img = blockIdx.z;
-    if (x >= a.ow) return;
-    const double X = x * a.shrink;
-    const int ix = static_cast<int>(X);
-    const int tx = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
-    const float *c = a.tab + tx * a.taps;
-    const u8 *row = a.in + img * a.in_img + static_cast<size_t>(y) * a.w * B;
-    float acc[B];
-#pragma unroll
-    for (int z = 0; z < B; ++z) acc[z] = 0.f;
-    for (int i = 0; i < a.taps; ++i) {
-        const u8 *p = row + clampi(ix + i - a.pad, 0, a.w - 1) * B;
-        const float ci = c[i];
-#pragma unroll
-        for (int z = 0; z < B; ++z) acc[z] = __builtin_fmaf(ci, static_cast<float>(p[z]), acc[z]);
-    }
-    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
-#pragma unroll
-    for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_u(acc[z]));
-}
 
 // ===========================================================================
 // Lanczos3 reduce by exactly 2 x 2, fused reducev -> reduceh (the north-star
@@ -510,61 +355,68 @@ __global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
 // launchers
 // ===========================================================================
 int reducev_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double vshrink, hipStream_t st) {
-    int taps = 0;
-    const float *tab = device_reduce_table(vshrink, &taps);
-    if (!tab) return MIPX_EDEVICE;
-    RedV a{};
-    a.in = in;
-    a.out = out;
-    a.row_bytes = w * b;
-    a.h = h;
-    a.oh = out_size_reduce(h, vshrink);
-    a.col_blocks = (a.row_bytes / 4 + 1 + 255) / 256;
-    a.pad = taps / 2 - 1;
-    a.taps = taps;
-    a.shrink = vshrink;
-    a.tab = tab;
-    a.in_img = img_bytes(w, h, b);
-    a.out_img = img_bytes(w, a.oh, b);
-    const long long blocks = static_cast<long long>(a.col_blocks) * a.oh * n;
-    if (!grid_ok(blocks)) return MIPX_EINVAL;
-    const bool dword = (a.row_bytes % 4) == 0 && (reinterpret_cast<uintptr_t>(in) % 4) == 0 &&
-                       (reinterpret_cast<uintptr_t>(out) % 4) == 0 && a.in_img < 0x7fffffffLL;
-    if (dword) hipLaunchKernelGGL(k_reducev_gen<true>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_reducev_gen<false>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, a);
-    return launch_check("k_reducev_gen");
+    SepSpec spec;
+    if (!sep_spec_reduce(vshrink, &spec)) return MIPX_EDEVICE;
+    SepWindow win{};
+    win.bands = b;
+    win.in_pitch = w * b;
+    win.in_base = 0;
+    win.in_img = img_bytes(w, h, b);
+    win.in_len = h;
+    win.o0 = 0;
+    win.out_w = w;
+    win.out_h = out_size_reduce(h, vshrink);
+    return vpass_launch(in, out, n, spec, win, st);
 }
 
 int reduceh_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hshrink, hipStream_t st) {
-    int taps = 0;
-    const float *tab = device_reduce_table(hshrink, &taps);
-    if (!tab) return MIPX_EDEVICE;
-    RedH a{};
-    a.in = in;
-    a.out = out;
-    a.w = w;
-    a.h = h;
-    a.ow = out_size_reduce(w, hshrink);
-    a.x_blocks = (a.ow + 255) / 256;
-    a.pad = taps / 2 - 1;
-    a.taps = taps;
-    a.shrink = hshrink;
-    a.tab = tab;
-    a.in_img = img_bytes(w, h, b);
-    a.out_img = img_bytes(a.ow, h, b);
-    a.span_max = static_cast<int>(std::ceil(255 * hshrink)) + taps + 2;
-    const size_t lds = (static_cast<size_t>(kTransformScale + 1) * taps + a.span_max) * 4;
-    const bool aligned4 = b != 4 || ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 4) == 0;
-    if (lds <= 48 * 1024 && aligned4) {
-        const long long blocks = static_cast<long long>(a.x_blocks) * h * n;
-        if (!grid_ok(blocks)) return MIPX_EINVAL;
-        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduceh_lds<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256),
-                                                  lds, st, a));
-        return launch_check("k_reduceh_lds");
+    SepSpec spec;
+    if (!sep_spec_reduce(hshrink, &spec)) return MIPX_EDEVICE;
+    SepWindow win{};
+    win.bands = b;
+    win.in_pitch = w * b;
+    win.in_base = 0;
+    win.in_img = img_bytes(w, h, b);
+    win.in_len = w;
+    win.o0 = 0;
+    win.out_w = out_size_reduce(w, hshrink);
+    win.out_h = h;
+    return hpass_launch(in, out, n, spec, win, st);
+}
+
+// vips_reduce followed by vips_extract_area(left, top, ow, oh): only the
+// window's output rows (vertical pass) and columns (horizontal pass) are
+// computed.  Every output is the same sum over the same input pixels, so the
+// result is identical to reduce-then-extract, minus the discarded work and the
+// extract pass.  ws: n * w * oh * b bytes when both shrinks are > 1.
+int reduce_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int left,
+                         int top, int ow, int oh, void *ws, size_t ws_bytes, hipStream_t st) {
+    const int rw = hs > 1.0 ? out_size_reduce(w, hs) : w;
+    const int rh = vs > 1.0 ? out_size_reduce(h, vs) : h;
+    if (left < 0 || top < 0 || ow <= 0 || oh <= 0 || left + ow > rw || top + oh > rh) return MIPX_EINVAL;
+    const long long in_img = img_bytes(w, h, b);
+    SepSpec sv, sh;
+    if (vs > 1.0 && !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
+    if (hs > 1.0 && !sep_spec_reduce(hs, &sh)) return MIPX_EDEVICE;
+    if (vs > 1.0 && hs > 1.0) {
+        const size_t need = align_up(static_cast<size_t>(n) * w * oh * b);
+        if (!ws || ws_bytes < need) return MIPX_EINVAL;
+        u8 *tmp = static_cast<u8 *>(ws);
+        const SepWindow v{b, w * b, 0, in_img, h, top, w, oh};
+        int e = vpass_launch(in, tmp, n, sv, v, st);
+        if (e) return e;
+        const SepWindow hw{b, w * b, 0, img_bytes(w, oh, b), w, left, ow, oh};
+        return hpass_launch(tmp, out, n, sh, hw, st);
     }
-    dim3 grid((a.ow + 255) / 256, h, n);
-    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduceh_gather<B_>, grid, dim3(256), 0, st, a));
-    return launch_check("k_reduceh_gather");
+    if (vs > 1.0) {
+        const SepWindow v{b, w * b, static_cast<long long>(left) * b, in_img, h, top, ow, oh};
+        return vpass_launch(in, out, n, sv, v, st);
+    }
+    if (hs > 1.0) {
+        const SepWindow hw{b, w * b, static_cast<long long>(top) * w * b, in_img, w, left, ow, oh};
+        return hpass_launch(in, out, n, sh, hw, st);
+    }
+    return extract_launch(in, out, n, w, h, b, left, top, ow, oh, st);
 }
 
 // Is the phase-0 mask of shrink 2 the 7-nonzero symmetric shape the fused

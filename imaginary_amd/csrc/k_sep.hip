@@ -1,0 +1,537 @@
+// k_sep.hip — the generic separable passes behind libvips vips_reduce
+// (reducev -> reduceh, Lanczos3, any shrink) and vips_gaussblur (convsep:
+// horizontal 1 x n mask, then vertical), on gfx950.
+//
+// Both libvips ops are "one 1-D integer mask per output position, uchar result":
+//   reduce (reducev.cpp / reduceh.cpp): position o samples X = o * shrink, taps
+//     start at floor(X) - (n/2 - 1), phase ((int(X*256) & 255) + 1) >> 1 of the
+//     129-phase 12-bit table, result (sum + 2048) >> 12 clipped;
+//   conv (convi.c via convsep): position o starts at o - n/2, one mask, result
+//     (sum + (scale+1)/2) / scale clipped;
+// both with EXTEND_COPY edges (restated in oracle/vips_ref.c).  Sums are
+// integers below 2^24, so fp32 FMAs reproduce them exactly in any order.
+//
+//  * k_vpass<KR, MODE, DW>: lanes own 4-byte columns of the row (channel
+//    agnostic); a block makes KR consecutive output rows by streaming each
+//    input row it needs ONCE (loads batched 8 deep) and adding it into every
+//    output row whose window contains it (wave-uniform predicate, taps from LDS).
+//  * k_hpass<B, RB, MODE>: a block = 256 output pixels x RB rows; the input
+//    spans are staged in LDS as one u32 per pixel (dword-coalesced loads, then a
+//    repack with the COPY edge), each lane reads its taps from LDS.
+// Both take a window (row / column offset and clamp range), so an extract that
+// follows a reduce or precedes a blur folds into the pass (mipx_runtime.cpp).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "device_common.h"
+
+namespace mipx {
+namespace {
+
+using namespace dev;
+
+struct SepTaps {
+    const float *tab;        // phased: (kTransformScale + 1) x taps, else 1 x taps
+    int taps, pad, phased;
+    double shrink;
+    float rounding, inv_scale;  // conv rounding
+};
+
+__device__ __forceinline__ void sep_position(const SepTaps &t, int o, int *start, int *phase) {
+    if (t.phased) {
+        const double X = o * t.shrink;
+        *start = static_cast<int>(X) - t.pad;
+        *phase = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
+    } else {
+        *start = o - t.pad;
+        *phase = 0;
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t sep_round(float acc, const SepTaps &t) {
+    if (MODE == kSepReduce) return fixed_round_u(acc);
+    return min(div_floor(acc + t.rounding, t.inv_scale), 255u);
+}
+
+// ===========================================================================
+// vertical pass
+// ===========================================================================
+struct VPassArgs {
+    const u8 *in;
+    u8 *out;
+    int row_bytes;        // bytes per output row == bytes the pass covers per input row
+    int in_pitch;         // bytes between input rows
+    long long in_base;    // byte offset of local input (row 0, first column) in an image
+    long long in_img, out_img;
+    int hl;               // local input rows (COPY clamp range)
+    int oy0, oh;          // output rows [oy0, oy0 + oh) in op-output coordinates
+    int col_blocks, kr_blocks;
+    int kr;               // output rows per block
+    int lrows;            // LDS input-row capacity (>= (kr - 1) * shrink + taps + 1)
+    SepTaps tp;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ lds_void *to_lds(void *p) { return (lds_void *)p; }  // generic -> LDS addrspacecast
+
+// DMA: 16 / 4 = bytes per lane of the direct-to-LDS buffer loads (alignment
+// permitting), 0 = register-staged byte loads.
+template <int MODE, int DMA>
+__global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t vsm[];
+    uint32_t *rows = vsm;                                          // lrows x 256 dwords
+    float *vcoef = reinterpret_cast<float *>(vsm + a.lrows * 256);  // kr x taps
+    int *soff = reinterpret_cast<int *>(vcoef + a.kr * a.tp.taps);  // kr start rows
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int cb = t % a.col_blocks;
+    const int rest = t / a.col_blocks;
+    const int kb = rest % a.kr_blocks;
+    const int img = rest / a.kr_blocks;
+    const int taps = a.tp.taps;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: no waterfall around the DMA
+    const int y0 = kb * a.kr;
+    const int nk = min(a.kr, a.oh - y0);
+    int r_lo, r_last, ph;
+    sep_position(a.tp, a.oy0 + y0, &r_lo, &ph);
+    sep_position(a.tp, a.oy0 + y0 + nk - 1, &r_last, &ph);
+    const int L = r_last + taps - r_lo;
+    // ---- stage the L input rows of this 1 KiB column block in LDS ----
+    const u8 *src = a.in + img * a.in_img;
+    const long long col0 = a.in_base + static_cast<long long>(cb) * 1024;
+    if (DMA == 16) {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
+        for (int l = wave; l < L; l += 4) {
+            const int r = clampi(r_lo + l, 0, a.hl - 1);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * 256), 16,
+                                                     static_cast<int>(col0) + lane * 16, r * a.in_pitch, 0, 0);
+        }
+    } else if (DMA == 4) {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
+        for (int l = 0; l < L; ++l) {
+            const int r = clampi(r_lo + l, 0, a.hl - 1);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * 256 + wave * 64), 4,
+                                                     static_cast<int>(col0) + wave * 256 + lane * 4,
+                                                     r * a.in_pitch, 0, 0);
+        }
+    } else {
+        const int j = cb * 1024 + tid * 4;
+        const int nb = max(0, min(4, a.row_bytes - j));
+        for (int l = 0; l < L; ++l) {
+            const int r = clampi(r_lo + l, 0, a.hl - 1);
+            const u8 *p = src + a.in_base + static_cast<long long>(r) * a.in_pitch + j;
+            uint32_t v = 0;
+            for (int z = 0; z < nb; ++z) v |= static_cast<uint32_t>(p[z]) << (8 * z);
+            rows[l * 256 + tid] = v;
+        }
+    }
+    for (int i = tid; i < nk * taps; i += 256) {
+        const int k = i / taps;
+        int s;
+        sep_position(a.tp, a.oy0 + y0 + k, &s, &ph);
+        vcoef[i] = a.tp.tab[ph * taps + (i - k * taps)];
+    }
+    if (tid < nk) {
+        int s;
+        sep_position(a.tp, a.oy0 + y0 + tid, &s, &ph);
+        soff[tid] = s - r_lo;
+    }
+    __syncthreads();
+    // ---- KR output rows from LDS ----
+    const int j = cb * 1024 + tid * 4;
+    if (j >= a.row_bytes) return;
+    const int nb = min(4, a.row_bytes - j);
+    u8 *dst = a.out + img * a.out_img + static_cast<long long>(y0) * a.row_bytes + j;
+    for (int k = 0; k < nk; ++k) {
+        const uint32_t *rp = rows + soff[k] * 256 + tid;
+        const float *ck = vcoef + k * taps;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 4
+        for (int i = 0; i < taps; ++i) {
+            const uint32_t v = rp[i * 256];
+            const float c = ck[i];
+            a0 = __builtin_fmaf(c, ubyte_f<0>(v), a0);
+            a1 = __builtin_fmaf(c, ubyte_f<1>(v), a1);
+            a2 = __builtin_fmaf(c, ubyte_f<2>(v), a2);
+            a3 = __builtin_fmaf(c, ubyte_f<3>(v), a3);
+        }
+        const uint32_t o = sep_round<MODE>(a0, a.tp) | (sep_round<MODE>(a1, a.tp) << 8) |
+                           (sep_round<MODE>(a2, a.tp) << 16) | (sep_round<MODE>(a3, a.tp) << 24);
+        u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
+        if (nb == 4 && (a.row_bytes & 3) == 0 && (a.out_img & 3) == 0) {
+            *reinterpret_cast<uint32_t *>(q) = o;
+        } else {
+            for (int z = 0; z < nb; ++z) q[z] = static_cast<u8>(o >> (8 * z));
+        }
+    }
+}
+
+// vertical pass for masks too tall for LDS staging: taps gathered through L1
+template <int MODE>
+__global__ void __launch_bounds__(256) k_vpass_gather(VPassArgs a) {
+    const int j = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const int y = blockIdx.y;
+    const int img = blockIdx.z;
+    if (j >= a.row_bytes) return;
+    const int nb = min(4, a.row_bytes - j);
+    int s, ph;
+    sep_position(a.tp, a.oy0 + y, &s, &ph);
+    const float *c = a.tp.tab + ph * a.tp.taps;
+    const u8 *src = a.in + img * a.in_img + a.in_base + j;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int i = 0; i < a.tp.taps; ++i) {
+        const u8 *p = src + static_cast<long long>(clampi(s + i, 0, a.hl - 1)) * a.in_pitch;
+        const float ci = c[i];
+        for (int z = 0; z < nb; ++z) acc[z] = __builtin_fmaf(ci, static_cast<float>(p[z]), acc[z]);
+    }
+    u8 *q = a.out + img * a.out_img + static_cast<long long>(y) * a.row_bytes + j;
+    for (int z = 0; z < nb; ++z) q[z] = static_cast<u8>(sep_round<MODE>(acc[z], a.tp));
+}
+
+// ===========================================================================
+// horizontal pass
+// ===========================================================================
+struct HPassArgs {
+    const u8 *in;
+    u8 *out;
+    int in_pitch;         // bytes between input rows
+    long long in_base;    // byte offset of local input (row 0, column 0) in an image
+    long long in_img, out_img;
+    int wl;               // local input width, pixels (COPY clamp range)
+    int rows;             // rows processed == output rows
+    int ox0, ow;          // output columns [ox0, ox0 + ow) in op-output coordinates
+    int x_blocks, rb_blocks;
+    int span_max;         // LDS pixels per staged row (incl. 64 of DMA overrun)
+    int raw_max;          // LDS dwords per staged raw row (B < 4; incl. 64 of overrun)
+    int ntab;             // floats of the tap table staged in LDS (0: taps in registers)
+    SepTaps tp;
+};
+
+template <int B>
+__device__ __forceinline__ uint32_t load_px_g(const u8 *p) {
+    uint32_t v = p[0];
+    if (B > 1) v |= static_cast<uint32_t>(p[1]) << 8;
+    if (B > 2) v |= static_cast<uint32_t>(p[2]) << 16;
+    if (B > 3) v |= static_cast<uint32_t>(p[3]) << 24;
+    return v;
+}
+
+// DW: rows dword aligned -> direct-to-LDS dword DMA of the span (B = 4) or of
+// its raw bytes (B < 4, repacked in LDS); else register-staged byte loads.
+// TREG > 0: each lane holds its (<= TREG) taps in registers (reduce); 0: taps
+// from the LDS table.
+template <int B, int RB, int MODE, bool DW, int TREG>
+__global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hsm[];
+    float *ctab = reinterpret_cast<float *>(hsm);
+    uint32_t *spx = hsm + a.ntab;
+    uint32_t *raw = spx + RB * a.span_max;
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int rb = rest % a.rb_blocks;
+    const int img = rest / a.rb_blocks;
+    const int taps = a.tp.taps;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: no waterfall around the DMA
+    const int x0 = xb * 256;
+    const int x_last = min(x0 + 255, a.ow - 1);
+    int lo, hi, ph;
+    sep_position(a.tp, a.ox0 + x0, &lo, &ph);
+    sep_position(a.tp, a.ox0 + x_last, &hi, &ph);
+    hi += taps - 1;
+    const int span = hi - lo + 1;
+    const int y_first = rb * RB;
+    const int nr = min(RB, a.rows - y_first);
+    const int cl = max(lo, 0), ch = min(hi, a.wl - 1);  // pixels actually inside the row
+    const u8 *img_base = a.in + img * a.in_img;
+    const long long row0 = a.in_base + static_cast<long long>(y_first) * a.in_pitch;
+    int bs = 0, a4 = 0, skew = 0;
+    if (DW) {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(img_base, a.in_img);
+        if (B == 4) {
+            const int chunks = (ch - cl + 1 + 63) >> 6;
+            for (int idx = wave; idx < nr * chunks; idx += 4) {
+                const int rr = idx / chunks, q = idx - rr * chunks;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, to_lds(spx + rr * a.span_max + (cl - lo) + q * 64), 4,
+                    static_cast<int>(row0) + 4 * (cl + q * 64 + lane), rr * a.in_pitch, 0, 0);
+            }
+        } else {
+            bs = B * cl;
+            a4 = bs & ~3;
+            skew = bs - a4;
+            const int nd = (B * (ch - cl + 1) + skew + 3) >> 2;
+            const int chunks = (nd + 63) >> 6;
+            for (int idx = wave; idx < nr * chunks; idx += 4) {
+                const int rr = idx / chunks, q = idx - rr * chunks;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, to_lds(raw + rr * a.raw_max + q * 64), 4,
+                    static_cast<int>(row0) + a4 + 4 * (q * 64 + lane), rr * a.in_pitch, 0, 0);
+            }
+        }
+    } else {
+        const u8 *src = img_base + row0;
+        for (int i = tid; i < nr * span; i += 256) {
+            const int rr = i / span, p = i - rr * span;
+            const int c = clampi(lo + p, 0, a.wl - 1);
+            spx[rr * a.span_max + p] = load_px_g<B>(src + static_cast<long long>(rr) * a.in_pitch + c * B);
+        }
+    }
+    // this lane's taps
+    const int x = x0 + tid;
+    int s = 0, xph = 0;
+    sep_position(a.tp, a.ox0 + min(x, x_last), &s, &xph);
+    float cr[TREG > 0 ? TREG : 1];
+    if (TREG > 0) {
+        const float *c = a.tp.tab + xph * taps;
+#pragma unroll
+        for (int i = 0; i < TREG; ++i) cr[i] = i < taps ? c[i] : 0.f;
+    } else {
+        for (int i = tid; i < a.ntab; i += 256) ctab[i] = a.tp.tab[i];
+    }
+    __syncthreads();
+    if (DW) {  // COPY edges (B = 4) or the repack of the raw bytes (B < 4)
+        if (B == 4) {
+            const int nl = cl - lo, nrt = hi - ch;
+            for (int i = tid; i < nr * (nl + nrt); i += 256) {
+                const int rr = i / (nl + nrt), f = i - rr * (nl + nrt);
+                uint32_t *row = spx + rr * a.span_max;
+                if (f < nl) row[f] = row[nl];
+                else row[ch - lo + 1 + (f - nl)] = row[ch - lo];
+            }
+        } else {
+            const u8 *rb8 = reinterpret_cast<const u8 *>(raw);
+            for (int i = tid; i < nr * span; i += 256) {
+                const int rr = i / span, p = i - rr * span;
+                const int c = clampi(lo + p, 0, a.wl - 1);
+                const u8 *q = rb8 + rr * a.raw_max * 4 + (c - cl) * B + skew;
+                uint32_t v = q[0];
+                if (B > 1) v |= static_cast<uint32_t>(q[1]) << 8;
+                if (B > 2) v |= static_cast<uint32_t>(q[2]) << 16;
+                spx[rr * a.span_max + p] = v;
+            }
+        }
+        __syncthreads();
+    }
+    if (x > x_last) return;
+    const uint32_t *sp = spx + (s - lo);
+    float acc[RB][B];
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int z = 0; z < B; ++z) acc[r][z] = 0.f;
+    auto tap = [&](int i, float ci) {
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            if (r < nr) {
+                const uint32_t v = sp[r * a.span_max + i];
+#pragma unroll
+                for (int z = 0; z < B; ++z) {
+                    const float pz = z == 0 ? ubyte_f<0>(v) : z == 1 ? ubyte_f<1>(v) : z == 2 ? ubyte_f<2>(v) : ubyte_f<3>(v);
+                    acc[r][z] = __builtin_fmaf(ci, pz, acc[r][z]);
+                }
+            }
+        }
+    };
+    if (TREG > 0) {
+#pragma unroll
+        for (int i = 0; i < TREG; ++i)
+            if (i < taps) tap(i, cr[i]);
+    } else {
+        const float *c = ctab + xph * taps;
+        for (int i = 0; i < taps; ++i) tap(i, c[i]);
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        if (r >= nr) continue;
+        u8 *q = a.out + img * a.out_img + (static_cast<long long>(y_first + r) * a.ow + x) * B;
+        if (B == 4) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int z = 0; z < B; ++z) o |= sep_round<MODE>(acc[r][z], a.tp) << (8 * z);
+            *reinterpret_cast<uint32_t *>(q) = o;
+        } else {
+#pragma unroll
+            for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(sep_round<MODE>(acc[r][z], a.tp));
+        }
+    }
+}
+
+// horizontal reduce without LDS staging, for shrinks whose span exceeds the
+// LDS budget: taps gathered through L1
+template <int B>
+__global__ void __launch_bounds__(256) k_hpass_gather(HPassArgs a) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int img = blockIdx.z;
+    if (x >= a.ow) return;
+    int s, ph;
+    sep_position(a.tp, a.ox0 + x, &s, &ph);
+    const float *c = a.tp.tab + ph * a.tp.taps;
+    const u8 *row = a.in + img * a.in_img + a.in_base + static_cast<long long>(y) * a.in_pitch;
+    float acc[B];
+#pragma unroll
+    for (int z = 0; z < B; ++z) acc[z] = 0.f;
+    for (int i = 0; i < a.tp.taps; ++i) {
+        const u8 *p = row + clampi(s + i, 0, a.wl - 1) * B;
+        const float ci = c[i];
+#pragma unroll
+        for (int z = 0; z < B; ++z) acc[z] = __builtin_fmaf(ci, static_cast<float>(p[z]), acc[z]);
+    }
+    u8 *q = a.out + img * a.out_img + (static_cast<long long>(y) * a.ow + x) * B;
+#pragma unroll
+    for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_u(acc[z]));
+}
+
+bool aligned4(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
+
+SepTaps make_taps(const SepSpec &s) {
+    SepTaps t{};
+    t.tab = s.tab;
+    t.taps = s.taps;
+    t.phased = s.mode == kSepReduce;
+    t.pad = t.phased ? s.taps / 2 - 1 : s.taps / 2;
+    t.shrink = s.shrink;
+    t.rounding = static_cast<float>((s.scale + 1) / 2);
+    t.inv_scale = s.scale > 0 ? 1.0f / s.scale : 1.0f;
+    return t;
+}
+
+}  // namespace
+
+bool sep_spec_reduce(double shrink, SepSpec *s) {
+    int taps = 0;
+    s->tab = device_reduce_table(shrink, &taps);
+    if (!s->tab) return false;
+    s->taps = taps;
+    s->mode = kSepReduce;
+    s->shrink = shrink;
+    s->scale = 0;
+    return true;
+}
+
+int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWindow &w, hipStream_t st) {
+    VPassArgs a{};
+    a.in = in;
+    a.out = out;
+    a.row_bytes = w.out_w * w.bands;
+    a.in_pitch = w.in_pitch;
+    a.in_base = w.in_base;
+    a.in_img = w.in_img;
+    a.out_img = static_cast<long long>(a.row_bytes) * w.out_h;
+    a.hl = w.in_len;
+    a.oy0 = w.o0;
+    a.oh = w.out_h;
+    a.tp = make_taps(spec);
+    const int taps = a.tp.taps;
+    const double s = spec.mode == kSepReduce ? spec.shrink : 1.0;
+    if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
+    a.col_blocks = (a.row_bytes + 1023) / 1024;
+    // rows per block: fill ~40 staged input rows (40 KiB of LDS)
+    constexpr int kRowBudget = 40, kRowMax = 60;
+    int kr = taps >= kRowBudget ? 1 : static_cast<int>(std::floor((kRowBudget - taps - 1) / s)) + 1;
+    kr = std::max(1, std::min({kr, 32, a.oh}));
+    a.kr = kr;
+    a.lrows = static_cast<int>(std::ceil((kr - 1) * s)) + taps + 2;
+    a.kr_blocks = (a.oh + kr - 1) / kr;
+    const dim3 blk(256);
+    const size_t lds = static_cast<size_t>(a.lrows) * 1024 + static_cast<size_t>(kr) * taps * 4 + kr * 4;
+    if (a.lrows > kRowMax || lds > 64 * 1024) {  // very tall masks: gather through L1
+        const dim3 grid((a.row_bytes + 1023) / 1024, a.oh, n);
+        if (spec.mode == kSepReduce) hipLaunchKernelGGL(k_vpass_gather<kSepReduce>, grid, blk, 0, st, a);
+        else hipLaunchKernelGGL(k_vpass_gather<kSepConv>, grid, blk, 0, st, a);
+        return launch_check("k_vpass_gather");
+    }
+    const long long blocks = static_cast<long long>(a.col_blocks) * a.kr_blocks * n;
+    if (!grid_ok(blocks)) return MIPX_EINVAL;
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(in);
+    const bool al16 = (ip % 16) == 0 && (a.in_pitch % 16) == 0 && (a.in_base % 16) == 0 && (a.in_img % 16) == 0;
+    const bool al4 = (ip % 4) == 0 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0;
+    const dim3 grid(static_cast<unsigned>(blocks));
+#define MIPX_VP(MODE)                                                                                   \
+    if (al16) hipLaunchKernelGGL((k_vpass<MODE, 16>), grid, blk, lds, st, a);                           \
+    else if (al4) hipLaunchKernelGGL((k_vpass<MODE, 4>), grid, blk, lds, st, a);                        \
+    else hipLaunchKernelGGL((k_vpass<MODE, 0>), grid, blk, lds, st, a);
+    if (spec.mode == kSepReduce) {
+        MIPX_VP(kSepReduce)
+    } else {
+        MIPX_VP(kSepConv)
+    }
+#undef MIPX_VP
+    return launch_check("k_vpass");
+}
+
+int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWindow &w, hipStream_t st) {
+    const int b = w.bands;
+    HPassArgs a{};
+    a.in = in;
+    a.out = out;
+    a.in_pitch = w.in_pitch;
+    a.in_base = w.in_base;
+    a.in_img = w.in_img;
+    a.out_img = static_cast<long long>(w.out_w) * w.out_h * b;
+    a.wl = w.in_len;
+    a.rows = w.out_h;
+    a.ox0 = w.o0;
+    a.ow = w.out_w;
+    a.tp = make_taps(spec);
+    a.x_blocks = (a.ow + 255) / 256;
+    constexpr int kTReg = 16;
+    const bool treg = a.tp.phased && a.tp.taps <= kTReg;
+    a.ntab = treg ? 0 : (((a.tp.phased ? kTransformScale + 1 : 1) * a.tp.taps + 3) & ~3);
+    const double s = a.tp.phased ? spec.shrink : 1.0;
+    a.span_max = static_cast<int>(std::ceil(255 * s)) + a.tp.taps + 2 + 64;
+    a.raw_max = (a.span_max * b + 8 + 3) / 4 + 64;
+    if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
+    const bool dw = (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0 && aligned4(in);
+    if (b == 4 && !(dw && aligned4(out))) return MIPX_EINVAL;
+    auto lds_for = [&](int rb) {
+        return (static_cast<size_t>(a.ntab) + static_cast<size_t>(rb) * a.span_max +
+                (b < 4 && dw ? static_cast<size_t>(rb) * a.raw_max : 0)) * 4;
+    };
+    constexpr size_t kLdsBudget = 40 * 1024;
+    int rb = 8;
+    while (rb > 1 && lds_for(rb) > kLdsBudget) rb >>= 1;
+    if (lds_for(rb) > 64 * 1024) {
+        if (spec.mode != kSepReduce) return MIPX_EUNSUPPORTED;
+        dim3 grid(a.x_blocks, a.rows, n);
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_hpass_gather<B_>, grid, dim3(256), 0, st, a));
+        return launch_check("k_hpass_gather");
+    }
+    a.rb_blocks = (a.rows + rb - 1) / rb;
+    const long long blocks = static_cast<long long>(a.x_blocks) * a.rb_blocks * n;
+    if (!grid_ok(blocks)) return MIPX_EINVAL;
+    const size_t lds = lds_for(rb);
+    const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
+#define MIPX_HP3(RB_, MODE_, DW_, TR_) \
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_hpass<B_, RB_, MODE_, DW_, TR_>), grid, blk, lds, st, a))
+#define MIPX_HP2(RB_)                                                   \
+    if (spec.mode == kSepReduce) {                                      \
+        if (treg) {                                                     \
+            if (dw) { MIPX_HP3(RB_, kSepReduce, true, kTReg) }          \
+            else { MIPX_HP3(RB_, kSepReduce, false, kTReg) }            \
+        } else {                                                        \
+            if (dw) { MIPX_HP3(RB_, kSepReduce, true, 0) }              \
+            else { MIPX_HP3(RB_, kSepReduce, false, 0) }                \
+        }                                                               \
+    } else {                                                            \
+        if (dw) { MIPX_HP3(RB_, kSepConv, true, 0) }                    \
+        else { MIPX_HP3(RB_, kSepConv, false, 0) }                      \
+    }
+    switch (rb) {
+        case 8: MIPX_HP2(8) break;
+        case 4: MIPX_HP2(4) break;
+        case 2: MIPX_HP2(2) break;
+        default: MIPX_HP2(1) break;
+    }
+#undef MIPX_HP2
+#undef MIPX_HP3
+    return launch_check("k_hpass");
+}
+
+}  // namespace mipx

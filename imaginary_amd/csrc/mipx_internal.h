@@ -53,12 +53,39 @@ int resize_schedule(int w, int h, double hscale, double vscale, ResizeSchedule &
 // float copy of reduce_table(shrink) resident on the current device.
 const float *device_reduce_table(double shrink, int *n_taps);
 const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt]
+// float copy of the integer gaussmat mask; *scale = mask sum
+const float *device_gauss_table(double sigma, double min_ampl, int *n_taps, int *scale);
 void free_device_tables();
+
+// ---- generic separable passes (k_sep.hip) -----------------------------------
+enum { kSepReduce = 0, kSepConv = 1 };
+struct SepSpec {            // one 1-D integer mask family
+    const float *tab;       // device table: reduce 129 x taps phases, conv 1 x taps
+    int taps;
+    int mode;               // kSepReduce / kSepConv
+    double shrink;          // reduce
+    int scale;              // conv: divisor (mask sum)
+};
+struct SepWindow {          // geometry of one pass over a batch of n images
+    int bands;
+    int in_pitch;           // bytes between input rows
+    long long in_base;      // byte offset of the local input origin inside an image
+    long long in_img;       // bytes per input image
+    int in_len;             // local input length along the pass axis (COPY clamp)
+    int o0;                 // first output position along the pass axis (op-output coords)
+    int out_w, out_h;       // packed output image of the pass
+};
+bool sep_spec_reduce(double shrink, SepSpec *s);
+bool sep_spec_gauss(double sigma, double min_ampl, SepSpec *s);
+int vpass_launch(const uint8_t *in, uint8_t *out, int n, const SepSpec &spec, const SepWindow &w, hipStream_t st);
+int hpass_launch(const uint8_t *in, uint8_t *out, int n, const SepSpec &spec, const SepWindow &w, hipStream_t st);
 
 // ---- kernel launchers (k_*.hip); batches of n images packed back to back -----
 // k_reduce.hip
 int reducev_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double vshrink, hipStream_t st);
 int reduceh_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hshrink, hipStream_t st);
+int reduce_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int left,
+                         int top, int ow, int oh, void *ws, size_t ws_bytes, hipStream_t st);
 bool reduce2_eligible(const uint8_t *in, int w, int h, int b, double hs, double vs);
 int reduce2_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, hipStream_t st);
 // k_shrink.hip
@@ -73,6 +100,8 @@ int extract_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, 
 // k_blur.hip (ws: n * w * h * b bytes for the uchar intermediate)
 int blur_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double sigma, double min_ampl,
                 void *ws, size_t ws_bytes, hipStream_t st);
+int blur_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int left, int top, int ow,
+                       int oh, double sigma, double min_ampl, void *ws, size_t ws_bytes, hipStream_t st);
 // k_composite.hip
 int watermark_launch(const uint8_t *base, const uint8_t *wm, uint8_t *out, int n, int w, int h, int bands, int ww,
                      int wh, int wb, int left, int top, float opacity, hipStream_t st);

@@ -22,6 +22,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -50,6 +51,7 @@ struct TableCache {
     std::mutex mu;
     std::map<std::pair<int, double>, std::pair<float *, int>> reduce;  // (device, shrink)
     std::map<int, float *> colour;
+    std::map<std::tuple<int, double, double>, std::tuple<float *, int, int>> gauss;  // (device, sigma, min_ampl)
 };
 TableCache &tables() {
     static TableCache *t = new TableCache();  // leaked on purpose: outlives static dtors
@@ -81,6 +83,46 @@ const float *device_reduce_table(double shrink, int *n_taps) {
     tc.reduce[key] = {d, n};
     *n_taps = n;
     return d;
+}
+
+const float *device_gauss_table(double sigma, double min_ampl, int *n_taps, int *scale) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    TableCache &tc = tables();
+    std::lock_guard<std::mutex> lk(tc.mu);
+    auto key = std::make_tuple(dev, sigma, min_ampl);
+    auto it = tc.gauss.find(key);
+    if (it != tc.gauss.end()) {
+        *n_taps = std::get<1>(it->second);
+        *scale = std::get<2>(it->second);
+        return std::get<0>(it->second);
+    }
+    std::vector<int> mask;
+    int sc = 0;
+    const int n = gaussmat(sigma, min_ampl, mask, sc);
+    if (n <= 0) return nullptr;
+    std::vector<float> f(mask.begin(), mask.end());
+    float *d = nullptr;
+    if (hipMalloc(&d, f.size() * sizeof(float)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    tc.gauss[key] = std::make_tuple(d, n, sc);
+    *n_taps = n;
+    *scale = sc;
+    return d;
+}
+
+bool sep_spec_gauss(double sigma, double min_ampl, SepSpec *s) {
+    int taps = 0, scale = 0;
+    s->tab = device_gauss_table(sigma, min_ampl, &taps, &scale);
+    if (!s->tab) return false;
+    s->taps = taps;
+    s->mode = kSepConv;
+    s->shrink = 1.0;
+    s->scale = scale;
+    return true;
 }
 
 const float *device_colour_tables() {
@@ -116,8 +158,13 @@ void free_device_tables() {
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second);
     }
+    for (auto &kv : tc.gauss) {
+        (void)hipSetDevice(std::get<0>(kv.first));
+        (void)hipFree(std::get<0>(kv.second));
+    }
     tc.reduce.clear();
     tc.colour.clear();
+    tc.gauss.clear();
     (void)hipSetDevice(cur);
 }
 
@@ -174,6 +221,32 @@ int execute_plan(const mipx_plan *p, int n, const uint8_t *d_in, uint8_t *d_out,
     for (int i = 0; i < p->n_steps; ++i) {
         const mipx_step &s = p->steps[i];
         uint8_t *dst = (i + 1 == p->n_steps) ? d_out : (cur == bufA ? bufB : bufA);
+        // Peephole fusions (results identical to running the two ops):
+        //  reduce -> extract : the reduce computes only the extract window
+        //  extract -> blur   : the blur reads the window in place (COPY edge = window edge)
+        if (i + 1 < p->n_steps && p->steps[i + 1].op == MIPX_OP_EXTRACT && s.op == MIPX_OP_REDUCE &&
+            !reduce2_eligible(cur, w, h, b, s.d[0], s.d[1])) {
+            const mipx_step &x = p->steps[i + 1];
+            uint8_t *dst2 = (i + 2 == p->n_steps) ? d_out : (cur == bufA ? bufB : bufA);
+            e = reduce_window_launch(cur, dst2, n, w, h, b, s.d[0], s.d[1], x.a[0], x.a[1], x.a[2], x.a[3], aux,
+                                     L.aux_bytes, st);
+            if (e) return e;
+            cur = dst2;
+            w = x.out_w, h = x.out_h, b = x.out_bands;
+            ++i;
+            continue;
+        }
+        if (i + 1 < p->n_steps && p->steps[i + 1].op == MIPX_OP_BLUR && s.op == MIPX_OP_EXTRACT) {
+            const mipx_step &g = p->steps[i + 1];
+            uint8_t *dst2 = (i + 2 == p->n_steps) ? d_out : (cur == bufA ? bufB : bufA);
+            e = blur_window_launch(cur, dst2, n, w, h, b, s.a[0], s.a[1], s.a[2], s.a[3], g.d[0], g.d[1], aux,
+                                   L.aux_bytes, st);
+            if (e) return e;
+            cur = dst2;
+            w = g.out_w, h = g.out_h, b = g.out_bands;
+            ++i;
+            continue;
+        }
         switch (s.op) {
             case MIPX_OP_ROT: e = mipx_op_rot(cur, dst, n, w, h, b, s.a[0], sv); break;
             case MIPX_OP_FLIP: e = mipx_op_flip(cur, dst, n, w, h, b, s.a[0], sv); break;

@@ -170,6 +170,12 @@ PLANS = [
     (dict(sigma=5.0), (200, 150, 4, "png", 0)),
     (dict(top=10, left=20, area_width=100, area_height=50), (200, 150, 3, "png", 0)),
     (dict(width=1024, embed=1), (2048, 2048, 4, "png", 0)),
+    # peephole fusions: reduce -> extract (window reduce), extract -> blur (window blur)
+    (dict(top=10, left=21, area_width=101, area_height=50, sigma=2.0), (200, 150, 3, "png", 0)),
+    (dict(top=3, left=4, area_width=64, area_height=40, sigma=5.0), (97, 61, 4, "png", 0)),
+    (dict(width=300, height=200, crop=1, sigma=1.5), (640, 480, 4, "png", 0)),
+    (dict(width=251, height=99, crop=1, gravity=3), (1001, 333, 3, "png", 0)),
+    (dict(width=768, height=512, crop=1), (1024, 1024, 4, "png", 0)),
 ]
 
 
