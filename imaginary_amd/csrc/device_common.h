@@ -68,6 +68,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc(const u8 *p, long l
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<u8 *>(p), 0, static_cast<int>(bytes), 0x00020000);
 }
 
+// The same over the dword-aligned-down image base: *delta = p & 3 is added to
+// every byte offset, so dword loads stay aligned for any image start.  Range
+// checks are per dword (a dword straddling num_records reads 0), so the range
+// is rounded up to the aligned word holding the image's last byte — never past
+// it, so never into another page.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc_aligned(const u8 *p, long long bytes, int *delta) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    *delta = static_cast<int>(a & 3u);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<u8 *>(a & ~uintptr_t(3)), 0,
+                                             static_cast<int>((bytes + *delta + 3) & ~3LL), 0x00020000);
+}
+
 }  // namespace dev
 
 // ---- host-side helpers shared by the launchers ----

@@ -101,6 +101,79 @@ __global__ void __launch_bounds__(256) k_remap(RemapArgs a) {
     else store_px(q, v, B);
 }
 
+// embed (and device-origin extract), 16 output bytes per lane.  Bytes whose
+// pixels all come from one source row's interior are read as aligned dwords +
+// v_alignbyte (any pixel offset, any band count); rows wholly outside in a
+// fill mode store the fill pattern; border dwords resolve each byte through the
+// extend mode.  Needs a dword aligned image base; bit-exact with k_remap<EMBED>.
+__device__ __forceinline__ int extend_index(int v, int n, int ext) {  // -1 = fill
+    const int c = clampi(v, 0, n - 1);
+    const int r = pmod(v, n);
+    const int u = pmod(v, 2 * n);
+    const int m = u < n ? u : 2 * n - 1 - u;
+    const int o = ext == MIPX_EXTEND_COPY ? c : ext == MIPX_EXTEND_REPEAT ? r : ext == MIPX_EXTEND_MIRROR ? m : -1;
+    return (v >= 0 && v < n) ? v : o;
+}
+
+template <int B>
+__global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
+    const int Y = blockIdx.y;
+    const int img = blockIdx.z;
+    const int row_out = a.ow * B;
+    const int j0 = (blockIdx.x * 256 + threadIdx.x) * 16;
+    if (j0 >= row_out) return;
+    int ox = a.x, oy = a.y;
+    if (a.origins) {
+        ox = -a.origins[2 * img];
+        oy = -a.origins[2 * img + 1];
+    }
+    const int sy = extend_index(Y - oy, a.h, a.extend);
+    const u8 *src = a.in + img * a.in_img;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
+    const int nb = min(16, row_out - j0);
+    uint32_t v[4];
+    if (sy < 0) {  // fill row: the pattern, phase j mod B
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w |= static_cast<uint32_t>(a.fill[(j0 + 4 * d + k) % B]) << (8 * k);
+            v[d] = w;
+        }
+    } else if (j0 / B - ox >= 0 && (j0 + 15) / B - ox < a.w) {  // interior: shifted row copy
+        const int o = sy * a.w * B + (j0 - ox * B);
+        const int o4 = o & ~3, sh = o & 3;
+        uint32_t w[5];
+#pragma unroll
+        for (int d = 0; d < 5; ++d) w[d] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 4 * d, 0, 0));
+#pragma unroll
+        for (int d = 0; d < 4; ++d) v[d] = __builtin_amdgcn_alignbyte(w[d + 1], w[d], sh);  // (hi:lo) >> 8 sh
+    } else {
+        const long long rowb = static_cast<long long>(sy) * a.w * B;
+#pragma unroll 1
+        for (int d = 0; d < 4; ++d) {
+            uint32_t w = 0;
+            for (int k = 0; k < 4; ++k) {
+                const int jb = j0 + 4 * d + k;
+                const int px = jb / B, c = jb - px * B;
+                const int sx = extend_index(px - ox, a.w, a.extend);
+                const uint32_t byte = sx < 0 ? a.fill[c] : src[rowb + static_cast<long long>(sx) * B + c];
+                w |= byte << (8 * k);
+            }
+            v[d] = w;
+        }
+    }
+    u8 *q = a.out + img * a.out_img + static_cast<long long>(Y) * row_out + j0;
+    if (nb == 16 && ((reinterpret_cast<uintptr_t>(q) & 15u) == 0)) {
+        *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
+    } else if (nb == 16 && ((reinterpret_cast<uintptr_t>(q) & 3u) == 0)) {
+        uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
+        q32[0] = v[0], q32[1] = v[1], q32[2] = v[2], q32[3] = v[3];
+    } else {
+        for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
+    }
+}
+
 // 90 (CW) / 270 rotation: out(x, y) = in(y, H-1-x) for CW, in(W-1-y, x) for CCW.
 // A block moves one 32 x 32 input tile; rows of the tile are read and rows of
 // the transposed tile written, each coalesced.
@@ -209,6 +282,11 @@ int embed_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x, int y
     a.out_img = img_bytes(ow, oh, b);
     a.origins = d_origins;
     if (b == 4 && !(aligned4(in) && aligned4(out))) return MIPX_EINVAL;
+    if (aligned4(in) && (a.in_img % 4) == 0 && a.in_img < 0x7fffffffLL && oh <= 65535) {
+        const dim3 grid((ow * b + 4095) / 4096, oh, n);
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_embed_rows<B_>, grid, dim3(256), 0, st, a));
+        return launch_check("k_embed_rows");
+    }
     return remap_launch(kEmbed, a, b, n, st);
 }
 

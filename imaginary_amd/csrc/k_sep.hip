@@ -11,13 +11,14 @@
 // both with EXTEND_COPY edges (restated in oracle/vips_ref.c).  Sums are
 // integers below 2^24, so fp32 FMAs reproduce them exactly in any order.
 //
-//  * k_vpass<KR, MODE, DW>: lanes own 4-byte columns of the row (channel
-//    agnostic); a block makes KR consecutive output rows by streaming each
-//    input row it needs ONCE (loads batched 8 deep) and adding it into every
-//    output row whose window contains it (wave-uniform predicate, taps from LDS).
-//  * k_hpass<B, RB, MODE>: a block = 256 output pixels x RB rows; the input
-//    spans are staged in LDS as one u32 per pixel (dword-coalesced loads, then a
-//    repack with the COPY edge), each lane reads its taps from LDS.
+//  * k_vpass<MODE, DMA>: a block = one 1 KiB column block x kr output rows.
+//    The input rows those outputs need are staged in LDS once with direct-to-
+//    LDS buffer loads (no VGPR staging, all in flight together); lanes own
+//    4-byte columns (channel agnostic) and read their taps from LDS.
+//  * k_hpass<B, RB, MODE, DIRECT, TREG>: a block = 256 output pixels x RB
+//    rows; the input spans are DMA'd to LDS and repacked to one u32 per pixel
+//    with the COPY edge; each lane reads its taps from LDS (reduce taps of
+//    <= 16 held per lane in registers).
 // Both take a window (row / column offset and clamp range), so an extract that
 // follows a reduce or precedes a blur folds into the pass (mipx_runtime.cpp).
 #include <hip/hip_runtime.h>
@@ -74,16 +75,19 @@ struct VPassArgs {
     SepTaps tp;
 };
 
+constexpr int kVStride = 260;  // LDS dwords per staged row: 256 + 1 (skewed rows) + pad
+
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ lds_void *to_lds(void *p) { return (lds_void *)p; }  // generic -> LDS addrspacecast
 
-// DMA: 16 / 4 = bytes per lane of the direct-to-LDS buffer loads (alignment
-// permitting), 0 = register-staged byte loads.
+// DMA: 16 / 4 = bytes per lane of the direct-to-LDS buffer loads when rows are
+// 16 / 4 byte aligned; 0 = any alignment (dword DMA from each row's aligned-down
+// start, bytes shifted into place with v_alignbyte).
 template <int MODE, int DMA>
 __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t vsm[];
-    uint32_t *rows = vsm;                                          // lrows x 256 dwords
-    float *vcoef = reinterpret_cast<float *>(vsm + a.lrows * 256);  // kr x taps
+    uint32_t *rows = vsm;                                                // lrows x kVStride dwords
+    float *vcoef = reinterpret_cast<float *>(vsm + a.lrows * kVStride);  // kr x taps
     int *soff = reinterpret_cast<int *>(vcoef + a.kr * a.tp.taps);  // kr start rows
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int cb = t % a.col_blocks;
@@ -102,30 +106,31 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
     // ---- stage the L input rows of this 1 KiB column block in LDS ----
     const u8 *src = a.in + img * a.in_img;
     const long long col0 = a.in_base + static_cast<long long>(cb) * 1024;
+    int delta = 0;
     if (DMA == 16) {
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
         for (int l = wave; l < L; l += 4) {
             const int r = clampi(r_lo + l, 0, a.hl - 1);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * 256), 16,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride), 16,
                                                      static_cast<int>(col0) + lane * 16, r * a.in_pitch, 0, 0);
         }
     } else if (DMA == 4) {
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
         for (int l = 0; l < L; ++l) {
             const int r = clampi(r_lo + l, 0, a.hl - 1);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * 256 + wave * 64), 4,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + wave * 64), 4,
                                                      static_cast<int>(col0) + wave * 256 + lane * 4,
                                                      r * a.in_pitch, 0, 0);
         }
-    } else {
-        const int j = cb * 1024 + tid * 4;
-        const int nb = max(0, min(4, a.row_bytes - j));
+    } else {  // any alignment: each row from its dword-aligned-down start, plus one dword
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, &delta);
         for (int l = 0; l < L; ++l) {
             const int r = clampi(r_lo + l, 0, a.hl - 1);
-            const u8 *p = src + a.in_base + static_cast<long long>(r) * a.in_pitch + j;
-            uint32_t v = 0;
-            for (int z = 0; z < nb; ++z) v |= static_cast<uint32_t>(p[z]) << (8 * z);
-            rows[l * 256 + tid] = v;
+            const int a4 = static_cast<int>(delta + col0 + static_cast<long long>(r) * a.in_pitch) & ~3;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + wave * 64), 4,
+                                                     wave * 256 + lane * 4, a4, 0, 0);
+            if (wave == 0 && lane == 0)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + 256), 4, 1024, a4, 0, 0);
         }
     }
     for (int i = tid; i < nk * taps; i += 256) {
@@ -145,13 +150,19 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
     if (j >= a.row_bytes) return;
     const int nb = min(4, a.row_bytes - j);
     u8 *dst = a.out + img * a.out_img + static_cast<long long>(y0) * a.row_bytes + j;
+    const long long skew0 = delta + col0;
     for (int k = 0; k < nk; ++k) {
-        const uint32_t *rp = rows + soff[k] * 256 + tid;
+        const uint32_t *rp = rows + soff[k] * kVStride + tid;
         const float *ck = vcoef + k * taps;
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll 4
         for (int i = 0; i < taps; ++i) {
-            const uint32_t v = rp[i * 256];
+            uint32_t v = rp[i * kVStride];
+            if (DMA == 0) {  // shift the row's bytes into place (row start skew is uniform)
+                const int r = clampi(r_lo + soff[k] + i, 0, a.hl - 1);
+                const int sh = static_cast<int>(skew0 + static_cast<long long>(r) * a.in_pitch) & 3;
+                v = __builtin_amdgcn_alignbyte(rp[i * kVStride + 1], v, sh);
+            }
             const float c = ck[i];
             a0 = __builtin_fmaf(c, ubyte_f<0>(v), a0);
             a1 = __builtin_fmaf(c, ubyte_f<1>(v), a1);
@@ -161,7 +172,7 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
         const uint32_t o = sep_round<MODE>(a0, a.tp) | (sep_round<MODE>(a1, a.tp) << 8) |
                            (sep_round<MODE>(a2, a.tp) << 16) | (sep_round<MODE>(a3, a.tp) << 24);
         u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
-        if (nb == 4 && (a.row_bytes & 3) == 0 && (a.out_img & 3) == 0) {
+        if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
             *reinterpret_cast<uint32_t *>(q) = o;
         } else {
             for (int z = 0; z < nb; ++z) q[z] = static_cast<u8>(o >> (8 * z));
@@ -220,11 +231,12 @@ __device__ __forceinline__ uint32_t load_px_g(const u8 *p) {
     return v;
 }
 
-// DW: rows dword aligned -> direct-to-LDS dword DMA of the span (B = 4) or of
-// its raw bytes (B < 4, repacked in LDS); else register-staged byte loads.
+// DIRECT (B = 4, rows dword aligned): direct-to-LDS dword DMA of the span into
+// the pixel slots; otherwise DMA of each row's raw bytes from its aligned-down
+// start, repacked to one u32 per pixel in LDS (any alignment, any band count).
 // TREG > 0: each lane holds its (<= TREG) taps in registers (reduce); 0: taps
 // from the LDS table.
-template <int B, int RB, int MODE, bool DW, int TREG>
+template <int B, int RB, int MODE, bool DIRECT, int TREG>
 __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hsm[];
     float *ctab = reinterpret_cast<float *>(hsm);
@@ -250,36 +262,25 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
     const int cl = max(lo, 0), ch = min(hi, a.wl - 1);  // pixels actually inside the row
     const u8 *img_base = a.in + img * a.in_img;
     const long long row0 = a.in_base + static_cast<long long>(y_first) * a.in_pitch;
-    int bs = 0, a4 = 0, skew = 0;
-    if (DW) {
+    int delta = 0;
+    if (DIRECT) {  // B = 4, rows dword aligned: pixels straight into their LDS slots
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(img_base, a.in_img);
-        if (B == 4) {
-            const int chunks = (ch - cl + 1 + 63) >> 6;
-            for (int idx = wave; idx < nr * chunks; idx += 4) {
-                const int rr = idx / chunks, q = idx - rr * chunks;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rs, to_lds(spx + rr * a.span_max + (cl - lo) + q * 64), 4,
-                    static_cast<int>(row0) + 4 * (cl + q * 64 + lane), rr * a.in_pitch, 0, 0);
-            }
-        } else {
-            bs = B * cl;
-            a4 = bs & ~3;
-            skew = bs - a4;
-            const int nd = (B * (ch - cl + 1) + skew + 3) >> 2;
-            const int chunks = (nd + 63) >> 6;
-            for (int idx = wave; idx < nr * chunks; idx += 4) {
-                const int rr = idx / chunks, q = idx - rr * chunks;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rs, to_lds(raw + rr * a.raw_max + q * 64), 4,
-                    static_cast<int>(row0) + a4 + 4 * (q * 64 + lane), rr * a.in_pitch, 0, 0);
-            }
+        const int chunks = (ch - cl + 1 + 63) >> 6;
+        for (int idx = wave; idx < nr * chunks; idx += 4) {
+            const int rr = idx / chunks, q = idx - rr * chunks;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, to_lds(spx + rr * a.span_max + (cl - lo) + q * 64), 4,
+                static_cast<int>(row0) + 4 * (cl + q * 64 + lane), rr * a.in_pitch, 0, 0);
         }
-    } else {
-        const u8 *src = img_base + row0;
-        for (int i = tid; i < nr * span; i += 256) {
-            const int rr = i / span, p = i - rr * span;
-            const int c = clampi(lo + p, 0, a.wl - 1);
-            spx[rr * a.span_max + p] = load_px_g<B>(src + static_cast<long long>(rr) * a.in_pitch + c * B);
+    } else {  // any alignment: each row's raw bytes from its dword-aligned-down start
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(img_base, a.in_img, &delta);
+        const int nd = (B * (ch - cl + 1) + 3 + 3) >> 2;
+        const int chunks = (nd + 63) >> 6;
+        for (int idx = wave; idx < nr * chunks; idx += 4) {
+            const int rr = idx / chunks, q = idx - rr * chunks;
+            const int a4 = static_cast<int>(delta + row0 + static_cast<long long>(rr) * a.in_pitch + B * cl) & ~3;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + rr * a.raw_max + q * 64), 4,
+                                                     4 * (q * 64 + lane), a4, 0, 0);
         }
     }
     // this lane's taps
@@ -295,8 +296,8 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
         for (int i = tid; i < a.ntab; i += 256) ctab[i] = a.tp.tab[i];
     }
     __syncthreads();
-    if (DW) {  // COPY edges (B = 4) or the repack of the raw bytes (B < 4)
-        if (B == 4) {
+    {  // COPY edges (direct) or the repack of the raw bytes with each row's skew
+        if (DIRECT) {
             const int nl = cl - lo, nrt = hi - ch;
             for (int i = tid; i < nr * (nl + nrt); i += 256) {
                 const int rr = i / (nl + nrt), f = i - rr * (nl + nrt);
@@ -309,10 +310,12 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
             for (int i = tid; i < nr * span; i += 256) {
                 const int rr = i / span, p = i - rr * span;
                 const int c = clampi(lo + p, 0, a.wl - 1);
+                const int skew = static_cast<int>(delta + row0 + static_cast<long long>(rr) * a.in_pitch + B * cl) & 3;
                 const u8 *q = rb8 + rr * a.raw_max * 4 + (c - cl) * B + skew;
                 uint32_t v = q[0];
                 if (B > 1) v |= static_cast<uint32_t>(q[1]) << 8;
                 if (B > 2) v |= static_cast<uint32_t>(q[2]) << 16;
+                if (B > 3) v |= static_cast<uint32_t>(q[3]) << 24;
                 spx[rr * a.span_max + p] = v;
             }
         }
@@ -440,7 +443,7 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     a.lrows = static_cast<int>(std::ceil((kr - 1) * s)) + taps + 2;
     a.kr_blocks = (a.oh + kr - 1) / kr;
     const dim3 blk(256);
-    const size_t lds = static_cast<size_t>(a.lrows) * 1024 + static_cast<size_t>(kr) * taps * 4 + kr * 4;
+    const size_t lds = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * taps * 4 + kr * 4;
     if (a.lrows > kRowMax || lds > 64 * 1024) {  // very tall masks: gather through L1
         const dim3 grid((a.row_bytes + 1023) / 1024, a.oh, n);
         if (spec.mode == kSepReduce) hipLaunchKernelGGL(k_vpass_gather<kSepReduce>, grid, blk, 0, st, a);
@@ -488,11 +491,11 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     a.span_max = static_cast<int>(std::ceil(255 * s)) + a.tp.taps + 2 + 64;
     a.raw_max = (a.span_max * b + 8 + 3) / 4 + 64;
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
-    const bool dw = (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0 && aligned4(in);
-    if (b == 4 && !(dw && aligned4(out))) return MIPX_EINVAL;
+    const bool dw = b == 4 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0 && aligned4(in);
+    if (b == 4 && !aligned4(out)) return MIPX_EINVAL;
     auto lds_for = [&](int rb) {
         return (static_cast<size_t>(a.ntab) + static_cast<size_t>(rb) * a.span_max +
-                (b < 4 && dw ? static_cast<size_t>(rb) * a.raw_max : 0)) * 4;
+                (!dw ? static_cast<size_t>(rb) * a.raw_max : 0)) * 4;
     };
     constexpr size_t kLdsBudget = 40 * 1024;
     int rb = 8;

@@ -58,15 +58,28 @@ __global__ void __launch_bounds__(256) k_shrink_lds(ShrinkArgs a) {
                 off[k] = min(p, a.w - 1) * B + c;  // COPY border beyond the last pixel
             }
         }
-        for (int k = 0; k < a.vs; ++k) {
+        if (whole) {  // batches of 8 independent row loads in flight
+            for (int k0 = 0; k0 < a.vs; k0 += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int r = min(y * a.vs + min(k0 + q, a.vs - 1), a.h - 1);
+                    v[q] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, g, r * row_bytes, 0));
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    if (k0 + q < a.vs) {
+                        s0 += v[q] & 0xff;
+                        s1 += (v[q] >> 8) & 0xff;
+                        s2 += (v[q] >> 16) & 0xff;
+                        s3 += v[q] >> 24;
+                    }
+                }
+            }
+        }
+        for (int k = 0; k < a.vs && !whole; ++k) {
             const int r = min(y * a.vs + k, a.h - 1);
-            if (whole) {
-                const uint32_t v = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, g, r * row_bytes, 0));
-                s0 += v & 0xff;
-                s1 += (v >> 8) & 0xff;
-                s2 += (v >> 16) & 0xff;
-                s3 += v >> 24;
-            } else {
+            {
                 const u8 *p = src + static_cast<size_t>(r) * row_bytes;
                 s0 += p[off[0]];
                 s1 += p[off[1]];

@@ -56,6 +56,20 @@ def test_reduce_matches_oracle(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"reduce {h}x{w}x{b} {hs}x{vs} img{i}")
 
 
+@pytest.mark.parametrize("h,w,b,hs,vs", [(41, 43, 3, 1.7, 1.7), (29, 31, 2, 1.25, 1.6), (77, 301, 1, 1.33, 2.9),
+                                         (240, 427, 3, 1.4233, 1.4233), (61, 97, 4, 3.1, 1.1)])
+def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
+    """Batches of odd-sized images: every image after the first starts at an
+    unaligned address, rows have odd pitches (the any-alignment DMA paths)."""
+    imgs = np.stack([rand_img(rng, h, w, b) for _ in range(3)])
+    got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+    for i in range(3):
+        assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"reduce {h}x{w}x{b} img{i}")
+    blur = gpu.run_op("gaussblur", imgs, sigma=1.7, min_ampl=0.2)
+    for i in range(3):
+        assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
+
+
 @pytest.mark.parametrize("h,w,b,s", [(50, 60, 3, 1.6), (31, 45, 4, 2.0), (20, 33, 1, 3.3)])
 def test_reducev_reduceh_separately(gpu, oracle, rng, h, w, b, s):
     img = rand_img(rng, h, w, b)
@@ -100,6 +114,16 @@ def test_embed_matches_oracle(gpu, oracle, rng, extend, x, y, W, H):
         img = rand_img(rng, 48, 64, b)
         got = gpu.run_op("embed", img, x=x, y=y, width=W, height=H, extend=extend, background=(12, 200, 77))
         assert_same(got[0], oracle.embed(img, x, y, W, H, extend, (12, 200, 77)), f"embed mode {extend} b{b}")
+
+
+@pytest.mark.parametrize("b", [1, 2, 3])
+@pytest.mark.parametrize("extend", [0, 1, 2, 3, 5])
+def test_embed_odd_sizes_all_bands(gpu, oracle, rng, b, extend):
+    """Row embed kernel: unaligned pixel offsets, odd row lengths, 1-3 bands."""
+    img = rand_img(rng, 37, 53, b)
+    for x, y, W, H in ((3, 2, 61, 40), (-5, -7, 33, 29), (0, 5, 53, 47), (13, 0, 101, 37), (-60, -40, 71, 45)):
+        got = gpu.run_op("embed", img, x=x, y=y, width=W, height=H, extend=extend, background=(9, 250, 31))
+        assert_same(got[0], oracle.embed(img, x, y, W, H, extend, (9, 250, 31)), f"embed {x},{y} {W}x{H} b{b}")
 
 
 @pytest.mark.parametrize("b", [1, 2, 3, 4])
