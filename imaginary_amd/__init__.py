@@ -4,7 +4,7 @@ The product is libmipx.so (gfx950 HIP kernels + C-ABI, include/mipx.h); this
 package is its Python binding plus a mirror of imaginary's operation layer.
 Importing it fails when libmipx.so has not been built: there is no CPU path.
 """
-from ._abi import lib, MipxError, MipxPlan, MipxOpts, MipxInput, LIB_PATH  # noqa: F401
+from ._abi import lib, MipxError, MipxPlan, MipxOpts, MipxInput, LIB_PATH, TYPES, EXTEND, GRAVITY  # noqa: F401
 from .engine import (DeviceBuffer, Engine, device_count, execute, fit_dimension, make_input,  # noqa: F401
                      make_opts, plan_make, run_op, smartcrop_origins, synchronize)
 

@@ -26,10 +26,14 @@ EXTEND = {"black": 0, "copy": 1, "repeat": 2, "mirror": 3, "white": 4, "backgrou
 TYPES = {"unknown": 0, "jpeg": 1, "webp": 2, "png": 3, "tiff": 4, "gif": 5, "pdf": 6, "svg": 7,
          "magick": 8, "heif": 9, "avif": 10}
 
-OP_ROT, OP_FLIP, OP_SHRINK, OP_REDUCE, OP_EXTRACT, OP_EMBED, OP_SMARTCROP, OP_BLUR, OP_WATERMARK = range(1, 10)
+(OP_ROT, OP_FLIP, OP_SHRINK, OP_REDUCE, OP_EXTRACT, OP_EMBED, OP_SMARTCROP, OP_BLUR, OP_WATERMARK,
+ OP_AFFINE, OP_ZOOM, OP_FLATTEN, OP_BW) = range(1, 14)
 OP_NAMES = {OP_ROT: "rot", OP_FLIP: "flip", OP_SHRINK: "shrink", OP_REDUCE: "reduce",
             OP_EXTRACT: "extract", OP_EMBED: "embed", OP_SMARTCROP: "smartcrop",
-            OP_BLUR: "blur", OP_WATERMARK: "watermark"}
+            OP_BLUR: "blur", OP_WATERMARK: "watermark", OP_AFFINE: "affine", OP_ZOOM: "zoom",
+            OP_FLATTEN: "flatten", OP_BW: "bw"}
+INTERPRETATION_SRGB = 22
+INTERPRETATION_BW = 26
 MAX_STEPS = 16
 
 
@@ -51,6 +55,7 @@ class MipxOpts(C.Structure):
         ("wm_enable", C.c_int32),
         ("wm_left", C.c_int32), ("wm_top", C.c_int32),
         ("wm_opacity", C.c_float),
+        ("interpretation", C.c_int32),
     ]
 
 
@@ -128,6 +133,10 @@ _SIG = {
     "mipx_op_flip": (C.c_int, [_U8P, _U8P, _I, _I, _I, _I, _I, _P]),
     "mipx_op_gaussblur": (C.c_int, [_U8P, _U8P, _I, _I, _I, _I, C.c_double, C.c_double, _P, C.c_size_t, _P]),
     "mipx_op_watermark": (C.c_int, [_U8P, _U8P, _U8P, _I, _I, _I, _I, _I, _I, _I, _I, _I, C.c_float, _P]),
+    "mipx_op_affine": (C.c_int, [_U8P, _U8P, _I, _I, _I, _I, C.c_double, C.c_double, _I, _P]),
+    "mipx_op_zoom": (C.c_int, [_U8P, _U8P, _I, _I, _I, _I, _I, _I, _P]),
+    "mipx_op_flatten": (C.c_int, [_U8P, _U8P, _I, _I, _I, _I, C.POINTER(_I), _P]),
+    "mipx_op_colourspace_bw": (C.c_int, [_U8P, _U8P, _I, _I, _I, _I, _P]),
     "mipx_op_smartcrop_origin": (C.c_int, [_U8P, _P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _P]),
     "mipx_op_workspace_bytes": (C.c_size_t, [_I, _I, _I, _I, _I, C.c_double, C.c_double]),
     "mipx_set_device": (C.c_int, [C.c_int]),

@@ -84,6 +84,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc_aligned(const u8 *p
 
 // ---- host-side helpers shared by the launchers ----
 inline long long img_bytes(int w, int h, int b) { return static_cast<long long>(w) * h * b; }
+inline int clampi_host(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 inline size_t align_up(size_t v) { return (v + 255) & ~static_cast<size_t>(255); }
 inline int launch_check(const char *what) {
     const hipError_t e = hipGetLastError();

@@ -39,6 +39,8 @@ int gaussmat(double sigma, double min_ampl, std::vector<int> &mask, int &scale);
 constexpr int kQuantElements = 100000;
 const float *v2y8_table();    // 256 entries: sRGB 8-bit -> linear
 const float *cbrt_table();    // kQuantElements entries: Lab f(t)
+const float *y2v8_table();    // 257 entries: linear Y x 255 -> sRGB 8-bit (B_W)
+void bicubic_table(int *t);   // 129 x 4 bicubic taps (vips_affine)
 
 // vips_resize() downsize schedule used by the smartcrop scorer.
 struct ResizeSchedule {
@@ -52,7 +54,8 @@ int resize_schedule(int w, int h, double hscale, double vscale, ResizeSchedule &
 // ---- device-side cached tables ----------------------------------------------
 // float copy of reduce_table(shrink) resident on the current device.
 const float *device_reduce_table(double shrink, int *n_taps);
-const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt]
+const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt | 257 y2v]
+const int *device_bicubic_table();     // 129 x 4
 // float copy of the integer gaussmat mask; *scale = mask sum
 const float *device_gauss_table(double sigma, double min_ampl, int *n_taps, int *scale);
 void free_device_tables();
@@ -102,6 +105,13 @@ int blur_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, dou
                 void *ws, size_t ws_bytes, hipStream_t st);
 int blur_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int left, int top, int ow,
                        int oh, double sigma, double min_ampl, void *ws, size_t ws_bytes, hipStream_t st);
+// k_affine.hip
+int affine_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double xs, double ys, int extend,
+                  hipStream_t st);
+int zoom_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int xf, int yf, hipStream_t st);
+// k_colour.hip
+int flatten_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, const int *bg, hipStream_t st);
+int bw_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, hipStream_t st);
 // k_composite.hip
 int watermark_launch(const uint8_t *base, const uint8_t *wm, uint8_t *out, int n, int w, int h, int bands, int ww,
                      int wh, int wb, int left, int top, float opacity, hipStream_t st);

@@ -123,6 +123,32 @@ int mipx_op_watermark(const uint8_t *d_base, const uint8_t *d_wm, uint8_t *d_out
     return watermark_launch(d_base, d_wm, d_out, n, w, h, bands, ww, wh, wb, left, top, opacity, as_stream(stream));
 }
 
+int mipx_op_affine(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h, int32_t bands, double xscale,
+                   double yscale, int32_t extend, void *stream) {
+    if (!d_in || !d_out || !geom_ok(n, w, h, bands) || !(xscale > 0) || !(yscale > 0)) return MIPX_EINVAL;
+    return affine_launch(d_in, d_out, n, w, h, bands, xscale, yscale, extend, as_stream(stream));
+}
+
+int mipx_op_zoom(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h, int32_t bands, int32_t xfac,
+                 int32_t yfac, void *stream) {
+    if (!d_in || !d_out || !geom_ok(n, w, h, bands) || xfac < 1 || yfac < 1) return MIPX_EINVAL;
+    return zoom_launch(d_in, d_out, n, w, h, bands, xfac, yfac, as_stream(stream));
+}
+
+int mipx_op_flatten(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h, int32_t bands,
+                    const int32_t *bg, void *stream) {
+    if (!d_in || !d_out || !geom_ok(n, w, h, bands)) return MIPX_EINVAL;
+    int b3[3] = {0, 0, 0};
+    if (bg) b3[0] = bg[0], b3[1] = bg[1], b3[2] = bg[2];
+    return flatten_launch(d_in, d_out, n, w, h, bands, b3, as_stream(stream));
+}
+
+int mipx_op_colourspace_bw(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h, int32_t bands,
+                           void *stream) {
+    if (!d_in || !d_out || !geom_ok(n, w, h, bands)) return MIPX_EINVAL;
+    return bw_launch(d_in, d_out, n, w, h, bands, as_stream(stream));
+}
+
 int mipx_op_smartcrop_origin(const uint8_t *d_in, int32_t *d_origins, int32_t n, int32_t w, int32_t h, int32_t bands,
                              int32_t cw, int32_t ch, void *d_ws, size_t ws_bytes, void *stream) {
     if (!d_in || !d_origins || !geom_ok(n, w, h, bands)) return MIPX_EINVAL;

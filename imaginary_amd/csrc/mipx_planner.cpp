@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "mipx_internal.h"
 
@@ -104,6 +105,36 @@ const ColourTables &colour() {
 }
 }  // namespace
 const float *v2y8_table() { return colour().v2y; }
+
+// 8-bit linear Y -> sRGB, 257 entries (the last repeated for the interpolation)
+const float *y2v8_table() {
+    static const std::vector<float> t = [] {
+        std::vector<float> v(257);
+        for (int i = 0; i < 256; ++i) {
+            const float f = i / 255.0f;
+            float e;
+            if (f <= 0.0031308f) e = 12.92f * f;
+            else e = static_cast<float>(1.055 * std::pow(f, 1.0 / 2.4) - 0.055);
+            v[i] = 255.0f * e;
+        }
+        v[256] = v[255];
+        return v;
+    }();
+    return t.data();
+}
+
+// vips_interpolate_bicubic matrixi: Catmull-Rom (templates.h
+// calculate_coefficients_catmull) x 4096, truncated; 129 phases x 4
+void bicubic_table(int *t) {
+    for (int x = 0; x <= kTransformScale; ++x) {
+        const double p = static_cast<float>(x) / kTransformScale;
+        const double cr1 = 1. - p, cr2 = -.5 * p, cr3 = cr1 * cr2;
+        const double cone = cr1 * cr3, cfou = p * cr3, cr4 = cfou - cone;
+        const double ctwo = cr1 - cr4 + cfou, cthr = p - cfou + cr4;
+        const double c[4] = {cone, ctwo, cthr, cfou};
+        for (int i = 0; i < 4; ++i) t[x * 4 + i] = static_cast<int>(c[i] * kInterpScale);
+    }
+}
 const float *cbrt_table() { return colour().cbrt.data(); }
 
 // vips_resize(): integer shrink floor(1 / (2 scale)), then residual reducev/h.
@@ -227,10 +258,6 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
     }
     mipx_opts o = *opts;  // bimg passes Options by value through the resizer
     PlanBuilder pb(plan);
-    if (o.zoom > 0) {
-        mipx::set_error("zoom (vips_zoom) is not implemented by the engine");
-        return MIPX_EUNSUPPORTED;
-    }
 
     // rotateAndFlipImage: EXIF consulted only when no explicit rotation.
     int rotate = o.rotate;
@@ -325,6 +352,18 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
         pb.last().a[0] = 1;
         pb.geom(pb.w(), pb.h(), pb.b());
     }
+    // zoomImage: vips_zoom(zoom + 1) after shrink-on-load and rotation
+    if (o.zoom > 0) {
+        const int z = o.zoom + 1;
+        if (static_cast<double>(pb.w()) * z * pb.h() * z * pb.b() > 2147483647.0) {
+            mipx::set_error("zoom %d of %dx%d is too large", z, pb.w(), pb.h());
+            return MIPX_EINVAL;
+        }
+        pb.push(MIPX_OP_ZOOM);
+        pb.last().a[0] = z;
+        pb.last().a[1] = z;
+        pb.geom(pb.w() * z, pb.h() * z, pb.b());
+    }
 
     const bool transform = o.force || (o.width > 0 && o.width != iw) ||
                            (o.height > 0 && o.height != ih) || o.area_width > 0 ||
@@ -353,8 +392,18 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
                 pb.geom(out_size_reduce(pb.w(), 1.0 / rx), out_size_reduce(pb.h(), 1.0 / ry),
                         pb.b());
             } else if (!(rx == 1.0 && ry == 1.0)) {
-                mipx::set_error("enlarge (vips_affine bicubic %.4fx%.4f) is not implemented", rx, ry);
-                return MIPX_EUNSUPPORTED;
+                // vipsAffine(residualx, residualy, bicubic, o.Extend): output = the
+                // transformed input rectangle (vips__transform_set_area)
+                const double ow = std::ceil(pb.w() * rx), oh = std::ceil(pb.h() * ry);
+                if (ow * oh * pb.b() > 2147483647.0) {
+                    mipx::set_error("affine output %.0fx%.0f is too large", ow, oh);
+                    return MIPX_EINVAL;
+                }
+                pb.push(MIPX_OP_AFFINE);
+                pb.last().d[0] = rx;
+                pb.last().d[1] = ry;
+                pb.last().a[0] = o.extend > 5 ? MIPX_EXTEND_BACKGROUND : o.extend;
+                pb.geom(static_cast<int>(ow), static_cast<int>(oh), pb.b());
             }
         }
         if (o.force) {
@@ -450,6 +499,19 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
         pb.last().a[4] = in->wm_bands;
         pb.last().d[0] = o.wm_opacity == 0.0f ? 1.0 : static_cast<double>(o.wm_opacity);
         pb.geom(pb.w(), pb.h(), bb);
+    }
+    // imageFlatten: PNG input, non-black background, an alpha band
+    if (in->type == MIPX_TYPE_PNG && (o.background[0] || o.background[1] || o.background[2]) && has_alpha(pb.b())) {
+        pb.push(MIPX_OP_FLATTEN);
+        pb.last().a[0] = o.background[0];
+        pb.last().a[1] = o.background[1];
+        pb.last().a[2] = o.background[2];
+        pb.geom(pb.w(), pb.h(), pb.b() - 1);
+    }
+    // vipsPreSave: vips_colourspace to the requested interpretation
+    if (o.interpretation == MIPX_INTERPRETATION_BW && pb.b() >= 3) {
+        pb.push(MIPX_OP_BW);
+        pb.geom(pb.w(), pb.h(), pb.b() == 4 ? 2 : 1);
     }
     plan->out_w = pb.w();
     plan->out_h = pb.h();

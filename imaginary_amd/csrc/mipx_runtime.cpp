@@ -51,6 +51,7 @@ struct TableCache {
     std::mutex mu;
     std::map<std::pair<int, double>, std::pair<float *, int>> reduce;  // (device, shrink)
     std::map<int, float *> colour;
+    std::map<int, int *> bicubic;
     std::map<std::tuple<int, double, double>, std::tuple<float *, int, int>> gauss;  // (device, sigma, min_ampl)
 };
 TableCache &tables() {
@@ -132,9 +133,10 @@ const float *device_colour_tables() {
     std::lock_guard<std::mutex> lk(tc.mu);
     auto it = tc.colour.find(dev);
     if (it != tc.colour.end()) return it->second;
-    std::vector<float> h(256 + kQuantElements);
+    std::vector<float> h(256 + kQuantElements + 257);
     std::memcpy(h.data(), v2y8_table(), 256 * sizeof(float));
     std::memcpy(h.data() + 256, cbrt_table(), kQuantElements * sizeof(float));
+    std::memcpy(h.data() + 256 + kQuantElements, y2v8_table(), 257 * sizeof(float));
     float *d = nullptr;
     if (hipMalloc(&d, h.size() * sizeof(float)) != hipSuccess) return nullptr;
     if (hipMemcpy(d, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
@@ -142,6 +144,25 @@ const float *device_colour_tables() {
         return nullptr;
     }
     tc.colour[dev] = d;
+    return d;
+}
+
+const int *device_bicubic_table() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    TableCache &tc = tables();
+    std::lock_guard<std::mutex> lk(tc.mu);
+    auto it = tc.bicubic.find(dev);
+    if (it != tc.bicubic.end()) return it->second;
+    std::vector<int> t((kTransformScale + 1) * 4);
+    bicubic_table(t.data());
+    int *d = nullptr;
+    if (hipMalloc(&d, t.size() * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, t.data(), t.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    tc.bicubic[dev] = d;
     return d;
 }
 
@@ -158,6 +179,11 @@ void free_device_tables() {
         (void)hipSetDevice(kv.first);
         (void)hipFree(kv.second);
     }
+    for (auto &kv : tc.bicubic) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second);
+    }
+    tc.bicubic.clear();
     for (auto &kv : tc.gauss) {
         (void)hipSetDevice(std::get<0>(kv.first));
         (void)hipFree(std::get<0>(kv.second));
@@ -266,6 +292,10 @@ int execute_plan(const mipx_plan *p, int n, const uint8_t *d_in, uint8_t *d_out,
             case MIPX_OP_BLUR:
                 e = mipx_op_gaussblur(cur, dst, n, w, h, b, s.d[0], s.d[1], aux, L.aux_bytes, sv);
                 break;
+            case MIPX_OP_AFFINE: e = mipx_op_affine(cur, dst, n, w, h, b, s.d[0], s.d[1], s.a[0], sv); break;
+            case MIPX_OP_ZOOM: e = mipx_op_zoom(cur, dst, n, w, h, b, s.a[0], s.a[1], sv); break;
+            case MIPX_OP_FLATTEN: e = mipx_op_flatten(cur, dst, n, w, h, b, s.a, sv); break;
+            case MIPX_OP_BW: e = mipx_op_colourspace_bw(cur, dst, n, w, h, b, sv); break;
             case MIPX_OP_WATERMARK:
                 if (!d_wm) return MIPX_EINVAL;
                 e = mipx_op_watermark(cur, d_wm, dst, n, w, h, b, s.a[2], s.a[3], s.a[4], s.a[0], s.a[1],

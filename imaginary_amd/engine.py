@@ -186,6 +186,15 @@ def run_op(name: str, imgs: np.ndarray, **p) -> np.ndarray:
     elif name == "watermark":
         oh, ow = h, w
         ob = b if b in (2, 4) else b + 1
+    elif name == "affine":
+        import math
+        ow, oh, ob = int(math.ceil(w * p["xscale"])), int(math.ceil(h * p["yscale"])), b
+    elif name == "zoom":
+        ow, oh, ob = w * p["xfac"], h * p["yfac"], b
+    elif name == "flatten":
+        oh, ow, ob = h, w, (b - 1 if b in (2, 4) else b)
+    elif name == "bw":
+        oh, ow, ob = h, w, (2 if b == 4 else 1 if b == 3 else b)
     else:
         raise ValueError(name)
     dout = DeviceBuffer(n * oh * ow * ob)
@@ -221,6 +230,14 @@ def run_op(name: str, imgs: np.ndarray, **p) -> np.ndarray:
         dwm = DeviceBuffer.from_array(wm)
         code = lib.mipx_op_watermark(din.ptr, dwm.ptr, dout.ptr, n, w, h, b, wm.shape[1], wm.shape[0],
                                      wm.shape[2], p["left"], p["top"], p["opacity"], None)
+    elif name == "affine":
+        code = lib.mipx_op_affine(din.ptr, dout.ptr, n, w, h, b, p["xscale"], p["yscale"], p.get("extend", 1), None)
+    elif name == "zoom":
+        code = lib.mipx_op_zoom(din.ptr, dout.ptr, n, w, h, b, p["xfac"], p["yfac"], None)
+    elif name == "flatten":
+        code = lib.mipx_op_flatten(din.ptr, dout.ptr, n, w, h, b, (C.c_int32 * 3)(*p["background"]), None)
+    elif name == "bw":
+        code = lib.mipx_op_colourspace_bw(din.ptr, dout.ptr, n, w, h, b, None)
     check(code, f"mipx_op_{name}")
     synchronize()
     return dout.download((n, oh, ow, ob))

@@ -82,6 +82,7 @@ class ImageOptions:
     aspect_ratio: str = ""
     background: List[int] = field(default_factory=list)
     extend: int = 1          # bimg.ExtendCopy default (params.go:342, 356)
+    colorspace: int = 0      # bimg.Interpretation (params.go:260, parseColorspace 392)
     gravity: int = 0
     operations: List[Dict[str, Any]] = field(default_factory=list)
     is_defined: IsDefinedField = field(default_factory=IsDefinedField)
@@ -141,6 +142,11 @@ def parse_gravity(v: str) -> int:
     return m.get(v.strip().lower(), 0)
 
 
+def parse_colorspace(v: str) -> int:
+    """params.go:392-397: "bw" -> InterpretationBW, anything else sRGB."""
+    return _abi.INTERPRETATION_BW if v.strip().lower() == "bw" else _abi.INTERPRETATION_SRGB
+
+
 def parse_color(v: str) -> List[int]:
     return [min(int(x.strip() or 0), 255) for x in v.split(",")] if v else []
 
@@ -165,6 +171,8 @@ def build_params_from_query(query: Dict[str, Any]) -> ImageOptions:
             o.extend = parse_extend_mode(v)
         elif k == "gravity":
             o.gravity = parse_gravity(v)
+        elif k == "colorspace":
+            o.colorspace = parse_colorspace(v)
         elif k == "background":
             o.background = parse_color(v) if isinstance(v, str) else list(v)
         elif k == "type":
@@ -197,7 +205,7 @@ def bimg_options(o: ImageOptions) -> Dict[str, Any]:
     """options.go:128-172 -> the mipx_opts field dict."""
     b = dict(width=o.width, height=o.height, flip=int(o.flip), flop=int(o.flop),
              no_auto_rotate=int(o.no_rotation), force=int(o.force), gravity=o.gravity,
-             embed=int(o.embed), extend=o.extend, rotate=o.rotate)
+             embed=int(o.embed), extend=o.extend, rotate=o.rotate, interpretation=o.colorspace)
     if o.background:
         b["background"] = (list(o.background) + [0, 0, 0])[:3]
     b["width"], b["height"] = _aspect(o, o.width, o.height)

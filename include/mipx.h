@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MIPX_ABI_VERSION 1
+#define MIPX_ABI_VERSION 2
 
 /* ---- error codes ---- */
 #define MIPX_OK 0
@@ -79,7 +79,12 @@ typedef struct mipx_opts {
     int32_t wm_enable;              /* WatermarkImage present (image.go:364-367) */
     int32_t wm_left, wm_top;
     float wm_opacity;               /* 0 -> 1.0 as bimg does */
+    int32_t interpretation;         /* bimg Interpretation at save (options.go:142): 0 or
+                                       sRGB = keep, MIPX_INTERPRETATION_BW = vips_colourspace B_W */
 } mipx_opts;
+
+#define MIPX_INTERPRETATION_SRGB 22 /* VIPS_INTERPRETATION_sRGB */
+#define MIPX_INTERPRETATION_BW 26   /* VIPS_INTERPRETATION_B_W (params.go:392 colorspace=bw) */
 
 /* What the host codec knows about the encoded input. */
 typedef struct mipx_input {
@@ -100,7 +105,11 @@ enum {
     MIPX_OP_EMBED,       /* a[0..3] = x, y, w, h; a[4] = extend; a[5..7] bg  (vips_embed) */
     MIPX_OP_SMARTCROP,   /* a[0..1] = width, height, attention strategy      (vips_smartcrop) */
     MIPX_OP_BLUR,        /* d[0] = sigma, d[1] = min_ampl                    (vips_gaussblur) */
-    MIPX_OP_WATERMARK    /* a[0..1] = left, top; d[0] = opacity  (bimg vips_watermark_image) */
+    MIPX_OP_WATERMARK,   /* a[0..1] = left, top; d[0] = opacity  (bimg vips_watermark_image) */
+    MIPX_OP_AFFINE,      /* d[0] = xscale, d[1] = yscale, a[0] = extend; bicubic  (vips_affine) */
+    MIPX_OP_ZOOM,        /* a[0] = xfac, a[1] = yfac                         (vips_zoom) */
+    MIPX_OP_FLATTEN,     /* a[0..2] = background rgb                         (vips_flatten) */
+    MIPX_OP_BW           /* sRGB -> B_W                                      (vips_colourspace) */
 };
 
 #define MIPX_MAX_STEPS 16
@@ -190,6 +199,14 @@ int mipx_op_gaussblur(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w,
 int mipx_op_watermark(const uint8_t *d_base, const uint8_t *d_wm, uint8_t *d_out, int32_t n,
                       int32_t w, int32_t h, int32_t bands, int32_t wm_w, int32_t wm_h,
                       int32_t wm_bands, int32_t left, int32_t top, float opacity, void *stream);
+int mipx_op_affine(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h,
+                   int32_t bands, double xscale, double yscale, int32_t extend, void *stream);
+int mipx_op_zoom(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h,
+                 int32_t bands, int32_t xfac, int32_t yfac, void *stream);
+int mipx_op_flatten(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h,
+                    int32_t bands, const int32_t *background3, void *stream);
+int mipx_op_colourspace_bw(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h,
+                           int32_t bands, void *stream);
 /* writes n (left, top) int32 pairs to d_origins */
 int mipx_op_smartcrop_origin(const uint8_t *d_in, int32_t *d_origins, int32_t n, int32_t w,
                              int32_t h, int32_t bands, int32_t crop_w, int32_t crop_h,

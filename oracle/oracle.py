@@ -35,7 +35,7 @@ class RefOpts(C.Structure):
         ("flip", C.c_int), ("flop", C.c_int), ("gravity", C.c_int), ("extend", C.c_int),
         ("background", C.c_int * 3), ("zoom", C.c_int), ("sigma", C.c_double), ("min_ampl", C.c_double),
         ("smart_crop", C.c_int), ("wm_enable", C.c_int), ("wm_left", C.c_int), ("wm_top", C.c_int),
-        ("wm_opacity", C.c_float),
+        ("wm_opacity", C.c_float), ("interpretation", C.c_int),
     ]
 
 
@@ -86,6 +86,11 @@ def lib():
             "ref_gaussmat": (C.c_int, [C.c_double, C.c_double, P(C.c_int), C.c_int, P(C.c_int)]),
             "ref_gaussblur": (C.c_int, [P(RefImg), P(RefImg), C.c_double, C.c_double]),
             "ref_watermark": (C.c_int, [P(RefImg), P(RefImg), P(RefImg), C.c_int, C.c_int, C.c_float]),
+            "ref_bicubic_table": (C.c_int, [P(C.c_int)]),
+            "ref_affine": (C.c_int, [P(RefImg), P(RefImg), C.c_double, C.c_double, C.c_int]),
+            "ref_zoom": (C.c_int, [P(RefImg), P(RefImg), C.c_int, C.c_int]),
+            "ref_flatten": (C.c_int, [P(RefImg), P(RefImg), P(C.c_int)]),
+            "ref_bw": (C.c_int, [P(RefImg), P(RefImg)]),
             "ref_smartcrop_origin": (C.c_int, [P(RefImg), C.c_int, C.c_int, P(C.c_int), P(C.c_int)]),
             "ref_execute": (C.c_int, [P(RefPlan), P(RefImg), P(RefImg), P(RefImg)]),
             "ref_reduce_batch": (C.c_int, [P(P(C.c_uint8)), P(P(C.c_uint8)), C.c_int, C.c_int, C.c_int,
@@ -183,6 +188,28 @@ def reduce_table(shrink):
     t = (C.c_int * (n * 129))()
     lib().ref_reduce_table(shrink, t, n)
     return np.array(t[:], dtype=np.int32).reshape(129, n)
+
+
+def bicubic_table():
+    t = (C.c_int * (129 * 4))()
+    lib().ref_bicubic_table(t)
+    return np.array(t[:], dtype=np.int32).reshape(129, 4)
+
+
+def affine(img, xscale, yscale, extend=1):
+    return _call("ref_affine", img, xscale, yscale, extend)
+
+
+def zoom(img, xfac, yfac):
+    return _call("ref_zoom", img, xfac, yfac)
+
+
+def flatten(img, bg):
+    return _call("ref_flatten", img, (C.c_int * 3)(*bg))
+
+
+def bw(img):
+    return _call("ref_bw", img)
 
 
 def watermark(base, wm, left, top, opacity):

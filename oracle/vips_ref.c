@@ -38,6 +38,7 @@ static struct {
     {"blur_vfirst", 0},          /* 1: vertical conv pass before horizontal */
     {"blur_honor_minampl", 0},   /* 1: bimg passes min_ampl (no NULL-terminator bug) */
     {"cast_round", 0},           /* 1: float->uchar cast rounds instead of truncating */
+    {"affine_corner", 0},        /* 1: vips_affine corner convention (X = x / scale) */
     {NULL, 0}};
 
 void ref_set_switch(const char *name, int value) {
@@ -646,6 +647,172 @@ int ref_smartcrop_origin(const ref_img *in, int width, int height, int *left, in
 }
 
 /* ------------------------------------------------------------------------- */
+/* vips_affine with the bicubic interpolator (resample/affine.c, bicubic.cpp,  */
+/* templates.h), vips_zoom (conversion/zoom.c), vips_flatten                   */
+/* (conversion/flatten.c), vips_colourspace sRGB -> B_W (colour/sRGB2scRGB.c,  */
+/* scRGB2BW.c, colour.c)                                                       */
+/* ------------------------------------------------------------------------- */
+/* templates.h calculate_coefficients_catmull (a = -0.5) */
+static void catmull(double c[4], double x) {
+    const double cr1 = 1. - x;
+    const double cr2 = -.5 * x;
+    const double cr3 = cr1 * cr2;
+    const double cone = cr1 * cr3;
+    const double cfou = x * cr3;
+    const double cr4 = cfou - cone;
+    const double ctwo = cr1 - cr4 + cfou;
+    const double cthr = x - cfou + cr4;
+    c[0] = cone;
+    c[1] = ctwo;
+    c[2] = cthr;
+    c[3] = cfou;
+}
+
+/* vips_interpolate_bicubic_class_init: matrixi[x][i] = matrixf * 4096 (truncated) */
+int ref_bicubic_table(int *table) {
+    for (int x = 0; x <= TRANSFORM_SCALE; x++) {
+        double c[4];
+        catmull(c, (float)x / TRANSFORM_SCALE);
+        for (int i = 0; i < 4; i++) table[x * 4 + i] = (int)(c[i] * INTERP_SCALE);
+    }
+    return 4;
+}
+
+/* unsigned_fixed_round: (v + 2048) >> 12 (arithmetic shift: floor) */
+static int ufr(int v) { return (v + (INTERP_SCALE >> 1)) >> INTERP_SHIFT; }
+
+/* window pixel index through the affine's input embed (bimg passes o.Extend;
+ * > 5 maps to background); -1 = fill (black: the affine's default background) */
+static int extend_idx(int v, int n, int extend) {
+    if (v >= 0 && v < n) return v;
+    switch (extend) {
+    case REF_EXTEND_COPY: return clampi(v, 0, n - 1);
+    case REF_EXTEND_REPEAT: return pmod(v, n);
+    case REF_EXTEND_MIRROR: { int u = pmod(v, 2 * n); return u < n ? u : 2 * n - 1 - u; }
+    default: return -1;
+    }
+}
+static int extend_fill(int extend) { return extend == REF_EXTEND_WHITE ? 255 : 0; }
+
+/* input position of output pixel o (window-offset coordinates: +1, so the
+ * interpolator's (int) truncation is a floor) */
+static double affine_pos(int o, double scale) {
+    double X = ref_get_switch("affine_corner") ? o / scale : (o + 0.5) / scale - 0.5;
+    return X + 1.0;
+}
+
+int ref_affine(const ref_img *in, ref_img *out, double xscale, double yscale, int extend) {
+    if (!(xscale > 0) || !(yscale > 0)) return REF_EINVAL;
+    if (extend > 5) extend = REF_EXTEND_BACKGROUND;
+    /* vips__transform_set_area: output = the transformed input rectangle */
+    int ow = (int)ceil(in->w * xscale), oh = (int)ceil(in->h * yscale);
+    int e = img_alloc(out, ow, oh, in->bands);
+    if (e) return e;
+    int tab[(TRANSFORM_SCALE + 1) * 4];
+    ref_bicubic_table(tab);
+    const int B = in->bands, fill = extend_fill(extend);
+    for (int y = 0; y < oh; y++) {
+        const double Y = affine_pos(y, yscale);
+        const int iy = (int)Y, ty = (((int)(Y * TRANSFORM_SCALE * 2) & (TRANSFORM_SCALE * 2 - 1)) + 1) >> 1;
+        const int *cy = tab + ty * 4;
+        int rows[4];
+        for (int j = 0; j < 4; j++) rows[j] = extend_idx(iy - 2 + j, in->h, extend);
+        for (int x = 0; x < ow; x++) {
+            const double X = affine_pos(x, xscale);
+            const int ix = (int)X, tx = (((int)(X * TRANSFORM_SCALE * 2) & (TRANSFORM_SCALE * 2 - 1)) + 1) >> 1;
+            const int *cx = tab + tx * 4;
+            int cols[4];
+            for (int i = 0; i < 4; i++) cols[i] = extend_idx(ix - 2 + i, in->w, extend);
+            for (int c = 0; c < B; c++) {
+                int r[4];
+                for (int j = 0; j < 4; j++) {
+                    int sum = 0;
+                    for (int i = 0; i < 4; i++) {
+                        int p = (rows[j] < 0 || cols[i] < 0) ? fill
+                                : in->data[((size_t)rows[j] * in->w + cols[i]) * B + c];
+                        sum += cx[i] * p;
+                    }
+                    r[j] = ufr(sum);
+                }
+                int v = ufr(cy[0] * r[0] + cy[1] * r[1] + cy[2] * r[2] + cy[3] * r[3]);
+                out->data[((size_t)y * ow + x) * B + c] = (uint8_t)clampi(v, 0, 255);
+            }
+        }
+    }
+    return REF_OK;
+}
+
+/* vips_zoom: every input pixel replicated xfac x yfac */
+int ref_zoom(const ref_img *in, ref_img *out, int xfac, int yfac) {
+    if (xfac < 1 || yfac < 1) return REF_EINVAL;
+    int e = img_alloc(out, in->w * xfac, in->h * yfac, in->bands);
+    if (e) return e;
+    const int B = in->bands;
+    for (int y = 0; y < out->h; y++)
+        for (int x = 0; x < out->w; x++)
+            memcpy(out->data + ((size_t)y * out->w + x) * B, in->data + ((size_t)(y / yfac) * in->w + x / xfac) * B, B);
+    return REF_OK;
+}
+
+/* vips_flatten(background): drop the alpha band,
+ * out = (p * alpha + bg * (255 - alpha)) / 255 in int arithmetic */
+int ref_flatten(const ref_img *in, ref_img *out, const int bg[3]) {
+    if (!has_alpha(in->bands)) return img_copy(in, out);
+    const int B = in->bands, ob = B - 1;
+    int e = img_alloc(out, in->w, in->h, ob);
+    if (e) return e;
+    for (size_t i = 0; i < (size_t)in->w * in->h; i++) {
+        const uint8_t *p = in->data + i * B;
+        const int alpha = p[B - 1], nalpha = 255 - alpha;
+        for (int c = 0; c < ob; c++) {
+            const int b = clampi(bg[c < 3 ? c : 2], 0, 255);
+            out->data[i * ob + c] = (uint8_t)((p[c] * alpha + b * nalpha) / 255);
+        }
+    }
+    return REF_OK;
+}
+
+/* sRGB -> B_W: 8-bit sRGB -> scRGB (vips_v2Y_8 LUT), Y = 0.2126 R + 0.7152 G +
+ * 0.0722 B, back through the 8-bit Y -> sRGB LUT with linear interpolation
+ * (vips_col_scRGB2BW_8); alpha passes through.  1-2 band input is already B_W. */
+static float Y2v8[257];
+static void bw_tables(void) {
+    static int done;
+    if (done) return;
+    for (int i = 0; i < 256; i++) {
+        float f = i / 255.0f, v;
+        if (f <= 0.0031308f) v = 12.92f * f;
+        else v = (float)(1.055 * pow(f, 1.0 / 2.4) - 0.055);
+        Y2v8[i] = 255.0f * v;
+    }
+    Y2v8[256] = Y2v8[255];
+    done = 1;
+}
+static float v2y_lut(int i) {
+    colour_tables();
+    return g_v2Y_8[i];
+}
+int ref_bw(const ref_img *in, ref_img *out) {
+    if (in->bands < 3) return img_copy(in, out);
+    bw_tables();
+    const int B = in->bands, ob = B == 4 ? 2 : 1;
+    int e = img_alloc(out, in->w, in->h, ob);
+    if (e) return e;
+    for (size_t i = 0; i < (size_t)in->w * in->h; i++) {
+        const uint8_t *p = in->data + i * B;
+        const float R = v2y_lut(p[0]), G = v2y_lut(p[1]), Bl = v2y_lut(p[2]);
+        const float Y = (float)(0.2126 * R + 0.7152 * G + 0.0722 * Bl);
+        const float Yf = Y * 255.0f;
+        const int k = clampi((int)Yf, 0, 255);
+        const float f = Yf - k;
+        const float v = Y2v8[k] + f * (Y2v8[k + 1] - Y2v8[k]);
+        out->data[i * ob] = (uint8_t)clampi((int)rintf(v), 0, 255);
+        if (ob == 2) out->data[i * ob + 1] = p[3];
+    }
+    return REF_OK;
+}
+
+/* ------------------------------------------------------------------------- */
 /* planner — bimg v1.1.9 resizer.go restated                                 */
 /* ------------------------------------------------------------------------- */
 /* imaginary image.go:190-200 calculateDestinationFitDimension */
@@ -681,7 +848,6 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
     memset(plan, 0, sizeof(*plan));
     if (in->w <= 0 || in->h <= 0 || in->bands <= 0 || in->bands > 4) return REF_EINVAL;
     int W = in->w, H = in->h, B = in->bands;
-    if (o.zoom > 0) return REF_EUNSUPPORTED; /* vips_zoom: §8(f) next */
 
     /* rotateAndFlipImage — EXIF via calculateRotationAndFlip, o by value */
     int rotate = o.rotate, flip = o.flip, flop = o.flop;
@@ -779,6 +945,17 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
         LAST(plan)->a[0] = 1;
         set_geom(plan, cw, ch, cb);
     }
+    /* zoomImage: vips_zoom(zoom + 1) after shrink-on-load and rotation */
+    if (o.zoom > 0) {
+        const int z = o.zoom + 1;
+        if ((double)cw * z * ch * z * cb > 2147483647.0) return REF_EINVAL;
+        push(plan, REF_OP_ZOOM, 0, 0, 0);
+        LAST(plan)->a[0] = z;
+        LAST(plan)->a[1] = z;
+        cw *= z;
+        ch *= z;
+        set_geom(plan, cw, ch, cb);
+    }
 
     /* shouldTransformImage (inWidth/inHeight = rotated header size) */
     int transform = o.force || (o.width > 0 && o.width != hw) || (o.height > 0 && o.height != hh) ||
@@ -810,7 +987,16 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
                 ch = ref_out_size_reduce(ch, 1.0 / ry);
                 set_geom(plan, cw, ch, cb);
             } else if (!(rx == 1.0 && ry == 1.0)) {
-                return REF_EUNSUPPORTED; /* vips_affine bicubic (enlarge): §8(f) next */
+                /* vipsAffine(residualx, residualy, bicubic, o.Extend) */
+                const double ow = ceil(cw * rx), oh = ceil(ch * ry);
+                if (ow * oh * cb > 2147483647.0) return REF_EINVAL;
+                push(plan, REF_OP_AFFINE, 0, 0, 0);
+                LAST(plan)->d[0] = rx;
+                LAST(plan)->d[1] = ry;
+                LAST(plan)->a[0] = o.extend > 5 ? REF_EXTEND_BACKGROUND : o.extend;
+                cw = (int)ow;
+                ch = (int)oh;
+                set_geom(plan, cw, ch, cb);
             }
         }
         if (o.force) { o.crop = 0; o.embed = 0; }
@@ -894,6 +1080,21 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
         cb = bb;
         set_geom(plan, cw, ch, cb);
     }
+    /* imageFlatten: PNG input with a non-black background and an alpha band */
+    if (in->type == REF_TYPE_PNG && (o.background[0] || o.background[1] || o.background[2]) && has_alpha(cb)) {
+        push(plan, REF_OP_FLATTEN, 0, 0, 0);
+        LAST(plan)->a[0] = o.background[0];
+        LAST(plan)->a[1] = o.background[1];
+        LAST(plan)->a[2] = o.background[2];
+        cb -= 1;
+        set_geom(plan, cw, ch, cb);
+    }
+    /* vipsPreSave: vips_colourspace to the requested interpretation (B_W) */
+    if (o.interpretation == REF_INTERPRETATION_BW && cb >= 3) {
+        push(plan, REF_OP_BW, 0, 0, 0);
+        cb = cb == 4 ? 2 : 1;
+        set_geom(plan, cw, ch, cb);
+    }
     plan->out_w = cw;
     plan->out_h = ch;
     plan->out_bands = cb;
@@ -922,6 +1123,10 @@ int ref_execute(const ref_plan *plan, const ref_img *in, const ref_img *wm, ref_
             break;
         }
         case REF_OP_BLUR: e = ref_gaussblur(&cur, &nx, s->d[0], s->d[1]); break;
+        case REF_OP_AFFINE: e = ref_affine(&cur, &nx, s->d[0], s->d[1], s->a[0]); break;
+        case REF_OP_ZOOM: e = ref_zoom(&cur, &nx, s->a[0], s->a[1]); break;
+        case REF_OP_FLATTEN: e = ref_flatten(&cur, &nx, s->a); break;
+        case REF_OP_BW: e = ref_bw(&cur, &nx); break;
         case REF_OP_WATERMARK:
             if (!wm || !wm->data) e = REF_EINVAL;
             else e = ref_watermark(&cur, wm, &nx, s->a[0], s->a[1], (float)s->d[0]);

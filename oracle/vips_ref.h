@@ -57,7 +57,10 @@ typedef struct {
     int wm_enable;
     int wm_left, wm_top;
     float wm_opacity;
+    int interpretation;  /* bimg Interpretation at save: 0 = keep, REF_INTERPRETATION_BW */
 } ref_opts;
+
+#define REF_INTERPRETATION_BW 26  /* VIPS_INTERPRETATION_B_W (bimg InterpretationBW) */
 
 typedef struct {
     int w, h, bands;     /* header size of the ENCODED input (pre shrink-on-load) */
@@ -76,7 +79,11 @@ enum {
     REF_OP_EMBED,        /* a[0..3] = x, y, width, height, a[4] = extend, a[5..7] = bg */
     REF_OP_SMARTCROP,    /* a[0..1] = width, height */
     REF_OP_BLUR,         /* d[0] = sigma, d[1] = min_ampl (effective) */
-    REF_OP_WATERMARK     /* a[0..1] = left, top; d[0] = opacity */
+    REF_OP_WATERMARK,    /* a[0..1] = left, top; d[0] = opacity */
+    REF_OP_AFFINE,       /* d[0] = xscale, d[1] = yscale; a[0] = extend (vips_affine bicubic) */
+    REF_OP_ZOOM,         /* a[0] = xfac, a[1] = yfac (vips_zoom) */
+    REF_OP_FLATTEN,      /* a[0..2] = background rgb (vips_flatten) */
+    REF_OP_BW            /* vips_colourspace sRGB -> B_W */
 };
 
 #define REF_MAX_STEPS 16
@@ -128,6 +135,13 @@ int ref_flip(const ref_img *in, ref_img *out, int vertical);
 /* ---- convolution ---- */
 int ref_gaussmat(double sigma, double min_ampl, int *mask, int max_width, int *scale);
 int ref_gaussblur(const ref_img *in, ref_img *out, double sigma, double min_ampl);
+
+/* ---- affine (bicubic) / zoom / flatten / colourspace ---- */
+int ref_bicubic_table(int *table);  /* 129 x 4 truncated 12-bit Catmull-Rom taps */
+int ref_affine(const ref_img *in, ref_img *out, double xscale, double yscale, int extend);
+int ref_zoom(const ref_img *in, ref_img *out, int xfac, int yfac);
+int ref_flatten(const ref_img *in, ref_img *out, const int bg[3]);
+int ref_bw(const ref_img *in, ref_img *out);
 
 /* ---- composite / smartcrop ---- */
 int ref_watermark(const ref_img *base, const ref_img *wm, ref_img *out, int left, int top,

@@ -160,6 +160,40 @@ def test_gaussblur_matches_oracle(gpu, oracle, rng, sigma, b):
                 f"blur {sigma}")
 
 
+# ---------------------------------------------------------------- affine (enlarge) / zoom / flatten / B_W
+@pytest.mark.parametrize("h,w,b,xs,ys,extend", [(30, 40, 3, 2.0, 2.0, 1), (17, 23, 4, 3.004291845493562, 3.004291845493562, 1),
+                                              (33, 29, 1, 1.7, 0.8, 1), (20, 20, 3, 2.5, 2.5, 0), (15, 31, 2, 1.3, 4.1, 3),
+                                              (12, 9, 3, 7.0, 7.0, 2), (25, 25, 4, 1.5, 1.5, 4)])
+def test_affine_matches_oracle(gpu, oracle, rng, h, w, b, xs, ys, extend):
+    imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+    got = gpu.run_op("affine", imgs, xscale=xs, yscale=ys, extend=extend)
+    for i in range(2):
+        assert_same(got[i], oracle.affine(imgs[i], xs, ys, extend), f"affine {xs}x{ys} e{extend} img{i}")
+
+
+@pytest.mark.parametrize("b", [1, 2, 3, 4])
+def test_zoom_flatten_bw_match_oracle(gpu, oracle, rng, b):
+    imgs = np.stack([rand_img(rng, 19, 23, b), smooth_img(rng, 19, 23, b)])
+    for xf, yf in ((2, 2), (3, 1), (1, 4), (5, 3)):
+        got = gpu.run_op("zoom", imgs, xfac=xf, yfac=yf)
+        for i in range(2):
+            assert_same(got[i], oracle.zoom(imgs[i], xf, yf), f"zoom {xf}x{yf}")
+    got = gpu.run_op("flatten", imgs, background=(200, 17, 90))
+    for i in range(2):
+        assert_same(got[i], oracle.flatten(imgs[i], (200, 17, 90)), "flatten")
+    got = gpu.run_op("bw", imgs)
+    for i in range(2):
+        assert_same(got[i], oracle.bw(imgs[i]), "bw")
+
+
+def test_bw_every_grey_level(gpu, oracle):
+    """All 256^3 / 4096 sampled colours through B_W: the float LUT pipeline is exact."""
+    v = np.arange(0, 256, 5, dtype=np.uint8)
+    rgb = np.stack(np.meshgrid(v, v, v, indexing="ij"), -1).reshape(-1, 3)
+    img = rgb.reshape(1, -1, 3)
+    assert_same(gpu.run_op("bw", img)[0], oracle.bw(img), "bw grid")
+
+
 # ---------------------------------------------------------------- watermark composite
 @pytest.mark.parametrize("bb,wb", [(3, 3), (3, 4), (4, 4), (4, 3), (1, 2), (2, 2)])
 @pytest.mark.parametrize("opacity", [0.5, 1.0, 0.2])
@@ -200,6 +234,15 @@ PLANS = [
     (dict(width=300, height=200, crop=1, sigma=1.5), (640, 480, 4, "png", 0)),
     (dict(width=251, height=99, crop=1, gravity=3), (1001, 333, 3, "png", 0)),
     (dict(width=768, height=512, crop=1), (1024, 1024, 4, "png", 0)),
+    # Enlarge (affine bicubic), Zoom, flatten, colorspace=bw
+    (dict(width=400, height=300, enlarge=1, crop=1), (200, 150, 3, "png", 0)),
+    (dict(width=1000, height=700, enlarge=1, crop=1), (333, 233, 3, "png", 0)),
+    (dict(width=500, enlarge=1, embed=1), (123, 77, 4, "png", 0)),
+    (dict(zoom=1), (41, 29, 3, "png", 0)),
+    (dict(zoom=2, top=5, left=7, area_width=30, area_height=20), (40, 30, 4, "png", 0)),
+    (dict(width=150, background=(250, 20, 3)), (300, 200, 4, "png", 0)),
+    (dict(width=150, interpretation=26), (300, 200, 3, "png", 0)),
+    (dict(width=150, interpretation=26, background=(9, 9, 9)), (300, 200, 4, "png", 0)),
 ]
 
 

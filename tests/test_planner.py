@@ -148,14 +148,51 @@ def test_rotate_angle_normalisation(rotate, angle):
         assert ops[0][0] == "rot" and ops[0][1][0] == angle
 
 
-def test_unsupported_ops_fall_back():
-    """Enlarge (vips_affine) and zoom are outside the engine: MIPX_EUNSUPPORTED."""
-    with pytest.raises(ia.MipxError) as e:
-        ia.plan_make(ia.make_opts(width=800, height=600, enlarge=1, crop=1), ia.make_input(400, 300, 3, "png"))
-    assert e.value.code == -2
-    with pytest.raises(ia.MipxError) as e:
-        ia.plan_make(ia.make_opts(zoom=2), ia.make_input(400, 300, 3, "png"))
-    assert e.value.code == -2
+def test_enlarge_is_bicubic_affine(oracle):
+    """Enlarge (image.go:202): residual > 1 -> vipsAffine(residual) with the bimg
+    default bicubic interpolator; output = ceil(w * r) x ceil(h * r), then the
+    crop/embed to the exact target (bimg transformImage / extractOrEmbedImage)."""
+    cases = [(dict(width=800, height=600, enlarge=1, crop=1), (400, 300), [("affine", (800, 600))], (800, 600)),
+             (dict(width=1000, height=700, enlarge=1, crop=1), (333, 233), None, (1000, 700)),
+             (dict(width=500, enlarge=1, embed=1), (123, 77), None, (500, 313))]
+    for opts, (w, h), want_steps, want_out in cases:
+        p = ia.plan_make(ia.make_opts(**opts), ia.make_input(w, h, 3, "png"))
+        e, rp = oracle.plan(opts, dict(w=w, h=h, bands=3, type=3))
+        assert e == 0 and _steps(p) == _steps(rp), (opts, p.describe())
+        assert p.describe()[0][0] == "affine"
+        if want_steps:
+            assert [(s[0], s[3][:2]) for s in p.describe()] == want_steps
+        if want_out:
+            assert (p.out_w, p.out_h) == want_out
+
+
+def test_zoom_plans(oracle):
+    """Zoom (image.go:286): vips_zoom(factor + 1) before the transform; with an
+    area the extract reads the zoomed image (bimg zoomImage)."""
+    for opts, (w, h), want in [(dict(zoom=1), (40, 30), (80, 60)), (dict(zoom=3), (17, 11), (68, 44)),
+                               (dict(zoom=1, top=5, left=7, area_width=30, area_height=20), (40, 30), (30, 20))]:
+        p = ia.plan_make(ia.make_opts(**opts), ia.make_input(w, h, 3, "png"))
+        e, rp = oracle.plan(opts, dict(w=w, h=h, bands=3, type=3))
+        assert e == 0 and _steps(p) == _steps(rp)
+        assert p.describe()[0][0] == "zoom" and (p.out_w, p.out_h) == want
+
+
+def test_flatten_and_bw_plans(oracle):
+    """imageFlatten (PNG input, non-black background, alpha) drops the alpha band;
+    colorspace=bw (params.go:392 -> Interpretation B_W) converts at save."""
+    for opts, typ, bands, want_ops, want_bands in [
+            (dict(width=250, background=(10, 20, 30)), "png", 4, ["reduce", "flatten"], 3),
+            (dict(width=250, background=(10, 20, 30)), "jpeg", 4, ["reduce"], 4),
+            (dict(width=250, background=(0, 0, 0)), "png", 4, ["reduce"], 4),
+            (dict(width=250, background=(0, 0, 9)), "png", 2, ["reduce", "flatten"], 1),
+            (dict(width=250, interpretation=26), "png", 3, ["reduce", "bw"], 1),
+            (dict(width=250, interpretation=26), "png", 4, ["reduce", "bw"], 2),
+            (dict(width=250, interpretation=22), "png", 3, ["reduce"], 3),
+            (dict(width=250, interpretation=26, background=(5, 5, 5)), "png", 4, ["reduce", "flatten", "bw"], 1)]:
+        p = ia.plan_make(ia.make_opts(**opts), ia.make_input(400, 300, bands, typ))
+        e, rp = oracle.plan(opts, dict(w=400, h=300, bands=bands, type=ia.TYPES[typ]))
+        assert e == 0 and _steps(p) == _steps(rp), opts
+        assert [s[0] for s in p.describe()] == want_ops and p.out_bands == want_bands, (opts, p.describe())
 
 
 def test_extract_out_of_bounds_is_einval():
@@ -194,7 +231,10 @@ def test_random_plans_agree_with_oracle(oracle):
                     crop=int(r.integers(0, 2)), embed=int(r.integers(0, 2)), force=int(r.integers(0, 2)),
                     gravity=int(r.integers(0, 6)), extend=int(r.integers(0, 7)),
                     rotate=int(r.choice([0, 0, 90, 180, 270, 45])), flip=int(r.integers(0, 2)),
-                    flop=int(r.integers(0, 2)), sigma=float(r.choice([0, 0, 1.5, 5.0])))
+                    flop=int(r.integers(0, 2)), sigma=float(r.choice([0, 0, 1.5, 5.0])),
+                    enlarge=int(r.integers(0, 2)), zoom=int(r.choice([0, 0, 0, 1, 2])),
+                    interpretation=int(r.choice([0, 22, 26])),
+                    background=[int(v) for v in r.choice([[0, 0, 0], [255, 10, 3]])])
         typ = int(r.choice([1, 2, 3]))
         orient = int(r.integers(0, 9))
         inp = dict(w=w, h=h, bands=int(r.integers(1, 5)), type=typ, orientation=orient)
