@@ -18,13 +18,14 @@ bimg.Resize there.
 from __future__ import annotations
 
 import dataclasses
+import json
 import math
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
 import numpy as np
 
-from . import _abi
+from . import _abi, codec
 from .engine import Engine, fit_dimension, make_input, make_opts, plan_make
 
 HTTP_BAD_REQUEST = 400
@@ -83,6 +84,9 @@ class ImageOptions:
     background: List[int] = field(default_factory=list)
     extend: int = 1          # bimg.ExtendCopy default (params.go:342, 356)
     colorspace: int = 0      # bimg.Interpretation (params.go:260, parseColorspace 392)
+    quality: int = 0
+    compression: int = 0
+    text: str = ""           # Watermark (text): pango rendering, not a pixel-engine op
     gravity: int = 0
     operations: List[Dict[str, Any]] = field(default_factory=list)
     is_defined: IsDefinedField = field(default_factory=IsDefinedField)
@@ -155,7 +159,8 @@ def build_params_from_query(query: Dict[str, Any]) -> ImageOptions:
     """params.go:354-366 for the pixel-relevant parameters (Extend defaults to copy)."""
     o = ImageOptions()
     ints = {"width": "width", "height": "height", "areawidth": "area_width", "areaheight": "area_height",
-            "rotate": "rotate", "top": "top", "left": "left", "factor": "factor"}
+            "rotate": "rotate", "top": "top", "left": "left", "factor": "factor", "quality": "quality",
+            "compression": "compression"}
     for k, v in query.items():
         v = v if isinstance(v, str) else str(v) if not isinstance(v, (list, dict, bool)) else v
         if k in ints:
@@ -181,6 +186,8 @@ def build_params_from_query(query: Dict[str, Any]) -> ImageOptions:
             o.aspect_ratio = v
         elif k == "image":
             o.image = v
+        elif k == "text":
+            o.text = v
         elif k == "operations":
             o.operations = v
     return o
@@ -211,6 +218,12 @@ def bimg_options(o: ImageOptions) -> Dict[str, Any]:
     b["width"], b["height"] = _aspect(o, o.width, o.height)
     if o.sigma > 0 or o.min_ampl > 0:
         b["sigma"], b["min_ampl"] = o.sigma, o.min_ampl
+    if o.type:
+        b["type"] = o.type            # encode-side: bimg Type (options.go:138)
+    if o.quality:
+        b["quality"] = o.quality
+    if o.compression:
+        b["compression"] = o.compression
     return b
 
 
@@ -219,21 +232,36 @@ _ENGINE: Optional[Engine] = None
 
 
 def engine() -> Engine:
+    """The process-wide request engine (mipx_init is idempotent, so this also
+    re-initialises after an mipx_shutdown)."""
     global _ENGINE
-    if _ENGINE is None:
-        _ENGINE = Engine()
+    _ENGINE = Engine()
     return _ENGINE
 
 
 Decoder = Callable[[Decoded, int], np.ndarray]
 
 
-def process(img: Decoded, opts: Dict[str, Any], wm: Optional[np.ndarray] = None,
-            redecode: Optional[Decoder] = None) -> np.ndarray:
-    """image.go:81-113 with bimg.Resize's pixel work on the GPU.
+@dataclass
+class Image:
+    """image.go:34-37."""
+    body: bytes
+    mime: str
 
+
+_ENCODE_ONLY = ("type", "quality", "compression")
+
+
+def process(img, opts: Dict[str, Any], wm=None, redecode: Optional[Decoder] = None):
+    """image.go:81-113 Process with bimg.Resize's pixel work on the GPU.
+
+    Encoded bytes in -> Image out (the drop-in: host codec, engine, host codec);
+    a Decoded in -> pixels out (the engine alone, for callers that own the codec).
     `redecode(img, s)` is the host codec's shrink-on-load (libjpeg scale 1/s);
     without one, a plan that asks for load_shrink > 1 is rejected."""
+    if isinstance(img, (bytes, bytearray, memoryview)):
+        return process_bytes(bytes(img), opts, wm)
+    opts = {k: v for k, v in opts.items() if k not in _ENCODE_ONLY}
     px = img.pixels if img.pixels.ndim == 3 else img.pixels[:, :, None]
     inp = make_input(img.w, img.h, px.shape[2], img.type, img.orientation)
     if wm is not None:
@@ -257,8 +285,53 @@ def process(img: Decoded, opts: Dict[str, Any], wm: Optional[np.ndarray] = None,
         raise ImaginaryError(f"image processing error: {e}", 500) from e
 
 
+def process_bytes(buf: bytes, opts: Dict[str, Any], wm=None) -> Image:
+    """Process(buf, opts) over encoded bytes: header -> plan -> decode (with the
+    plan's shrink-on-load) -> engine -> encode; WEBP/HEIF/AVIF encode failures
+    retry as JPEG (image.go:97-107); MIME from the output bytes (image.go:109-112)."""
+    opts = dict(opts)
+    out_type = str(opts.pop("type", "") or "")
+    quality = int(opts.pop("quality", 0) or 0)
+    compression = opts.pop("compression", 0) or None
+    try:
+        hdr = codec.header(buf)
+        wm_px = codec.decode(bytes(wm)) if isinstance(wm, (bytes, bytearray)) else wm
+    except codec.CodecError as e:
+        raise ImaginaryError(str(e), HTTP_BAD_REQUEST) from e
+
+    def redecode(_img: Decoded, s: int) -> np.ndarray:
+        return codec.decode(buf, s)
+
+    itype = hdr.type if hdr.type in _abi.TYPES else "unknown"
+    if wm_px is not None:
+        opts = dict(opts, wm_enable=1)
+    # plan on the header first: the decode depends on the plan's shrink-on-load
+    inp = make_input(hdr.w, hdr.h, hdr.bands, itype, hdr.orientation)
+    if wm_px is not None:
+        inp.wm_w, inp.wm_h, inp.wm_bands = wm_px.shape[1], wm_px.shape[0], (wm_px.shape[2] if wm_px.ndim == 3 else 1)
+    try:
+        plan = plan_make(make_opts(**opts), inp)
+    except _abi.MipxError as e:
+        if e.code == _abi.MIPX_EUNSUPPORTED:
+            raise EngineUnsupported(str(e)) from e
+        raise ImaginaryError(f"image processing error: {e}", 500) from e
+    if plan.load_shrink > 1:  # process() re-plans on the codec-shrunk size
+        src = Decoded(np.zeros((1, 1, hdr.bands), np.uint8), itype, hdr.orientation, hdr.w, hdr.h)
+        px = process(src, opts, wm=wm_px, redecode=redecode)
+    else:
+        px = process(Decoded(codec.decode(buf), itype, hdr.orientation), opts, wm=wm_px)
+    t = out_type or (hdr.type if hdr.type in ("jpeg", "png", "webp", "gif", "tiff") else "png")
+    try:
+        body = codec.encode(px, t, quality or None, compression)
+    except codec.CodecError as e:
+        if t not in ("webp", "heif", "avif"):
+            raise ImaginaryError(f"image processing error: {e}", 500) from e
+        body = codec.encode(px, "jpeg", quality or None)
+    return Image(body, codec.mime_type(codec.sniff_type(body)))
+
+
 # ---- image.go operations ----------------------------------------------------------------
-def Resize(img: Decoded, o: ImageOptions, **kw):
+def Resize(img, o: ImageOptions, **kw):
     if o.width == 0 and o.height == 0:
         raise ImaginaryError("Missing required param: height or width")
     opts = bimg_options(o)
@@ -272,14 +345,21 @@ def calculate_destination_fit_dimension(iw, ih, fw, fh):
     return fit_dimension(iw, ih, fw, fh)
 
 
-def Fit(img: Decoded, o: ImageOptions, **kw):
+def Fit(img, o: ImageOptions, **kw):
     if o.width == 0 or o.height == 0:
         raise ImaginaryError("Missing required params: height, width")
-    w, h = img.w, img.h
+    if isinstance(img, (bytes, bytearray, memoryview)):  # bimg.Metadata (image.go:144)
+        try:
+            m = codec.header(bytes(img))
+        except codec.CodecError as e:
+            raise ImaginaryError(str(e)) from e
+        w, h, orientation = m.w, m.h, m.orientation
+    else:
+        w, h, orientation = img.w, img.h, img.orientation
     if w == 0 or h == 0:
         raise ImaginaryError("Width or height of requested image is zero", HTTP_NOT_ACCEPTABLE)
     o = dataclasses.replace(o)
-    if o.no_rotation or img.orientation <= 4:
+    if o.no_rotation or orientation <= 4:
         o.width, o.height = calculate_destination_fit_dimension(w, h, o.width, o.height)
     else:  # width/height switched by auto rotation
         o.height, o.width = calculate_destination_fit_dimension(h, w, o.height, o.width)
@@ -288,7 +368,7 @@ def Fit(img: Decoded, o: ImageOptions, **kw):
     return process(img, opts, **kw)
 
 
-def Enlarge(img: Decoded, o: ImageOptions, **kw):
+def Enlarge(img, o: ImageOptions, **kw):
     if o.width == 0 or o.height == 0:
         raise ImaginaryError("Missing required params: height, width")
     opts = bimg_options(o)
@@ -297,7 +377,7 @@ def Enlarge(img: Decoded, o: ImageOptions, **kw):
     return process(img, opts, **kw)
 
 
-def Extract(img: Decoded, o: ImageOptions, **kw):
+def Extract(img, o: ImageOptions, **kw):
     if o.area_width == 0 or o.area_height == 0:
         raise ImaginaryError("Missing required params: areawidth or areaheight")
     opts = bimg_options(o)
@@ -305,7 +385,7 @@ def Extract(img: Decoded, o: ImageOptions, **kw):
     return process(img, opts, **kw)
 
 
-def Crop(img: Decoded, o: ImageOptions, **kw):
+def Crop(img, o: ImageOptions, **kw):
     if o.width == 0 and o.height == 0:
         raise ImaginaryError("Missing required param: height or width")
     opts = bimg_options(o)
@@ -313,7 +393,7 @@ def Crop(img: Decoded, o: ImageOptions, **kw):
     return process(img, opts, **kw)
 
 
-def SmartCrop(img: Decoded, o: ImageOptions, **kw):
+def SmartCrop(img, o: ImageOptions, **kw):
     if o.width == 0 and o.height == 0:
         raise ImaginaryError("Missing required param: height or width")
     opts = bimg_options(o)
@@ -322,31 +402,63 @@ def SmartCrop(img: Decoded, o: ImageOptions, **kw):
     return process(img, opts, **kw)
 
 
-def Rotate(img: Decoded, o: ImageOptions, **kw):
+def Rotate(img, o: ImageOptions, **kw):
     if o.rotate == 0:
         raise ImaginaryError("Missing required param: rotate")
     return process(img, bimg_options(o), **kw)
 
 
-def Flip(img: Decoded, o: ImageOptions, **kw):
+def AutoRotate(img, o: ImageOptions, **kw):
+    """image.go:255-265: bimg AutoRotate = the EXIF rotation/flip alone, same type."""
+    return process(img, dict(no_auto_rotate=0), **kw)
+
+
+def Convert(img, o: ImageOptions, **kw):
+    """image.go:312-320."""
+    if o.type == "":
+        raise ImaginaryError("Missing required param: type")
+    if o.type not in ("jpeg", "png", "webp", "tiff", "gif", "heif", "avif", "pdf", "svg", "magick", "auto"):
+        raise ImaginaryError("Invalid image type: " + o.type)
+    return process(img, bimg_options(o), **kw)
+
+
+def Watermark(img, o: ImageOptions, **kw):
+    """image.go:322-341: text watermark (pango rendering) stays with libvips."""
+    if o.text == "":
+        raise ImaginaryError("Missing required param: text")
+    raise EngineUnsupported("text watermark is rendered by libvips, not the pixel engine")
+
+
+def Info(buf: bytes, o: ImageOptions, **kw) -> Image:
+    """image.go:56-79: metadata only (host codec header), no pixel work."""
+    try:
+        h = codec.header(buf)
+    except codec.CodecError as e:
+        raise ImaginaryError("Cannot retrieve image metadata: " + str(e)) from e
+    info = {"width": h.w, "height": h.h, "type": h.type, "space": "b-w" if h.bands <= 2 else "srgb",
+            "hasAlpha": h.bands in (2, 4), "hasProfile": False, "channels": h.bands, "orientation": h.orientation}
+    return Image(json.dumps(info).encode(), "application/json")
+
+
+def Flip(img, o: ImageOptions, **kw):
     opts = bimg_options(o)
     opts["flip"] = 1
     return process(img, opts, **kw)
 
 
-def Flop(img: Decoded, o: ImageOptions, **kw):
+def Flop(img, o: ImageOptions, **kw):
     opts = bimg_options(o)
     opts["flop"] = 1
     return process(img, opts, **kw)
 
 
-def Thumbnail(img: Decoded, o: ImageOptions, **kw):
+def Thumbnail(img, o: ImageOptions, **kw):
     if o.width == 0 and o.height == 0:
         raise ImaginaryError("Missing required params: width or height")
     return process(img, bimg_options(o), **kw)
 
 
-def Zoom(img: Decoded, o: ImageOptions, **kw):
+def Zoom(img, o: ImageOptions, **kw):
     if o.factor == 0:
         raise ImaginaryError("Missing required param: factor")
     opts = bimg_options(o)
@@ -360,17 +472,17 @@ def Zoom(img: Decoded, o: ImageOptions, **kw):
     return process(img, opts, **kw)
 
 
-def GaussianBlur(img: Decoded, o: ImageOptions, **kw):
+def GaussianBlur(img, o: ImageOptions, **kw):
     if o.sigma == 0 and o.min_ampl == 0:
         raise ImaginaryError("Missing required param: sigma or minampl")
     return process(img, bimg_options(o), **kw)
 
 
-def WatermarkImage(img: Decoded, o: ImageOptions, wm: Optional[np.ndarray] = None, **kw):
+def WatermarkImage(img, o: ImageOptions, wm: Optional[np.ndarray] = None, **kw):
     """image.go:343-370; the watermark bytes are fetched (and decoded) by the host."""
     if o.image == "" and wm is None:
         raise ImaginaryError("Missing required param: image")
-    if wm is None or wm.size == 0:
+    if wm is None or len(wm) == 0 or (isinstance(wm, np.ndarray) and wm.size == 0):
         raise ImaginaryError("Unable to read watermark image")
     opts = bimg_options(o)
     opts.update(wm_left=o.left, wm_top=o.top, wm_opacity=float(o.opacity))
@@ -379,13 +491,33 @@ def WatermarkImage(img: Decoded, o: ImageOptions, wm: Optional[np.ndarray] = Non
 
 OperationsMap: Dict[str, Callable] = {
     "crop": Crop, "resize": Resize, "enlarge": Enlarge, "extract": Extract, "rotate": Rotate,
-    "flip": Flip, "flop": Flop, "thumbnail": Thumbnail, "zoom": Zoom,
-    "watermarkImage": WatermarkImage, "blur": GaussianBlur, "smartcrop": SmartCrop, "fit": Fit,
+    "autorotate": AutoRotate, "flip": Flip, "flop": Flop, "thumbnail": Thumbnail, "zoom": Zoom,
+    "convert": Convert, "watermark": Watermark, "watermarkImage": WatermarkImage, "blur": GaussianBlur,
+    "smartcrop": SmartCrop, "fit": Fit,
 }
 
 
-def Pipeline(img: Decoded, o: ImageOptions, **kw):
-    """image.go:379-410 with lossless (PNG) intermediates kept as pixels."""
+def Pipeline(img, o: ImageOptions, **kw):
+    """image.go:379-410.  On encoded bytes every stage decodes and re-encodes in
+    the stage's output format, exactly as the reference; on a Decoded input the
+    intermediates stay pixels (lossless, as PNG intermediates would be)."""
+    if isinstance(img, (bytes, bytearray, memoryview)):
+        if len(o.operations) == 0:
+            raise ImaginaryError("Missing pipeline operations")
+        if len(o.operations) > 10:
+            raise ImaginaryError("Maximum pipeline operations (10) exceeded")
+        out = Image(bytes(img), codec.mime_type(codec.sniff_type(img)))
+        for op in o.operations:
+            name = op.get("operation") or op.get("name")
+            fn = OperationsMap.get(name)
+            if fn is None:
+                raise ImaginaryError(f"Unsupported operation: {name}")
+            try:
+                out = fn(out.body, build_params_from_query(op.get("params", {})), **kw)
+            except ImaginaryError:
+                if not op.get("ignore_failure"):
+                    raise
+        return out
     if len(o.operations) == 0:
         raise ImaginaryError("Missing pipeline operations")
     if len(o.operations) > 10:
