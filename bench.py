@@ -60,7 +60,7 @@ def cpu_baseline(args, sample):
                       f"(reducev+reduceh Lanczos3 2x2), {threads} OpenMP threads, {dt:.2f} s wall"}
 
 
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic_v6.json")
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r01", "traffic_v10.json")
 
 
 def pmc_traffic(kernel_name_hint):
@@ -173,7 +173,7 @@ def main():
         value = images / wall_max
         alg_bytes = n * (in_img + out_img)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        variant = os.environ.get("MIPX_R2_VARIANT", "2")
+        variant = os.environ.get("MIPX_R2_VARIANT", "66")
         traffic, traffic_src = pmc_traffic(f"k_reduce2x2<3, {variant}>")
         line = {
             "metric": "images/sec (4K RGB->1080p Lanczos3 batch) + achieved HBM GB/s, 1/2/4/8 GPUs",

@@ -49,17 +49,25 @@ using namespace dev;
 // workgroup, so occupancy is set by registers, not LDS.
 // ===========================================================================
 constexpr int kR = 12;           // output rows per LDS chunk (2 ring periods)
-constexpr int kThreads = 128;
-constexpr int kPitch = 160;      // LDS dwords per intermediate row (== 32 mod 64)
+// WIDE (variant bit 6): 256 threads and strips twice as wide (half the
+// relative halo, 480-byte output row segments, half the workgroups)
+template <bool WIDE>
+struct R2T {
+    static constexpr int kThreads = WIDE ? 256 : 128;
+    static constexpr int kPitch = WIDE ? 288 : 160;  // LDS dwords per intermediate row (== 32 mod 64)
+};
 
-template <int B>
+template <int B, bool WIDE = false>
 struct R2 {
-    static constexpr int TW = B == 3 ? 80 : 56;     // output pixels per strip
+    static constexpr int kThreads = R2T<WIDE>::kThreads;
+    static constexpr int kPitch = R2T<WIDE>::kPitch;
+    static constexpr int TW = WIDE ? (B == 3 ? 160 : 120) : (B == 3 ? 80 : 56);  // output pixels per strip
     static constexpr int NPX = 2 * TW + 9;           // intermediate px 2x0-5 .. 2x0+2TW+3
     static constexpr int K = B == 3 ? 4 : 2;         // output pixels per horizontal item
     static constexpr int OFF0 = B == 3 ? 1 : 0;      // B*(2x0-5) - floor4(B*(2x0-5))
     static constexpr int ND = (B * NPX + OFF0 + 3) / 4;  // dwords per row
     static_assert(ND <= kThreads && ND <= kPitch, "strip too wide");
+    static_assert(((TW / K) * K) == TW, "items must tile the strip");
     static_assert((B * 2 * K) % 8 == 0, "window start must be 8-byte aligned");
 };
 
@@ -113,10 +121,11 @@ __device__ __forceinline__ uint32_t pack4b(float a, float b, float c, float d) {
     return __builtin_amdgcn_cvt_pk_u8_f32(d, 3, v);
 }
 
-template <int B, int R, bool PF, bool PK, bool MEM, int LAUX, bool NTS>
+template <int B, int R, bool PF, bool PK, bool MEM, int LAUX, bool NTS, bool WIDE>
 __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int strip, int band,
                                              uint32_t *lds) {
-    using G = R2<B>;
+    using G = R2<B, WIDE>;
+    constexpr int kThreads = G::kThreads, kPitch = G::kPitch;
     constexpr int TW = G::TW, K = G::K;
     const int tid = threadIdx.x;
     const int x0 = strip * TW;
@@ -320,11 +329,14 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 // Variant bits (A/B in one process via MIPX_R2_VARIANT; default = best measured):
 // bit 0: R = 6 (else 12), bit 1: register prefetch of the next chunk,
 // bit 2: packed-FP32 vertical taps, bit 3: memory-only diagnostic (not exact),
-// bit 4: non-temporal loads, bit 5: non-temporal stores.  Measured in
+// bit 4: non-temporal loads, bit 5: non-temporal stores, bit 6: 256-thread
+// workgroups over strips twice as wide.  Measured in
 // profiles/r01/v7_variants_ab.log: the memory-only build is no faster than the
 // full one (the arithmetic is hidden), packed math and nt hints lose.
 template <int B, int VAR>
-__global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
+__global__ void __launch_bounds__(R2T<(VAR & 64) != 0>::kThreads) k_reduce2x2(Reduce2Args a) {
+    constexpr bool WIDE = (VAR & 64) != 0;
+    constexpr int kPitch = R2T<WIDE>::kPitch;
     constexpr int R = (VAR & 1) ? 6 : 12;
     constexpr bool PF = (VAR & 2) != 0;
     constexpr bool PK = (VAR & 4) != 0;
@@ -345,7 +357,7 @@ __global__ void __launch_bounds__(kThreads) k_reduce2x2(Reduce2Args a) {
         band = rest % a.n_bands;
         img = rest / a.n_bands;
     }
-    reduce2_tile<B, R, PF, PK, MEM, LAUX, NTS>(a, img, strip, band, lds);
+    reduce2_tile<B, R, PF, PK, MEM, LAUX, NTS, WIDE>(a, img, strip, band, lds);
 }
 
 
@@ -451,13 +463,13 @@ bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
 
 // MIPX_R2_VARIANT overrides the default variant of k_reduce2x2 for A/B runs
 // (scripts/ab_reduce.py); read per launch so one process can interleave them.
-constexpr int kR2Default = 2;  // R = 12 + register prefetch: measured best (profiles/r01/v5_variants_ab.log)
+constexpr int kR2Default = 66;  // wide strips, R = 12 + register prefetch: measured best (profiles/r01/v10_wide_ab.log)
 int reduce2_variant() {
     const char *e = std::getenv("MIPX_R2_VARIANT");
     if (!e || !*e) return kR2Default;
     const int v = std::atoi(e);
     switch (v) {
-        case 0: case 1: case 2: case 3: case 6: case 10: return v;
+        case 0: case 1: case 2: case 3: case 6: case 10: case 66: case 67: return v;
         default: return kR2Default;
     }
 }
@@ -472,7 +484,9 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     a.h = h;
     a.ow = out_size_reduce(w, 2.0);
     a.oh = out_size_reduce(h, 2.0);
-    const int tw = b == 3 ? R2<3>::TW : R2<4>::TW;
+    const int var = reduce2_variant();
+    const bool wide = (var & 64) != 0;
+    const int tw = b == 3 ? (wide ? R2<3, true>::TW : R2<3>::TW) : (wide ? R2<4, true>::TW : R2<4>::TW);
     a.n_strips = (a.ow + tw - 1) / tw;
     const int chunks = (a.oh + kR - 1) / kR;
     // rows per workgroup: 2 chunks of 12 (measured best, profiles/r01/geom_ab.log; MIPX_R2_BAND overrides)
@@ -495,14 +509,15 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
     dim3 grid(static_cast<unsigned>(tiles));
-    const int var = reduce2_variant();
-#define MIPX_R2(V)                                                                           \
-    case V:                                                                                  \
-        if (b == 3) hipLaunchKernelGGL((k_reduce2x2<3, V>), grid, dim3(kThreads), 0, st, a); \
-        else hipLaunchKernelGGL((k_reduce2x2<4, V>), grid, dim3(kThreads), 0, st, a);        \
-        break;
+#define MIPX_R2(V)                                                                                      \
+    case V: {                                                                                           \
+        const dim3 blk(R2T<(V & 64) != 0>::kThreads);                                                   \
+        if (b == 3) hipLaunchKernelGGL((k_reduce2x2<3, V>), grid, blk, 0, st, a);                       \
+        else hipLaunchKernelGGL((k_reduce2x2<4, V>), grid, blk, 0, st, a);                              \
+        break;                                                                                          \
+    }
     switch (var) {
-        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3) MIPX_R2(6) MIPX_R2(10)
+        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3) MIPX_R2(6) MIPX_R2(10) MIPX_R2(66) MIPX_R2(67)
         default: return MIPX_EINVAL;
     }
 #undef MIPX_R2

@@ -70,6 +70,20 @@ def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
 
 
+@pytest.mark.parametrize("var", [0, 1, 2, 3, 6, 66, 67])
+def test_reduce2x2_variants_exact(gpu, oracle, rng, var, monkeypatch):
+    """Every A/B build of the fused 2x2 kernel (MIPX_R2_VARIANT, read per launch)
+    is bit-exact, including strips that end at the image edge."""
+    monkeypatch.setenv("MIPX_R2_VARIANT", str(var))
+    for h, w, b in ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1001 * 4 // 4 - 1, 4), (200, 646, 3)):
+        if (w * b) % 4:
+            continue
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("reduce", imgs, hshrink=2.0, vshrink=2.0)
+        for i in range(2):
+            assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"var {var} {h}x{w}x{b} img{i}")
+
+
 @pytest.mark.parametrize("h,w,b,s", [(50, 60, 3, 1.6), (31, 45, 4, 2.0), (20, 33, 1, 3.3)])
 def test_reducev_reduceh_separately(gpu, oracle, rng, h, w, b, s):
     img = rand_img(rng, h, w, b)
