@@ -411,6 +411,8 @@ int reduce_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     if (vs > 1.0 && !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
     if (hs > 1.0 && !sep_spec_reduce(hs, &sh)) return MIPX_EDEVICE;
     if (vs > 1.0 && hs > 1.0) {
+        const int fe = reduce_fused_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
+        if (fe != MIPX_EUNSUPPORTED) return fe;
         const size_t need = align_up(static_cast<size_t>(n) * w * oh * b);
         if (!ws || ws_bytes < need) return MIPX_EINVAL;
         u8 *tmp = static_cast<u8 *>(ws);

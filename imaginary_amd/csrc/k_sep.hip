@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "device_common.h"
 
@@ -391,6 +392,176 @@ __global__ void __launch_bounds__(256) k_hpass_gather(HPassArgs a) {
     for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_u(acc[z]));
 }
 
+// ===========================================================================
+// fused reduce: reducev -> reduceh for any shrink pair in one launch, the
+// rounded uchar intermediate kept in LDS (libvips materialises it; every value
+// is the same, it just never reaches HBM).
+//
+// A block = kFW output columns x th output rows of one image.  The input rows
+// [r_lo, r_lo + L) x columns [cl, ch] it needs are DMA'd to LDS (raw bytes from
+// each row's dword-aligned-down start, any alignment); the vertical pass turns
+// them into th intermediate rows (dword lanes, channel agnostic, byte skew
+// fixed with v_alignbyte); the rows are repacked to one u32 per pixel; the
+// horizontal pass (taps <= 16 per lane in registers) writes the outputs.
+// ===========================================================================
+constexpr int kFW = 64;          // output columns per block
+constexpr int kFMaxTaps = 16;
+
+struct FusedArgs {
+    const u8 *in;
+    u8 *out;
+    int w, h, in_pitch;
+    long long in_img, out_img;
+    int ox0, oy0, ow, oh;        // output window (op-output coordinates) and its size
+    int th;                      // output rows per block
+    int x_blocks, y_blocks;
+    int raw_stride;              // LDS dwords per staged input row
+    int lrows;                   // staged input rows capacity
+    int span_max;                // intermediate pixels per row capacity
+    SepTaps tv, thz;             // vertical / horizontal taps
+};
+
+template <int B>
+__global__ void __launch_bounds__(256) k_reduce_fused(FusedArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t fsm[];
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int yb = rest % a.y_blocks;
+    const int img = rest / a.y_blocks;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tv = a.tv.taps, thz = a.thz.taps;
+    // ---- geometry of this tile ----
+    const int x0 = xb * kFW, y0 = yb * a.th;
+    const int nx = min(kFW, a.ow - x0), ny = min(a.th, a.oh - y0);
+    int lo, hi, r_lo, r_last, ph;
+    sep_position(a.thz, a.ox0 + x0, &lo, &ph);
+    sep_position(a.thz, a.ox0 + x0 + nx - 1, &hi, &ph);
+    hi += thz - 1;
+    sep_position(a.tv, a.oy0 + y0, &r_lo, &ph);
+    sep_position(a.tv, a.oy0 + y0 + ny - 1, &r_last, &ph);
+    const int L = r_last + tv - r_lo;
+    const int cl = max(lo, 0), ch = min(hi, a.w - 1);   // intermediate columns actually computed
+    const int ncol = ch - cl + 1;
+    const int nd = (B * ncol + 3) >> 2;                 // intermediate dwords per row
+    uint32_t *raw = fsm;                                 // lrows x raw_stride
+    uint32_t *mid = raw + a.lrows * a.raw_stride;        // th x span_max (u32 per pixel)
+    float *vco = reinterpret_cast<float *>(mid + a.th * a.span_max);  // th x tv
+    int *vso = reinterpret_cast<int *>(vco + a.th * tv);               // th row starts
+    // ---- DMA the input rows ----
+    int delta = 0;
+    const u8 *src = a.in + img * a.in_img;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, &delta);
+    const int ndl = (B * ncol + 3 + 3) >> 2;            // dwords to cover any skew
+    const int chunks = (ndl + 63) >> 6;
+    for (int idx = wave; idx < L * chunks; idx += 4) {
+        const int l = idx / chunks, q = idx - l * chunks;
+        const int r = clampi(r_lo + l, 0, a.h - 1);
+        const int a4 = static_cast<int>(delta + static_cast<long long>(r) * a.in_pitch + B * cl) & ~3;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * a.raw_stride + q * 64), 4,
+                                                 4 * (q * 64 + lane), a4, 0, 0);
+    }
+    for (int i = tid; i < ny * tv; i += 256) {
+        const int k = i / tv;
+        int s2;
+        sep_position(a.tv, a.oy0 + y0 + k, &s2, &ph);
+        vco[i] = a.tv.tab[ph * tv + (i - k * tv)];
+    }
+    if (tid < ny) {
+        int s2;
+        sep_position(a.tv, a.oy0 + y0 + tid, &s2, &ph);
+        vso[tid] = s2 - r_lo;
+    }
+    // this lane's horizontal taps (lane -> output column x0 + (tid & 63))
+    const int xi = tid & 63, rgrp = tid >> 6;
+    int xs = 0, xph = 0;
+    sep_position(a.thz, a.ox0 + x0 + min(xi, nx - 1), &xs, &xph);
+    float cr[kFMaxTaps];
+    {
+        const float *c = a.thz.tab + xph * thz;
+#pragma unroll
+        for (int i = 0; i < kFMaxTaps; ++i) cr[i] = i < thz ? c[i] : 0.f;
+    }
+    __syncthreads();
+    // ---- vertical pass: ny intermediate rows x nd dwords ----
+    u8 *mid8 = reinterpret_cast<u8 *>(mid);
+    for (int it = tid; it < ny * nd; it += 256) {
+        const int k = it / nd, d = it - k * nd;
+        const int s0 = vso[k];
+        const float *ck = vco + k * tv;
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        for (int i = 0; i < tv; ++i) {
+            const int l = s0 + i;
+            const int r = clampi(r_lo + l, 0, a.h - 1);
+            const int sh = static_cast<int>(delta + static_cast<long long>(r) * a.in_pitch + B * cl) & 3;
+            const uint32_t *rp = raw + l * a.raw_stride + d;
+            const uint32_t v = __builtin_amdgcn_alignbyte(rp[1], rp[0], sh);
+            const float c = ck[i];
+            a0 = __builtin_fmaf(c, ubyte_f<0>(v), a0);
+            a1 = __builtin_fmaf(c, ubyte_f<1>(v), a1);
+            a2 = __builtin_fmaf(c, ubyte_f<2>(v), a2);
+            a3 = __builtin_fmaf(c, ubyte_f<3>(v), a3);
+        }
+        const uint32_t o = fixed_round_u(a0) | (fixed_round_u(a1) << 8) | (fixed_round_u(a2) << 16) |
+                           (fixed_round_u(a3) << 24);
+        if (B == 4) {
+            mid[k * a.span_max + (cl - lo) + d] = o;  // one pixel per dword already
+        } else {  // scatter the 4 bytes to their pixel slots (u32 per pixel)
+#pragma unroll
+            for (int z = 0; z < 4; ++z) {
+                const int byte = 4 * d + z;
+                if (byte < B * ncol) {
+                    const int px = byte / B, c = byte - px * B;
+                    mid8[(k * a.span_max + (cl - lo) + px) * 4 + c] = static_cast<u8>(o >> (8 * z));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // COPY edge of the intermediate rows: slots outside [cl, ch]
+    {
+        const int nl = cl - lo, nr = hi - ch;
+        for (int i = tid; i < ny * (nl + nr); i += 256) {
+            const int k = i / (nl + nr), f = i - k * (nl + nr);
+            uint32_t *row = mid + k * a.span_max;
+            if (f < nl) row[f] = row[nl];
+            else row[ch - lo + 1 + (f - nl)] = row[ch - lo];
+        }
+    }
+    __syncthreads();
+    // ---- horizontal pass: lane = column xi, rows rgrp, rgrp + 4, ... ----
+    if (xi >= nx) return;
+    const uint32_t *sp = mid + (xs - lo);
+    for (int k = rgrp; k < ny; k += 4) {
+        const uint32_t *rowp = sp + k * a.span_max;
+        float acc[B];
+#pragma unroll
+        for (int z = 0; z < B; ++z) acc[z] = 0.f;
+#pragma unroll
+        for (int i = 0; i < kFMaxTaps; ++i) {
+            if (i < thz) {
+                const uint32_t v = rowp[i];
+#pragma unroll
+                for (int z = 0; z < B; ++z) {
+                    const float pz = z == 0 ? ubyte_f<0>(v) : z == 1 ? ubyte_f<1>(v) : z == 2 ? ubyte_f<2>(v) : ubyte_f<3>(v);
+                    acc[z] = __builtin_fmaf(cr[i], pz, acc[z]);
+                }
+            }
+        }
+        u8 *q = a.out + img * a.out_img + (static_cast<long long>(y0 + k) * a.ow + x0 + xi) * B;
+        if (B == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int z = 0; z < B; ++z) o |= fixed_round_u(acc[z]) << (8 * z);
+            *reinterpret_cast<uint32_t *>(q) = o;
+        } else {
+#pragma unroll
+            for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_u(acc[z]));
+        }
+    }
+}
+
 bool aligned4(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
 
 SepTaps make_taps(const SepSpec &s) {
@@ -535,6 +706,61 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
 #undef MIPX_HP2
 #undef MIPX_HP3
     return launch_check("k_hpass");
+}
+
+// Fused reducev -> reduceh of the output window [ox0, ox0 + ow) x [oy0, oy0 + oh);
+// MIPX_EUNSUPPORTED when the tile would not fit LDS (caller runs two passes).
+int reduce_fused_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
+                        int ow, int oh, hipStream_t st) {
+    // Measured (profiles/r01/v11_fused_ab.log): the fused launch wins on small
+    // images (<= ~0.5 MB, the thumbnail / smartcrop / post-shrink shapes) and loses
+    // to the two DMA-staged passes on large ones.  MIPX_FUSED_REDUCE=0/1 forces it.
+    const char *ef = std::getenv("MIPX_FUSED_REDUCE");
+    if (ef && *ef) {
+        if (ef[0] == '0') return MIPX_EUNSUPPORTED;
+    } else if (img_bytes(w, h, b) > 512 * 1024) {
+        return MIPX_EUNSUPPORTED;
+    }
+    SepSpec sh, sv;
+    if (!sep_spec_reduce(hs, &sh) || !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
+    if (sh.taps > kFMaxTaps || sv.taps > 40) return MIPX_EUNSUPPORTED;
+    FusedArgs a{};
+    a.in = in;
+    a.out = out;
+    a.w = w;
+    a.h = h;
+    a.in_pitch = w * b;
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = img_bytes(ow, oh, b);
+    a.ox0 = ox0;
+    a.oy0 = oy0;
+    a.ow = ow;
+    a.oh = oh;
+    a.tv = make_taps(sv);
+    a.thz = make_taps(sh);
+    if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
+    a.span_max = static_cast<int>(std::ceil((kFW - 1) * hs)) + sh.taps + 2;
+    a.raw_stride = ((a.span_max * b + 3 + 3) / 4 + 63) / 64 * 64 + 1;  // DMA chunks of 64 dwords + alignbyte spill
+    constexpr size_t kBudget = 48 * 1024;
+    auto lds_for = [&](int th) {
+        const int lrows = static_cast<int>(std::ceil((th - 1) * vs)) + sv.taps + 2;
+        return (static_cast<size_t>(lrows) * a.raw_stride + static_cast<size_t>(th) * a.span_max) * 4 +
+               static_cast<size_t>(th) * (sv.taps + 1) * 4;
+    };
+    int th = 32;
+    while (th > 4 && lds_for(th) > kBudget) th -= 4;
+    if (lds_for(th) > 64 * 1024) return MIPX_EUNSUPPORTED;
+    th = std::min(th, oh);
+    a.th = th;
+    a.lrows = static_cast<int>(std::ceil((th - 1) * vs)) + sv.taps + 2;
+    a.x_blocks = (ow + kFW - 1) / kFW;
+    a.y_blocks = (oh + th - 1) / th;
+    const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
+    if (!grid_ok(blocks)) return MIPX_EINVAL;
+    const size_t lds = lds_for(th);
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduce_fused<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds,
+                                              st, a));
+    return launch_check("k_reduce_fused");
 }
 
 }  // namespace mipx

@@ -84,6 +84,25 @@ def test_reduce2x2_variants_exact(gpu, oracle, rng, var, monkeypatch):
             assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"var {var} {h}x{w}x{b} img{i}")
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_reduce_fused_and_two_pass_paths(gpu, oracle, rng, fused, monkeypatch):
+    """Both generic reduce paths (one fused launch / two DMA-staged passes) on the
+    same shapes, including output windows (reduce -> extract plans)."""
+    monkeypatch.setenv("MIPX_FUSED_REDUCE", fused)
+    for h, w, b, hs, vs in ((240, 427, 3, 1.4233, 1.4233), (273, 364, 3, 1.421875, 1.06640625),
+                            (97, 130, 4, 1.3333333333333333, 1.3333333333333333), (45, 61, 1, 2.9, 1.7),
+                            (60, 90, 2, 1.05, 3.3), (300, 200, 3, 2.4666666666666666, 2.4666666666666666)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+        for i in range(2):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"fused={fused} {h}x{w}x{b} {hs}x{vs}")
+    opts = dict(width=251, height=99, crop=1, gravity=3)
+    p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(401, 333, 3, "png"))
+    e, rp = oracle.plan(opts, dict(w=401, h=333, bands=3, type=3))
+    img = rand_img(rng, 333, 401, 3)
+    assert_same(gpu.execute(p, img)[0], oracle.execute(rp, img), f"fused={fused} window plan")
+
+
 @pytest.mark.parametrize("h,w,b,s", [(50, 60, 3, 1.6), (31, 45, 4, 2.0), (20, 33, 1, 3.3)])
 def test_reducev_reduceh_separately(gpu, oracle, rng, h, w, b, s):
     img = rand_img(rng, h, w, b)
