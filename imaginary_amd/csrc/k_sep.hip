@@ -607,7 +607,10 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     a.col_blocks = (a.row_bytes + 1023) / 1024;
     // rows per block: fill ~40 staged input rows (40 KiB of LDS)
-    constexpr int kRowBudget = 40, kRowMax = 60;
+    // staged input rows per block (LDS KiB); MIPX_VP_ROWS overrides for A/B runs
+    const char *erb = std::getenv("MIPX_VP_ROWS");
+    const int kRowBudget = (erb && *erb) ? std::max(8, std::atoi(erb)) : 24;  // A/B: profiles/r01/v12_vpass_ab.log
+    constexpr int kRowMax = 60;
     int kr = taps >= kRowBudget ? 1 : static_cast<int>(std::floor((kRowBudget - taps - 1) / s)) + 1;
     kr = std::max(1, std::min({kr, 32, a.oh}));
     a.kr = kr;
@@ -624,8 +627,14 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     const long long blocks = static_cast<long long>(a.col_blocks) * a.kr_blocks * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const uintptr_t ip = reinterpret_cast<uintptr_t>(in);
-    const bool al16 = (ip % 16) == 0 && (a.in_pitch % 16) == 0 && (a.in_base % 16) == 0 && (a.in_img % 16) == 0;
-    const bool al4 = (ip % 4) == 0 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0;
+    bool al16 = (ip % 16) == 0 && (a.in_pitch % 16) == 0 && (a.in_base % 16) == 0 && (a.in_img % 16) == 0;
+    bool al4 = (ip % 4) == 0 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0;
+    const char *edm = std::getenv("MIPX_VP_DMA");  // A/B: cap the DMA width (16 / 4 / 0)
+    if (edm && *edm) {
+        const int cap = std::atoi(edm);
+        al16 = al16 && cap >= 16;
+        al4 = al4 && cap >= 4;
+    }
     const dim3 grid(static_cast<unsigned>(blocks));
 #define MIPX_VP(MODE)                                                                                   \
     if (al16) hipLaunchKernelGGL((k_vpass<MODE, 16>), grid, blk, lds, st, a);                           \
