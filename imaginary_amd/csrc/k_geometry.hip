@@ -174,6 +174,117 @@ __global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
     }
 }
 
+// flip H / flip V / rot 180 as row remaps: output row Y = source row sy
+// (Y or h-1-Y), pixels mirrored for H / 180.  A block stages the source bytes
+// of its 4 KiB output segment in LDS with dword loads (aligned-down start),
+// then each lane gathers its 16 output bytes from LDS and stores them at once.
+template <int B, bool MIRROR>
+__global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
+                                                   int vflip, long long img_bytes_) {
+    __shared__ uint32_t seg[1024 + 8];
+    const int Y = blockIdx.y;
+    const int img = blockIdx.z;
+    const int row_bytes = w * B;
+    const int j0 = blockIdx.x * 4096;              // output byte range [j0, j1) of the row
+    const int j1 = min(j0 + 4096, row_bytes);
+    const int sy = vflip ? h - 1 - Y : Y;
+    // source bytes: pixels mirrored -> [s0, s1)
+    const int p0 = j0 / B, p1 = (j1 + B - 1) / B;  // output pixels touched
+    const int s0 = MIRROR ? (w - p1) * B : p0 * B;
+    const int s1 = MIRROR ? (w - p0) * B : p1 * B;
+    int delta = 0;
+    const u8 *src = in + img * img_bytes_;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, img_bytes_, &delta);
+    const int abs0 = delta + sy * row_bytes + s0;
+    const int a4 = abs0 & ~3, skew = abs0 - a4;
+    const int nd = (s1 - s0 + skew + 3) >> 2;
+    for (int d = threadIdx.x; d < nd; d += 256)
+        seg[d] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4 * d, 0, 0));
+    __syncthreads();
+    const u8 *sb = reinterpret_cast<const u8 *>(seg) + skew;
+    const int jl = j0 + threadIdx.x * 16;
+    if (jl >= j1) return;
+    const int nb = min(16, j1 - jl);
+    uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (k < nb) {
+            const int jb = jl + k;
+            const int px = jb / B, c = jb - px * B;
+            const int sbyte = MIRROR ? (w - 1 - px) * B + c - s0 : jb - s0;
+            v[k >> 2] |= static_cast<uint32_t>(sb[sbyte]) << (8 * (k & 3));
+        }
+    }
+    u8 *q = out + img * img_bytes_ + static_cast<long long>(Y) * row_bytes + jl;
+    if (nb == 16 && (reinterpret_cast<uintptr_t>(q) & 15u) == 0) {
+        *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
+    } else {
+        for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
+    }
+}
+
+// 90 / 270 via 64 x 64 pixel tiles: input tile rows staged in LDS with dword
+// loads, output rows gathered from LDS 16 bytes per lane.
+template <int B, bool CW>
+__global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
+                                                   long long img_bytes_) {
+    constexpr int T = 64;
+    constexpr int RS = (T * B + 8 + 3) / 4;  // dwords per staged row (skew + spill)
+    __shared__ uint32_t tile[T * RS];
+    __shared__ int skews[T];
+    const int img = blockIdx.z;
+    const int tx0 = blockIdx.x * T, ty0 = blockIdx.y * T;  // input tile origin
+    const int tw = min(T, w - tx0), th = min(T, h - ty0);
+    int delta = 0;
+    const u8 *src = in + img * img_bytes_;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, img_bytes_, &delta);
+    const int nd = (tw * B + 3 + 3) >> 2;
+    for (int i = threadIdx.x; i < th * nd; i += 256) {
+        const int r = i / nd, d = i - r * nd;
+        const int abs0 = delta + ((ty0 + r) * w + tx0) * B;
+        tile[r * RS + d] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, (abs0 & ~3) + 4 * d, 0, 0));
+        if (d == 0) skews[r] = abs0 & 3;
+    }
+    __syncthreads();
+    const u8 *t8 = reinterpret_cast<const u8 *>(tile);
+    // output tile: th columns wide (output x <- input y), tw rows tall
+    const int orow_bytes = th * B;
+    const int tasks_per_row = (orow_bytes + 15) / 16;
+    u8 *dst = out + img * img_bytes_;
+    for (int task = threadIdx.x; task < tw * tasks_per_row; task += 256) {
+        const int orr = task / tasks_per_row, q16 = task - orr * tasks_per_row;
+        // output row within the tile -> input column; output columns -> input rows
+        const int icol = CW ? orr : tw - 1 - orr;
+        int ox, oy;
+        if (CW) {  // out(x, y) = in(y, h-1-x): output row oy = input col, output col ox = h-1-input row
+            oy = tx0 + icol;
+            ox = h - (ty0 + th);  // output column of the tile's first byte (input row ty0 + th - 1)
+        } else {   // out(x, y) = in(w-1-y, x): output row oy = w-1-input col, output col ox = input row
+            oy = w - 1 - (tx0 + icol);
+            ox = ty0;
+        }
+        const int jb0 = q16 * 16;
+        const int nb = min(16, orow_bytes - jb0);
+        uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k < nb) {
+                const int jb = jb0 + k;
+                const int px = jb / B, c = jb - px * B;
+                const int ir = CW ? th - 1 - px : px;  // input row within the tile
+                v[k >> 2] |= static_cast<uint32_t>(t8[ir * RS * 4 + skews[ir] + icol * B + c]) << (8 * (k & 3));
+            }
+        }
+        u8 *q = dst + (static_cast<long long>(oy) * h + ox) * B + jb0;
+        if (nb == 16 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+            uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
+            q32[0] = v[0], q32[1] = v[1], q32[2] = v[2], q32[3] = v[3];
+        } else {
+            for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+
 // 90 (CW) / 270 rotation: out(x, y) = in(y, H-1-x) for CW, in(W-1-y, x) for CCW.
 // A block moves one 32 x 32 input tile; rows of the tile are read and rows of
 // the transposed tile written, each coalesced.
@@ -290,7 +401,24 @@ int embed_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x, int y
     return remap_launch(kEmbed, a, b, n, st);
 }
 
+int flip_rows_launch(const u8 *in, u8 *out, int n, int w, int h, int b, bool mirror, bool vflip, hipStream_t st) {
+    if (h > 65535) return MIPX_EUNSUPPORTED;
+    const long long ib = img_bytes(w, h, b);
+    if (ib >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
+    const dim3 grid((w * b + 4095) / 4096, h, n);
+    if (mirror) {
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_flip_rows<B_, true>), grid, dim3(256), 0, st, in, out, w, h,
+                                                  vflip ? 1 : 0, ib));
+    } else {
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_flip_rows<B_, false>), grid, dim3(256), 0, st, in, out, w, h,
+                                                  vflip ? 1 : 0, ib));
+    }
+    return launch_check("k_flip_rows");
+}
+
 int flip_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int vertical, hipStream_t st) {
+    if (img_bytes(w, h, b) < 0x7fffffffLL && h <= 65535)
+        return flip_rows_launch(in, out, n, w, h, b, !vertical, vertical != 0, st);
     RemapArgs a{};
     a.in = in;
     a.out = out;
@@ -310,6 +438,18 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
     if (angle == 0) {
         MIPX_HIP(hipMemcpyAsync(out, in, static_cast<size_t>(img_bytes(w, h, b)) * n, hipMemcpyDeviceToDevice, st));
         return MIPX_OK;
+    }
+    if (angle == 180 && img_bytes(w, h, b) < 0x7fffffffLL && h <= 65535)
+        return flip_rows_launch(in, out, n, w, h, b, true, true, st);
+    if ((angle == 90 || angle == 270) && img_bytes(w, h, b) < 0x7fffffffLL) {
+        const dim3 grid((w + 63) / 64, (h + 63) / 64, n);
+        const long long ib = img_bytes(w, h, b);
+        if (angle == 90) {
+            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, true>), grid, dim3(256), 0, st, in, out, w, h, ib));
+        } else {
+            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, false>), grid, dim3(256), 0, st, in, out, w, h, ib));
+        }
+        return launch_check("k_rot90_lds");
     }
     if (angle == 180) {
         RemapArgs a{};
