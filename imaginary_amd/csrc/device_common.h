@@ -80,6 +80,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc_aligned(const u8 *p
                                              static_cast<int>((bytes + *delta + 3) & ~3LL), 0x00020000);
 }
 
+// Individually rounded float ops for the kernels that restate libvips' float
+// order of operations.  The HIP headers define __fmul_rn & co. as plain operators,
+// which the backend may still fuse into FMAs; the pragma inside each body marks
+// these operations non-contractable, so they stay separately rounded after inlining.
+#define MIPX_RN_OP(name, T, op)                                   \
+    __device__ __forceinline__ T name(T a, T b) {                 \
+        _Pragma("clang fp contract(off)") return a op b;          \
+    }
+MIPX_RN_OP(fmul_rn, float, *)
+MIPX_RN_OP(fadd_rn, float, +)
+MIPX_RN_OP(fsub_rn, float, -)
+MIPX_RN_OP(fdiv_rn, float, /)
+MIPX_RN_OP(dmul_rn, double, *)
+MIPX_RN_OP(dadd_rn, double, +)
+#undef MIPX_RN_OP
+
 }  // namespace dev
 
 // ---- host-side helpers shared by the launchers ----

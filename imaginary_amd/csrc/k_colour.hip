@@ -43,12 +43,12 @@ __global__ void __launch_bounds__(256) k_bw(const u8 *__restrict__ in, u8 *__res
     constexpr int OB = B == 4 ? 2 : 1;
     const u8 *p = in + i * B;
     const float R = sv2y[p[0]], G = sv2y[p[1]], Bl = sv2y[p[2]];
-    const double yd = __dadd_rn(__dadd_rn(__dmul_rn(0.2126, R), __dmul_rn(0.7152, G)), __dmul_rn(0.0722, Bl));
+    const double yd = dadd_rn(dadd_rn(dmul_rn(0.2126, R), dmul_rn(0.7152, G)), dmul_rn(0.0722, Bl));
     const float Y = static_cast<float>(yd);
-    const float Yf = __fmul_rn(Y, 255.0f);
+    const float Yf = fmul_rn(Y, 255.0f);
     const int k = clampi(static_cast<int>(Yf), 0, 255);
-    const float f = __fsub_rn(Yf, static_cast<float>(k));
-    const float v = __fadd_rn(sy2v[k], __fmul_rn(f, __fsub_rn(sy2v[k + 1], sy2v[k])));
+    const float f = fsub_rn(Yf, static_cast<float>(k));
+    const float v = fadd_rn(sy2v[k], fmul_rn(f, fsub_rn(sy2v[k + 1], sy2v[k])));
     u8 *q = out + i * OB;
     q[0] = static_cast<u8>(clampi(static_cast<int>(rintf(v)), 0, 255));
     if (OB == 2) q[1] = p[3];

@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(256) k_watermark(const u8 *__restrict__ base, 
         const u8 *s = wm + (static_cast<size_t>(wy) * ww + wx) * WB;
 #pragma unroll
         for (int z = 0; z < BO; ++z) av[z] = z < WB ? s[z] : 255;
-        const float f = __fadd_rn(__fmul_rn(static_cast<float>(av[BO - 1]), opacity), 0.0f);
+        const float f = fadd_rn(fmul_rn(static_cast<float>(av[BO - 1]), opacity), 0.0f);
         m = f < 0.f ? 0 : (f > 255.f ? 255 : static_cast<int>(f));
     } else {
 #pragma unroll

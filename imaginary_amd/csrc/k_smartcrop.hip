@@ -47,10 +47,10 @@ struct ScoreArgs {
 };
 
 __device__ __forceinline__ float lab_cbrt(const float *tab, float v, double white) {
-    const float nq = static_cast<float>(static_cast<double>(__fmul_rn(100000.0f, v)) / white);
+    const float nq = static_cast<float>(static_cast<double>(fmul_rn(100000.0f, v)) / white);
     const int i = clampi(static_cast<int>(nq), 0, kQuantElements - 2);
-    const float f = __fsub_rn(nq, static_cast<float>(i));
-    return __fadd_rn(tab[i], __fmul_rn(f, __fsub_rn(tab[i + 1], tab[i])));
+    const float f = fsub_rn(nq, static_cast<float>(i));
+    return fadd_rn(tab[i], fmul_rn(f, fsub_rn(tab[i + 1], tab[i])));
 }
 
 __global__ void __launch_bounds__(256) k_smartcrop_score(ScoreArgs a) {
@@ -66,42 +66,42 @@ __global__ void __launch_bounds__(256) k_smartcrop_score(ScoreArgs a) {
     // pass 1: Y into sY, skin into sA, sat into sB
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
         const u8 *p = src + static_cast<size_t>(i) * a.bands;
-        const float R = __fmul_rn(a.v2y[p[0]], 100.0f);
-        const float G = __fmul_rn(a.v2y[p[1]], 100.0f);
-        const float Bc = __fmul_rn(a.v2y[p[2]], 100.0f);
-        const float X = static_cast<float>(__dadd_rn(__dadd_rn(__dmul_rn(0.4124, R), __dmul_rn(0.3576, G)), __dmul_rn(0.1805, Bc)));
-        const float Y = static_cast<float>(__dadd_rn(__dadd_rn(__dmul_rn(0.2126, R), __dmul_rn(0.7152, G)), __dmul_rn(0.0722, Bc)));
-        const float Z = static_cast<float>(__dadd_rn(__dadd_rn(__dmul_rn(0.0193, R), __dmul_rn(0.1192, G)), __dmul_rn(0.9505, Bc)));
+        const float R = fmul_rn(a.v2y[p[0]], 100.0f);
+        const float G = fmul_rn(a.v2y[p[1]], 100.0f);
+        const float Bc = fmul_rn(a.v2y[p[2]], 100.0f);
+        const float X = static_cast<float>(dadd_rn(dadd_rn(dmul_rn(0.4124, R), dmul_rn(0.3576, G)), dmul_rn(0.1805, Bc)));
+        const float Y = static_cast<float>(dadd_rn(dadd_rn(dmul_rn(0.2126, R), dmul_rn(0.7152, G)), dmul_rn(0.0722, Bc)));
+        const float Z = static_cast<float>(dadd_rn(dadd_rn(dmul_rn(0.0193, R), dmul_rn(0.1192, G)), dmul_rn(0.9505, Bc)));
         sY[i] = Y;
-        float sq = __fmul_rn(X, X);
-        sq = __fadd_rn(sq, __fmul_rn(Y, Y));
-        sq = __fadd_rn(sq, __fmul_rn(Z, Z));
+        float sq = fmul_rn(X, X);
+        sq = fadd_rn(sq, fmul_rn(Y, Y));
+        sq = fadd_rn(sq, fmul_rn(Z, Z));
         const float mag = static_cast<float>(sqrt(static_cast<double>(sq)));
-        const float nx = mag == 0.0f ? 0.0f : __fdiv_rn(X, mag);
-        const float ny = mag == 0.0f ? 0.0f : __fdiv_rn(Y, mag);
-        const float nz = mag == 0.0f ? 0.0f : __fdiv_rn(Z, mag);
-        const float dx = __fadd_rn(nx, -0.78f), dy = __fadd_rn(ny, -0.57f), dz = __fadd_rn(nz, -0.44f);
-        float d2 = __fmul_rn(dx, dx);
-        d2 = __fadd_rn(d2, __fmul_rn(dy, dy));
-        d2 = __fadd_rn(d2, __fmul_rn(dz, dz));
+        const float nx = mag == 0.0f ? 0.0f : fdiv_rn(X, mag);
+        const float ny = mag == 0.0f ? 0.0f : fdiv_rn(Y, mag);
+        const float nz = mag == 0.0f ? 0.0f : fdiv_rn(Z, mag);
+        const float dx = fadd_rn(nx, -0.78f), dy = fadd_rn(ny, -0.57f), dz = fadd_rn(nz, -0.44f);
+        float d2 = fmul_rn(dx, dx);
+        d2 = fadd_rn(d2, fmul_rn(dy, dy));
+        d2 = fadd_rn(d2, fmul_rn(dz, dz));
         const float dist = static_cast<float>(sqrt(static_cast<double>(d2)));
         const bool bright = static_cast<double>(Y) > 5.0;
-        sA[i] = bright ? __fadd_rn(__fmul_rn(-100.0f, dist), 100.0f) : 0.0f;
+        sA[i] = bright ? fadd_rn(fmul_rn(-100.0f, dist), 100.0f) : 0.0f;
         const float cbx = lab_cbrt(a.cbrt, X, 95.047), cby = lab_cbrt(a.cbrt, Y, 100.0);
-        sB[i] = bright ? static_cast<float>(500.0 * static_cast<double>(__fsub_rn(cbx, cby))) : 0.0f;
+        sB[i] = bright ? static_cast<float>(500.0 * static_cast<double>(fsub_rn(cbx, cby))) : 0.0f;
     }
     __syncthreads();
     // pass 2: score = (edge + skin) + sat into sC
     for (int i = threadIdx.x; i < N; i += blockDim.x) {
         const int y = i / W, x = i - y * W;
         double acc = 0.0;
-        acc = __dadd_rn(acc, -1.0 * sY[clampi(y - 1, 0, H - 1) * W + x]);
-        acc = __dadd_rn(acc, -1.0 * sY[y * W + clampi(x - 1, 0, W - 1)]);
-        acc = __dadd_rn(acc, 4.0 * sY[i]);
-        acc = __dadd_rn(acc, -1.0 * sY[y * W + clampi(x + 1, 0, W - 1)]);
-        acc = __dadd_rn(acc, -1.0 * sY[clampi(y + 1, 0, H - 1) * W + x]);
-        const float edge = fabsf(__fadd_rn(__fmul_rn(5.0f, static_cast<float>(acc / 1.0 + 0.0)), 0.0f));
-        sC[i] = __fadd_rn(__fadd_rn(edge, sA[i]), sB[i]);
+        acc = dadd_rn(acc, -1.0 * sY[clampi(y - 1, 0, H - 1) * W + x]);
+        acc = dadd_rn(acc, -1.0 * sY[y * W + clampi(x - 1, 0, W - 1)]);
+        acc = dadd_rn(acc, 4.0 * sY[i]);
+        acc = dadd_rn(acc, -1.0 * sY[y * W + clampi(x + 1, 0, W - 1)]);
+        acc = dadd_rn(acc, -1.0 * sY[clampi(y + 1, 0, H - 1) * W + x]);
+        const float edge = fabsf(fadd_rn(fmul_rn(5.0f, static_cast<float>(acc / 1.0 + 0.0)), 0.0f));
+        sC[i] = fadd_rn(fadd_rn(edge, sA[i]), sB[i]);
     }
     __syncthreads();
     // pass 3: horizontal blur sC -> sB, vertical blur sB -> argmax
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(256) k_smartcrop_score(ScoreArgs a) {
         const int y = i / W, x = i - y * W;
         double s = 0.0;
         for (int t = 0; t < a.n_mask; ++t)
-            s = __dadd_rn(s, static_cast<double>(a.mask[t]) * sC[y * W + clampi(x + t - half, 0, W - 1)]);
+            s = dadd_rn(s, static_cast<double>(a.mask[t]) * sC[y * W + clampi(x + t - half, 0, W - 1)]);
         sB[i] = static_cast<float>(s / a.mask_scale + 0.0);
     }
     __syncthreads();
@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(256) k_smartcrop_score(ScoreArgs a) {
         const int y = i / W, x = i - y * W;
         double s = 0.0;
         for (int t = 0; t < a.n_mask; ++t)
-            s = __dadd_rn(s, static_cast<double>(a.mask[t]) * sB[clampi(y + t - half, 0, H - 1) * W + x]);
+            s = dadd_rn(s, static_cast<double>(a.mask[t]) * sB[clampi(y + t - half, 0, H - 1) * W + x]);
         const float v = static_cast<float>(s / a.mask_scale + 0.0);
         if (v > best) { best = v; bidx = i; }  // i ascends per thread: first max kept
     }

@@ -70,3 +70,33 @@ def test_product_does_not_import_oracle():
                 assert not bad.search(open(os.path.join(dirpath, f)).read()), f
     out = subprocess.run(["nm", "-D", os.path.join(pkg, "libmipx.so")], capture_output=True, text=True).stdout
     assert "ref_" not in out and "liboracle" not in out
+
+
+def test_entry_points_reject_bad_arguments_without_touching_the_device():
+    """Every mipx_op_* validates its arguments before any HIP call: NULL pointers,
+    empty or oversized batches and bad geometry return MIPX_EINVAL (-1)."""
+    import imaginary_amd as ia
+    L = ia.lib
+    EINVAL = -1
+    assert L.mipx_op_reduce(None, None, 1, 8, 8, 3, 2.0, 2.0, None, 0, None) == EINVAL
+    assert L.mipx_op_reduce(1, 1, 0, 8, 8, 3, 2.0, 2.0, None, 0, None) == EINVAL
+    assert L.mipx_op_reduce(1, 1, 1, 8, 8, 5, 2.0, 2.0, None, 0, None) == EINVAL
+    assert L.mipx_op_reduce(1, 1, 1, 8, 8, 3, 0.5, 2.0, None, 0, None) == EINVAL
+    assert L.mipx_op_shrink(1, 1, 1, 8, 8, 3, 0, 2, None) == EINVAL
+    assert L.mipx_op_extract(1, 1, 1, 8, 8, 3, 4, 4, 8, 8, None) == EINVAL
+    assert L.mipx_op_embed(1, 1, 1, 8, 8, 3, 0, 0, 0, 8, 1, None, None) == EINVAL
+    assert L.mipx_op_affine(1, 1, 1, 8, 8, 3, 0.0, 2.0, 1, None) == EINVAL
+    assert L.mipx_op_zoom(1, 1, 1, 8, 8, 3, 0, 2, None) == EINVAL
+    assert L.mipx_op_watermark(1, 1, 1, 1, 8, 8, 3, 0, 4, 4, 0, 0, 1.0, None) == EINVAL
+    assert L.mipx_op_gaussblur(None, 1, 1, 8, 8, 3, 2.0, 0.2, None, 0, None) == EINVAL
+    assert L.mipx_op_flatten(None, 1, 1, 8, 8, 4, None, None) == EINVAL
+    assert L.mipx_op_colourspace_bw(1, None, 1, 8, 8, 3, None) == EINVAL
+    assert L.mipx_execute_dev(None, 1, 1, 1, None, None, 0, None) == EINVAL
+
+
+def test_request_api_before_init():
+    import ctypes as C
+    import imaginary_amd as ia
+    t = C.c_uint64()
+    assert ia.lib.mipx_wait(12345, 0) == -8           # unknown ticket
+    assert ia.lib.mipx_stats(0, C.byref(t), C.byref(t)) in (-7, -1, 0)

@@ -219,12 +219,13 @@ def test_zoom_flatten_bw_match_oracle(gpu, oracle, rng, b):
         assert_same(got[i], oracle.bw(imgs[i]), "bw")
 
 
-def test_bw_every_grey_level(gpu, oracle):
-    """All 256^3 / 4096 sampled colours through B_W: the float LUT pipeline is exact."""
-    v = np.arange(0, 256, 5, dtype=np.uint8)
-    rgb = np.stack(np.meshgrid(v, v, v, indexing="ij"), -1).reshape(-1, 3)
-    img = rgb.reshape(1, -1, 3)
-    assert_same(gpu.run_op("bw", img)[0], oracle.bw(img), "bw grid")
+def test_bw_every_colour(gpu, oracle):
+    """Every one of the 2^24 sRGB colours through B_W (as a 4096 x 4096 image).
+    The float LUT pipeline has exact .5 ties (e.g. RGB (206, 28, 113) -> 108.5 ->
+    108), so one fused multiply-add anywhere in it shows up here."""
+    v = np.arange(1 << 24, dtype=np.uint32)
+    img = np.stack([(v >> 16) & 255, (v >> 8) & 255, v & 255], -1).astype(np.uint8).reshape(4096, 4096, 3)
+    assert_same(gpu.run_op("bw", img)[0], oracle.bw(img), "bw all colours")
 
 
 # ---------------------------------------------------------------- watermark composite
