@@ -35,8 +35,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU (BASELINE C2: 256)")
     ap.add_argument("--cpu-images", type=int, default=96, help="CPU baseline sample size (images)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")

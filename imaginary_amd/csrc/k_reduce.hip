@@ -49,19 +49,19 @@ using namespace dev;
 // workgroup, so occupancy is set by registers, not LDS.
 // ===========================================================================
 constexpr int kR = 12;           // output rows per LDS chunk (2 ring periods)
-// WIDE (variant bit 6): 256 threads and strips twice as wide (half the
-// relative halo, 480-byte output row segments, half the workgroups)
-template <bool WIDE>
+// WIDE level (variant bits 6 / 7): 128 << WIDE threads and strips 2x / 4x as
+// wide (less relative halo, longer contiguous row segments, fewer workgroups)
+template <int WIDE>
 struct R2T {
-    static constexpr int kThreads = WIDE ? 256 : 128;
-    static constexpr int kPitch = WIDE ? 288 : 160;  // LDS dwords per intermediate row (== 32 mod 64)
+    static constexpr int kThreads = 128 << WIDE;
+    static constexpr int kPitch = WIDE == 2 ? 544 : WIDE == 1 ? 288 : 160;  // LDS dwords per row (== 32 mod 64)
 };
 
-template <int B, bool WIDE = false>
+template <int B, int WIDE = 0>
 struct R2 {
     static constexpr int kThreads = R2T<WIDE>::kThreads;
     static constexpr int kPitch = R2T<WIDE>::kPitch;
-    static constexpr int TW = WIDE ? (B == 3 ? 160 : 120) : (B == 3 ? 80 : 56);  // output pixels per strip
+    static constexpr int TW = B == 3 ? 80 << WIDE : WIDE == 0 ? 56 : 60 << WIDE;  // output pixels per strip
     static constexpr int NPX = 2 * TW + 9;           // intermediate px 2x0-5 .. 2x0+2TW+3
     static constexpr int K = B == 3 ? 4 : 2;         // output pixels per horizontal item
     static constexpr int OFF0 = B == 3 ? 1 : 0;      // B*(2x0-5) - floor4(B*(2x0-5))
@@ -121,7 +121,7 @@ __device__ __forceinline__ uint32_t pack4b(float a, float b, float c, float d) {
     return __builtin_amdgcn_cvt_pk_u8_f32(d, 3, v);
 }
 
-template <int B, int R, bool PF, bool PK, bool MEM, int LAUX, bool NTS, bool WIDE>
+template <int B, int R, bool PF, bool PK, bool MEM, int LAUX, bool NTS, int WIDE>
 __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int strip, int band,
                                              uint32_t *lds) {
     using G = R2<B, WIDE>;
@@ -330,12 +330,13 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 // bit 0: R = 6 (else 12), bit 1: register prefetch of the next chunk,
 // bit 2: packed-FP32 vertical taps, bit 3: memory-only diagnostic (not exact),
 // bit 4: non-temporal loads, bit 5: non-temporal stores, bit 6: 256-thread
-// workgroups over strips twice as wide.  Measured in
+// workgroups over strips twice as wide, bit 7: 512-thread workgroups over
+// strips four times as wide.  Measured in
 // profiles/r01/v7_variants_ab.log: the memory-only build is no faster than the
 // full one (the arithmetic is hidden), packed math and nt hints lose.
 template <int B, int VAR>
-__global__ void __launch_bounds__(R2T<(VAR & 64) != 0>::kThreads) k_reduce2x2(Reduce2Args a) {
-    constexpr bool WIDE = (VAR & 64) != 0;
+__global__ void __launch_bounds__(R2T<(VAR & 128) ? 2 : (VAR & 64) ? 1 : 0>::kThreads) k_reduce2x2(Reduce2Args a) {
+    constexpr int WIDE = (VAR & 128) ? 2 : (VAR & 64) ? 1 : 0;
     constexpr int kPitch = R2T<WIDE>::kPitch;
     constexpr int R = (VAR & 1) ? 6 : 12;
     constexpr bool PF = (VAR & 2) != 0;
@@ -471,7 +472,7 @@ int reduce2_variant() {
     if (!e || !*e) return kR2Default;
     const int v = std::atoi(e);
     switch (v) {
-        case 0: case 1: case 2: case 3: case 6: case 10: case 66: case 67: return v;
+        case 0: case 1: case 2: case 3: case 6: case 10: case 66: case 67: case 130: case 131: return v;
         default: return kR2Default;
     }
 }
@@ -487,8 +488,9 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     a.ow = out_size_reduce(w, 2.0);
     a.oh = out_size_reduce(h, 2.0);
     const int var = reduce2_variant();
-    const bool wide = (var & 64) != 0;
-    const int tw = b == 3 ? (wide ? R2<3, true>::TW : R2<3>::TW) : (wide ? R2<4, true>::TW : R2<4>::TW);
+    const int wl = (var & 128) ? 2 : (var & 64) ? 1 : 0;
+    const int tw = b == 3 ? (wl == 2 ? R2<3, 2>::TW : wl == 1 ? R2<3, 1>::TW : R2<3>::TW)
+                          : (wl == 2 ? R2<4, 2>::TW : wl == 1 ? R2<4, 1>::TW : R2<4>::TW);
     a.n_strips = (a.ow + tw - 1) / tw;
     const int chunks = (a.oh + kR - 1) / kR;
     // rows per workgroup: 2 chunks of 12 (measured best, profiles/r01/geom_ab.log; MIPX_R2_BAND overrides)
@@ -513,13 +515,13 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     dim3 grid(static_cast<unsigned>(tiles));
 #define MIPX_R2(V)                                                                                      \
     case V: {                                                                                           \
-        const dim3 blk(R2T<(V & 64) != 0>::kThreads);                                                   \
+        const dim3 blk(R2T<(V & 128) ? 2 : (V & 64) ? 1 : 0>::kThreads);                                                   \
         if (b == 3) hipLaunchKernelGGL((k_reduce2x2<3, V>), grid, blk, 0, st, a);                       \
         else hipLaunchKernelGGL((k_reduce2x2<4, V>), grid, blk, 0, st, a);                              \
         break;                                                                                          \
     }
     switch (var) {
-        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3) MIPX_R2(6) MIPX_R2(10) MIPX_R2(66) MIPX_R2(67)
+        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3) MIPX_R2(6) MIPX_R2(10) MIPX_R2(66) MIPX_R2(67) MIPX_R2(130) MIPX_R2(131)
         default: return MIPX_EINVAL;
     }
 #undef MIPX_R2

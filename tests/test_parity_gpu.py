@@ -70,7 +70,7 @@ def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
 
 
-@pytest.mark.parametrize("var", [0, 1, 2, 3, 6, 66, 67])
+@pytest.mark.parametrize("var", [0, 1, 2, 3, 6, 66, 67, 130, 131])
 def test_reduce2x2_variants_exact(gpu, oracle, rng, var, monkeypatch):
     """Every A/B build of the fused 2x2 kernel (MIPX_R2_VARIANT, read per launch)
     is bit-exact, including strips that end at the image edge."""
