@@ -98,28 +98,31 @@ def line(name, workload, images, wall_s, dev_ms, alg_bytes, verified, extra=None
 
 
 def c3(args, dev, sp, stream):
+    """/pipeline fused on the device (mipx_plan_chain): the three stage plans run
+    as one plan, PNG intermediates lossless and resident in HBM."""
+    from oracle import oracle as o
     n = args.c3_batch
-    stages = [("resize", dict(width=1024, embed=1)), ("crop", dict(width=768, height=512, crop=1)),
-              ("blur", dict(sigma=5.0))]
-    groups, w, h = [], 2048, 2048
-    for i, (name, opts) in enumerate(stages):
-        p = plan_for(opts, w, h, 4)
-        groups.append((Group(p, n, dev, 3 + i), opts))
-        w, h = p.out_w, p.out_h
+    stages = [dict(width=1024, embed=1), dict(width=768, height=512, crop=1), dict(sigma=5.0)]
+    plans, w, h = [], 2048, 2048
+    for opts in stages:
+        plans.append(plan_for(opts, w, h, 4))
+        w, h = plans[-1].out_w, plans[-1].out_h
+    g = Group(ia.plan_chain(plans), n, dev, 3)
 
-    def run_all():  # PNG intermediates are lossless: stages chain on the device
-        for gi, (g, _) in enumerate(groups):
-            if gi > 0:
-                g.x = groups[gi - 1][0].y
-            g.run(sp)
+    def run_all():
+        g.run(sp)
 
     run_all()
     torch.cuda.synchronize()
-    ok = all(verify(g, opts) for g, opts in groups)
+    px = g.x[0].cpu().numpy().reshape(2048, 2048, 4)
+    for opts, p in zip(stages, plans):  # the oracle runs the stages one by one
+        e, rp = o.plan(opts, dict(w=p.in_w, h=p.in_h, bands=p.in_bands, type=3))
+        assert e == 0
+        px = o.execute(rp, px)
+    ok = bool(np.array_equal(g.y[0].cpu().numpy().reshape(px.shape), px))
     wall, dev_ms = time_groups(run_all, args.steps, args.warmup, stream)
-    alg = groups[0][0].in_bytes + groups[-1][0].out_bytes
-    line("C3", "pipeline resize(w=1024)+crop(768x512)+blur(sigma=5), 2048^2 RGBA", n, wall, dev_ms, alg, ok,
-         {"batch": n, "stages": [g.plan.describe() for g, _ in groups]})
+    line("C3", "pipeline resize(w=1024)+crop(768x512)+blur(sigma=5), 2048^2 RGBA", n, wall, dev_ms,
+         g.in_bytes + g.out_bytes, ok, {"batch": n, "fused_plan": g.plan.describe()})
 
 
 def c4(args, dev, sp, stream):

@@ -6,6 +6,6 @@ Importing it fails when libmipx.so has not been built: there is no CPU path.
 """
 from ._abi import lib, MipxError, MipxPlan, MipxOpts, MipxInput, LIB_PATH, TYPES, EXTEND, GRAVITY  # noqa: F401
 from .engine import (DeviceBuffer, Engine, device_count, execute, fit_dimension, make_input,  # noqa: F401
-                     make_opts, plan_make, run_op, smartcrop_origins, synchronize)
+                     make_opts, plan_chain, plan_make, run_op, smartcrop_origins, synchronize)
 
 __version__ = "0.1.0"

@@ -34,7 +34,7 @@ OP_NAMES = {OP_ROT: "rot", OP_FLIP: "flip", OP_SHRINK: "shrink", OP_REDUCE: "red
             OP_FLATTEN: "flatten", OP_BW: "bw"}
 INTERPRETATION_SRGB = 22
 INTERPRETATION_BW = 26
-MAX_STEPS = 16
+MAX_STEPS = 64
 
 
 class MipxOpts(C.Structure):
@@ -109,6 +109,7 @@ _I = C.c_int32
 _SIG = {
     "mipx_version": (C.c_char_p, []),
     "mipx_abi_version": (C.c_int, []),
+    "mipx_plan_chain": (C.c_int, [C.POINTER(MipxPlan), C.c_int32, C.POINTER(MipxPlan)]),
     "mipx_strerror": (C.c_char_p, [C.c_int]),
     "mipx_last_error": (C.c_char_p, []),
     "mipx_init": (C.c_int, [C.POINTER(MipxCfg)]),

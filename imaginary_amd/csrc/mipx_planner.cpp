@@ -518,3 +518,41 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
     plan->out_bands = pb.b();
     return MIPX_OK;
 }
+
+extern "C" int mipx_plan_chain(const mipx_plan *stages, int32_t n_stages, mipx_plan *out) {
+    if (!stages || !out || n_stages <= 0) return MIPX_EINVAL;
+    mipx_plan m{};
+    m.load_shrink = stages[0].load_shrink;
+    m.in_w = stages[0].in_w;
+    m.in_h = stages[0].in_h;
+    m.in_bands = stages[0].in_bands;
+    int wm_stages = 0;
+    for (int k = 0; k < n_stages; ++k) {
+        const mipx_plan &s = stages[k];
+        if (s.n_steps < 0 || s.n_steps > MIPX_MAX_STEPS) return MIPX_EINVAL;
+        if (k > 0 && (s.load_shrink != 1 || s.in_w != stages[k - 1].out_w || s.in_h != stages[k - 1].out_h ||
+                      s.in_bands != stages[k - 1].out_bands)) {
+            mipx::set_error("mipx_plan_chain: stage %d takes %dx%dx%d (load_shrink %d), stage %d gives %dx%dx%d", k,
+                            s.in_w, s.in_h, s.in_bands, s.load_shrink, k - 1, stages[k - 1].out_w,
+                            stages[k - 1].out_h, stages[k - 1].out_bands);
+            return MIPX_EINVAL;
+        }
+        bool wm = false;
+        for (int i = 0; i < s.n_steps; ++i) wm |= s.steps[i].op == MIPX_OP_WATERMARK;
+        wm_stages += wm;
+        if (wm_stages > 1) {
+            mipx::set_error("mipx_plan_chain: more than one watermark stage");
+            return MIPX_EUNSUPPORTED;
+        }
+        if (m.n_steps + s.n_steps > MIPX_MAX_STEPS) {
+            mipx::set_error("mipx_plan_chain: %d steps exceed MIPX_MAX_STEPS", m.n_steps + s.n_steps);
+            return MIPX_EUNSUPPORTED;
+        }
+        for (int i = 0; i < s.n_steps; ++i) m.steps[m.n_steps++] = s.steps[i];
+    }
+    m.out_w = stages[n_stages - 1].out_w;
+    m.out_h = stages[n_stages - 1].out_h;
+    m.out_bands = stages[n_stages - 1].out_bands;
+    *out = m;
+    return MIPX_OK;
+}

@@ -90,6 +90,14 @@ def plan_make(opts: MipxOpts, inp: MipxInput) -> MipxPlan:
     return p
 
 
+def plan_chain(stages) -> MipxPlan:
+    """mipx_plan_chain: one plan for a /pipeline chain of stage plans."""
+    arr = (MipxPlan * len(stages))(*stages)
+    p = MipxPlan()
+    check(lib.mipx_plan_chain(arr, len(stages), C.byref(p)), "mipx_plan_chain")
+    return p
+
+
 def fit_dimension(iw, ih, fw, fh):
     a, b = C.c_int32(), C.c_int32()
     check(lib.mipx_fit_dimension(iw, ih, fw, fh, C.byref(a), C.byref(b)), "mipx_fit_dimension")

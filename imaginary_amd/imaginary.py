@@ -26,7 +26,7 @@ from typing import Any, Callable, Dict, List, Optional
 import numpy as np
 
 from . import _abi, codec
-from .engine import Engine, fit_dimension, make_input, make_opts, plan_make
+from .engine import Engine, fit_dimension, make_input, make_opts, plan_chain, plan_make
 
 HTTP_BAD_REQUEST = 400
 HTTP_NOT_ACCEPTABLE = 406
@@ -252,13 +252,30 @@ class Image:
 _ENCODE_ONLY = ("type", "quality", "compression")
 
 
-def process(img, opts: Dict[str, Any], wm=None, redecode: Optional[Decoder] = None):
+def _placeholder(h: int, w: int, b: int) -> np.ndarray:
+    """Stand-in pixels of a planned-but-not-run stage: only the shape is read."""
+    return np.lib.stride_tricks.as_strided(np.zeros(1, np.uint8), (h, w, b), (0, 0, 0), writeable=False)
+
+
+def _run(plan, px, wm):
+    try:
+        return engine().process(plan, px, wm)
+    except _abi.MipxError as e:
+        if e.code == _abi.MIPX_EUNSUPPORTED:
+            raise EngineUnsupported(str(e)) from e
+        raise ImaginaryError(f"image processing error: {e}", 500) from e
+
+
+def process(img, opts: Dict[str, Any], wm=None, redecode: Optional[Decoder] = None, chain: Optional[list] = None):
     """image.go:81-113 Process with bimg.Resize's pixel work on the GPU.
 
     Encoded bytes in -> Image out (the drop-in: host codec, engine, host codec);
     a Decoded in -> pixels out (the engine alone, for callers that own the codec).
     `redecode(img, s)` is the host codec's shrink-on-load (libjpeg scale 1/s);
-    without one, a plan that asks for load_shrink > 1 is rejected."""
+    without one, a plan that asks for load_shrink > 1 is rejected.
+    With `chain` (a list), a Decoded input is planned but not run: (plan, pixels,
+    watermark) is appended and placeholder pixels of the output shape returned
+    (Pipeline fuses the stages into one device-resident plan)."""
     if isinstance(img, (bytes, bytearray, memoryview)):
         return process_bytes(bytes(img), opts, wm)
     opts = {k: v for k, v in opts.items() if k not in _ENCODE_ONLY}
@@ -278,6 +295,9 @@ def process(img, opts: Dict[str, Any], wm=None, redecode: Optional[Decoder] = No
             plan = plan_make(make_opts(**opts), inp)
         elif img.header_w and (img.header_w, img.header_h) != (px.shape[1], px.shape[0]):
             raise ImaginaryError("decoded size does not match the header", 500)
+        if chain is not None:
+            chain.append((plan, px, wm))
+            return _placeholder(plan.out_h, plan.out_w, plan.out_bands)
         return engine().process(plan, px, wm)
     except _abi.MipxError as e:
         if e.code == _abi.MIPX_EUNSUPPORTED:
@@ -497,6 +517,11 @@ OperationsMap: Dict[str, Callable] = {
 }
 
 
+def _stage_kw(fn, kw):
+    """The caller's watermark pixels belong to watermarkImage stages only."""
+    return kw if fn is WatermarkImage else {k: v for k, v in kw.items() if k != "wm"}
+
+
 def Pipeline(img, o: ImageOptions, **kw):
     """image.go:379-410.  On encoded bytes every stage decodes and re-encodes in
     the stage's output format, exactly as the reference; on a Decoded input the
@@ -513,7 +538,7 @@ def Pipeline(img, o: ImageOptions, **kw):
             if fn is None:
                 raise ImaginaryError(f"Unsupported operation: {name}")
             try:
-                out = fn(out.body, build_params_from_query(op.get("params", {})), **kw)
+                out = fn(out.body, build_params_from_query(op.get("params", {})), **_stage_kw(fn, kw))
             except ImaginaryError:
                 if not op.get("ignore_failure"):
                     raise
@@ -522,6 +547,10 @@ def Pipeline(img, o: ImageOptions, **kw):
         raise ImaginaryError("Missing pipeline operations")
     if len(o.operations) > 10:
         raise ImaginaryError("Maximum pipeline operations (10) exceeded")
+    # plan every stage on the previous stage's output geometry, then run the chain
+    # as ONE plan (mipx_plan_chain): one upload, intermediates stay in HBM, one
+    # download, and the runtime's peepholes see across stage boundaries
+    stages: list = []
     cur = img
     for i, op in enumerate(o.operations):
         name = op.get("operation")
@@ -530,10 +559,22 @@ def Pipeline(img, o: ImageOptions, **kw):
             raise ImaginaryError(f"Unsupported operation: {name}")
         opts = build_params_from_query(op.get("params", {}))
         try:
-            out = fn(cur, opts, **kw)
+            out = fn(cur, opts, chain=stages, **_stage_kw(fn, kw))
         except ImaginaryError:
             if not op.get("ignore_failure"):
                 raise
             continue
         cur = Decoded(out, type="png", orientation=0)
-    return cur.pixels
+    if not stages:
+        return cur.pixels
+    try:
+        merged = plan_chain([s[0] for s in stages])
+    except _abi.MipxError as e:
+        if e.code != _abi.MIPX_EUNSUPPORTED:
+            raise ImaginaryError(f"image processing error: {e}", 500) from e
+        px = stages[0][1]
+        for plan, _, wm in stages:  # too long or two watermarks: stage by stage
+            px = _run(plan, px, wm)
+        return px
+    wms = [s[2] for s in stages if s[2] is not None]
+    return _run(merged, stages[0][1], wms[0] if wms else None)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MIPX_ABI_VERSION 2
+#define MIPX_ABI_VERSION 3
 
 /* ---- error codes ---- */
 #define MIPX_OK 0
@@ -112,7 +112,7 @@ enum {
     MIPX_OP_BW           /* sRGB -> B_W                                      (vips_colourspace) */
 };
 
-#define MIPX_MAX_STEPS 16
+#define MIPX_MAX_STEPS 64   /* room for a merged /pipeline chain (mipx_plan_chain) */
 typedef struct mipx_step {
     int32_t op;
     int32_t a[8];
@@ -153,6 +153,14 @@ int mipx_device_count(void);
 
 /* ---- host planner (bimg resizer.go restated; callable without a GPU) ---- */
 int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_plan *plan);
+/* /pipeline GPU-resident fusion (image.go:379-410 Pipeline): concatenate the plans of
+ * a pipeline's stages (stage k planned on stage k-1's output, decoded intermediates)
+ * into one plan, so the request path runs the chain with one upload, device-resident
+ * intermediates and one download.  Stage k > 0 must take stage k-1's output geometry
+ * and have load_shrink 1; at most one stage may carry a watermark step.
+ * MIPX_EUNSUPPORTED when the chain exceeds MIPX_MAX_STEPS or has two watermark stages
+ * (the caller then runs the stages one by one). */
+int mipx_plan_chain(const mipx_plan *stages, int32_t n_stages, mipx_plan *out);
 /* imaginary image.go:190 calculateDestinationFitDimension */
 int mipx_fit_dimension(int32_t image_w, int32_t image_h, int32_t fit_w, int32_t fit_h,
                        int32_t *out_w, int32_t *out_h);
