@@ -39,7 +39,31 @@ struct SepTaps {
     int taps, pad, phased;
     double shrink;
     float rounding, inv_scale;  // conv rounding
+    int dot;                 // conv: integer v_dot4 path (MIPX_SEP_DOT=0 selects the float path)
 };
+
+// Conv masks (vips_gaussmat integer: every coefficient rint(20 * e^-x^2/2s^2),
+// 0..20) fit packed u8, so 4 taps x 4 bytes are 8 v_perm_b32 (4 x 4 byte
+// transpose) + 4 v_dot4_u32_u8, exact integer sums, instead of 16 byte
+// conversions + 16 FMAs.  in[j] byte c -> out[c] byte j.
+__device__ __forceinline__ void transpose4x4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t t[4]) {
+    const uint32_t ab_lo = __builtin_amdgcn_perm(b, a, 0x05010400u);  // a0 b0 a1 b1
+    const uint32_t ab_hi = __builtin_amdgcn_perm(b, a, 0x07030602u);  // a2 b2 a3 b3
+    const uint32_t cd_lo = __builtin_amdgcn_perm(d, c, 0x05010400u);
+    const uint32_t cd_hi = __builtin_amdgcn_perm(d, c, 0x07030602u);
+    t[0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);  // a0 b0 c0 d0
+    t[1] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);
+    t[2] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
+    t[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
+}
+// taps 4q .. 4q+3 of a 1-phase table as packed u8 (0 past the last tap)
+__device__ __forceinline__ uint32_t pack_taps(const float *c, int taps, int q) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (4 * q + j < taps) w |= static_cast<uint32_t>(c[4 * q + j]) << (8 * j);
+    return w;
+}
 
 __device__ __forceinline__ void sep_position(const SepTaps &t, int o, int *start, int *phase) {
     if (t.phased) {
@@ -145,6 +169,9 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
         sep_position(a.tp, a.oy0 + y0 + tid, &s, &ph);
         soff[tid] = s - r_lo;
     }
+    uint32_t *cpk = reinterpret_cast<uint32_t *>(soff + a.kr);  // conv: packed taps
+    const int tq = (taps + 3) >> 2;
+    if (MODE == kSepConv && tid < tq) cpk[tid] = pack_taps(a.tp.tab, taps, tid);
     __syncthreads();
     // ---- KR output rows from LDS ----
     const int j = cb * 1024 + tid * 4;
@@ -152,6 +179,39 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
     const int nb = min(4, a.row_bytes - j);
     u8 *dst = a.out + img * a.out_img + static_cast<long long>(y0) * a.row_bytes + j;
     const long long skew0 = delta + col0;
+    if (MODE == kSepConv && a.tp.dot) {
+        for (int k = 0; k < nk; ++k) {
+            const uint32_t *rp = rows + soff[k] * kVStride + tid;
+            uint32_t acc[4] = {0u, 0u, 0u, 0u};
+            for (int q = 0; q < tq; ++q) {
+                uint32_t v[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    v[i] = rp[(4 * q + i) * kVStride];
+                    if (DMA == 0) {
+                        const int r = clampi(r_lo + soff[k] + 4 * q + i, 0, a.hl - 1);
+                        const int sh = static_cast<int>(skew0 + static_cast<long long>(r) * a.in_pitch) & 3;
+                        v[i] = __builtin_amdgcn_alignbyte(rp[(4 * q + i) * kVStride + 1], v[i], sh);
+                    }
+                }
+                uint32_t t[4];
+                transpose4x4(v[0], v[1], v[2], v[3], t);
+                const uint32_t cw = cpk[q];
+#pragma unroll
+                for (int z = 0; z < 4; ++z) acc[z] = __builtin_amdgcn_udot4(t[z], cw, acc[z], false);
+            }
+            uint32_t o = 0;
+#pragma unroll
+            for (int z = 0; z < 4; ++z) o |= sep_round<MODE>(static_cast<float>(acc[z]), a.tp) << (8 * z);
+            u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
+            if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+                *reinterpret_cast<uint32_t *>(q) = o;
+            } else {
+                for (int z = 0; z < nb; ++z) q[z] = static_cast<u8>(o >> (8 * z));
+            }
+        }
+        return;
+    }
     for (int k = 0; k < nk; ++k) {
         const uint32_t *rp = rows + soff[k] * kVStride + tid;
         const float *ck = vcoef + k * taps;
@@ -294,7 +354,8 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
 #pragma unroll
         for (int i = 0; i < TREG; ++i) cr[i] = i < taps ? c[i] : 0.f;
     } else {
-        for (int i = tid; i < a.ntab; i += 256) ctab[i] = a.tp.tab[i];
+        const int nt = (a.tp.phased ? kTransformScale + 1 : 1) * taps;
+        for (int i = tid; i < a.ntab; i += 256) ctab[i] = i < nt ? a.tp.tab[i] : 0.f;
     }
     __syncthreads();
     {  // COPY edges (direct) or the repack of the raw bytes with each row's skew
@@ -342,7 +403,31 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
             }
         }
     };
-    if (TREG > 0) {
+    if (MODE == kSepConv && a.tp.dot) {  // conv: one phase, taps packed u8 (uniform)
+        uint32_t iacc[RB][4];
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int z = 0; z < 4; ++z) iacc[r][z] = 0u;
+        const int tq = (taps + 3) >> 2;
+        for (int q = 0; q < tq; ++q) {
+            const uint32_t cw = pack_taps(ctab, taps, q);
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                if (r < nr) {
+                    const uint32_t *pr = sp + r * a.span_max + 4 * q;
+                    uint32_t t[4];
+                    transpose4x4(pr[0], pr[1], pr[2], pr[3], t);
+#pragma unroll
+                    for (int z = 0; z < B; ++z) iacc[r][z] = __builtin_amdgcn_udot4(t[z], cw, iacc[r][z], false);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int z = 0; z < B; ++z) acc[r][z] = static_cast<float>(iacc[r][z]);
+    } else if (TREG > 0) {
 #pragma unroll
         for (int i = 0; i < TREG; ++i)
             if (i < taps) tap(i, cr[i]);
@@ -573,6 +658,8 @@ SepTaps make_taps(const SepSpec &s) {
     t.shrink = s.shrink;
     t.rounding = static_cast<float>((s.scale + 1) / 2);
     t.inv_scale = s.scale > 0 ? 1.0f / s.scale : 1.0f;
+    const char *e = std::getenv("MIPX_SEP_DOT");
+    t.dot = s.mode == kSepConv && !(e && *e == '0');
     return t;
 }
 
@@ -614,10 +701,11 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     int kr = taps >= kRowBudget ? 1 : static_cast<int>(std::floor((kRowBudget - taps - 1) / s)) + 1;
     kr = std::max(1, std::min({kr, 32, a.oh}));
     a.kr = kr;
-    a.lrows = static_cast<int>(std::ceil((kr - 1) * s)) + taps + 2;
+    a.lrows = static_cast<int>(std::ceil((kr - 1) * s)) + taps + 2 + (spec.mode == kSepConv ? 2 : 0);  // conv: taps read in 4s
     a.kr_blocks = (a.oh + kr - 1) / kr;
     const dim3 blk(256);
-    const size_t lds = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * taps * 4 + kr * 4;
+    const size_t lds = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * taps * 4 + kr * 4 +
+                       static_cast<size_t>((taps + 3) / 4) * 4;
     if (a.lrows > kRowMax || lds > 64 * 1024) {  // very tall masks: gather through L1
         const dim3 grid((a.row_bytes + 1023) / 1024, a.oh, n);
         if (spec.mode == kSepReduce) hipLaunchKernelGGL(k_vpass_gather<kSepReduce>, grid, blk, 0, st, a);

@@ -193,6 +193,20 @@ def test_gaussblur_matches_oracle(gpu, oracle, rng, sigma, b):
                 f"blur {sigma}")
 
 
+@pytest.mark.parametrize("dot", ["1", "0"])
+@pytest.mark.parametrize("sigma", [0.6, 2.2, 5.0, 9.0])
+def test_gaussblur_dot4_and_float_paths(gpu, oracle, rng, monkeypatch, dot, sigma):
+    """Conv passes: the packed-u8 v_dot4 path (default) and the float path
+    (MIPX_SEP_DOT=0) on every band count, odd widths and unaligned batches
+    (3 images of an odd byte size: the DMA=0 vertical staging)."""
+    monkeypatch.setenv("MIPX_SEP_DOT", dot)
+    for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
+        got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
+        for i in range(3):
+            assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur {sigma} {h}x{w}x{b} dot={dot} img{i}")
+
+
 # ---------------------------------------------------------------- affine (enlarge) / zoom / flatten / B_W
 @pytest.mark.parametrize("h,w,b,xs,ys,extend", [(30, 40, 3, 2.0, 2.0, 1), (17, 23, 4, 3.004291845493562, 3.004291845493562, 1),
                                               (33, 29, 1, 1.7, 0.8, 1), (20, 20, 3, 2.5, 2.5, 0), (15, 31, 2, 1.3, 4.1, 3),
