@@ -15,7 +15,7 @@
 //    The input rows those outputs need are staged in LDS once with direct-to-
 //    LDS buffer loads (no VGPR staging, all in flight together); lanes own
 //    4-byte columns (channel agnostic) and read their taps from LDS.
-//  * k_hpass<B, RB, MODE, DIRECT, TREG>: a block = 256 output pixels x RB
+//  * k_hpass<B, RB, MODE, DW, TREG>: a block = 256 output pixels x RB
 //    rows; the input spans are DMA'd to LDS and repacked to one u32 per pixel
 //    with the COPY edge; each lane reads its taps from LDS (reduce taps of
 //    <= 16 held per lane in registers).
@@ -39,8 +39,31 @@ struct SepTaps {
     int taps, pad, phased;
     double shrink;
     float rounding, inv_scale;  // conv rounding
-    int dot;                 // conv: integer v_dot4 path (MIPX_SEP_DOT=0 selects the float path)
+    int dot;                 // integer dot paths (MIPX_SEP_DOT=0 selects the float path)
 };
+
+// Reduce masks are 12-bit signed integers (x 4096), so tap pairs fit packed
+// int16 and v_dot2_i32_i16 sums byte pairs zero-extended to int16 exactly:
+// 4 v_perm_b32 + 4 dot2 per 2 taps x 4 bytes instead of 8 conversions + 8
+// FMAs, and libvips' (sum + 2048) >> 12 becomes an integer shift.
+typedef short short2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int dot2_byte(uint32_t lo_row, uint32_t hi_row, int z, uint32_t cw, int acc) {
+    const uint32_t sel = 0x0C040C00u + 0x00010001u * static_cast<uint32_t>(z);  // [lo.z, 0, hi.z, 0]
+    const uint32_t pr = __builtin_amdgcn_perm(hi_row, lo_row, sel);
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr), __builtin_bit_cast(short2v, cw), acc, false);
+}
+// The asm barrier keeps the backend from fusing shift + clamp + byte packing of
+// two channels into gfx950's v_ashr_pk_u8_i32: that instruction writes only the
+// low 16 bits of its destination, yet the fused code ORs the next channels into
+// bits 16-31 as if they were zero (seen as a channel-2 error on 4-band rows).
+__device__ __forceinline__ uint32_t fixed_round_i(int sum) {
+    int v = clampi((sum + 2048) >> 12, 0, 255);
+    asm("" : "+v"(v));
+    return static_cast<uint32_t>(v);
+}
+__device__ __forceinline__ uint32_t pack_pair(float c0, float c1) {
+    return (static_cast<uint32_t>(static_cast<int>(c0)) & 0xffffu) | (static_cast<uint32_t>(static_cast<int>(c1)) << 16);
+}
 
 // Conv masks (vips_gaussmat integer: every coefficient rint(20 * e^-x^2/2s^2),
 // 0..20) fit packed u8, so 4 taps x 4 bytes are 8 v_perm_b32 (4 x 4 byte
@@ -169,9 +192,18 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
         sep_position(a.tp, a.oy0 + y0 + tid, &s, &ph);
         soff[tid] = s - r_lo;
     }
-    uint32_t *cpk = reinterpret_cast<uint32_t *>(soff + a.kr);  // conv: packed taps
-    const int tq = (taps + 3) >> 2;
+    uint32_t *cpk = reinterpret_cast<uint32_t *>(soff + a.kr);  // conv: packed u8 taps; reduce: int16 pairs per row
+    const int tq = (taps + 3) >> 2, tp2 = (taps + 1) >> 1;
     if (MODE == kSepConv && tid < tq) cpk[tid] = pack_taps(a.tp.tab, taps, tid);
+    if (MODE == kSepReduce && a.tp.dot) {
+        for (int i = tid; i < nk * tp2; i += 256) {
+            const int k = i / tp2, m = i - k * tp2;
+            int st;
+            sep_position(a.tp, a.oy0 + y0 + k, &st, &ph);
+            const float *c = a.tp.tab + ph * taps;
+            cpk[i] = pack_pair(c[2 * m], 2 * m + 1 < taps ? c[2 * m + 1] : 0.f);
+        }
+    }
     __syncthreads();
     // ---- KR output rows from LDS ----
     const int j = cb * 1024 + tid * 4;
@@ -203,6 +235,38 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
             uint32_t o = 0;
 #pragma unroll
             for (int z = 0; z < 4; ++z) o |= sep_round<MODE>(static_cast<float>(acc[z]), a.tp) << (8 * z);
+            u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
+            if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+                *reinterpret_cast<uint32_t *>(q) = o;
+            } else {
+                for (int z = 0; z < nb; ++z) q[z] = static_cast<u8>(o >> (8 * z));
+            }
+        }
+        return;
+    }
+    if (MODE == kSepReduce && a.tp.dot) {
+        for (int k = 0; k < nk; ++k) {
+            const uint32_t *rp = rows + soff[k] * kVStride + tid;
+            const uint32_t *ck = cpk + k * tp2;
+            int acc[4] = {0, 0, 0, 0};
+            for (int m = 0; m < tp2; ++m) {
+                uint32_t v[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    v[i] = rp[(2 * m + i) * kVStride];
+                    if (DMA == 0) {
+                        const int r = clampi(r_lo + soff[k] + 2 * m + i, 0, a.hl - 1);
+                        const int sh = static_cast<int>(skew0 + static_cast<long long>(r) * a.in_pitch) & 3;
+                        v[i] = __builtin_amdgcn_alignbyte(rp[(2 * m + i) * kVStride + 1], v[i], sh);
+                    }
+                }
+                const uint32_t cw = ck[m];
+#pragma unroll
+                for (int z = 0; z < 4; ++z) acc[z] = dot2_byte(v[0], v[1], z, cw, acc[z]);
+            }
+            uint32_t o = 0;
+#pragma unroll
+            for (int z = 0; z < 4; ++z) o |= fixed_round_i(acc[z]) << (8 * z);
             u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
             if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
                 *reinterpret_cast<uint32_t *>(q) = o;
@@ -292,13 +356,16 @@ __device__ __forceinline__ uint32_t load_px_g(const u8 *p) {
     return v;
 }
 
-// DIRECT (B = 4, rows dword aligned): direct-to-LDS dword DMA of the span into
-// the pixel slots; otherwise DMA of each row's raw bytes from its aligned-down
-// start, repacked to one u32 per pixel in LDS (any alignment, any band count).
+// DW = 16 / 4 (B = 4, rows 16 / 4 byte aligned): direct-to-LDS dwordx4 / dword
+// DMA of the span into the pixel slots (DW 16 stages from the 4-pixel-aligned
+// start, so each row's LDS origin is lo rounded down to 4 pixels); DW = 0: DMA
+// of each row's raw bytes from its aligned-down start, repacked to one u32 per
+// pixel in LDS (any alignment, any band count).
 // TREG > 0: each lane holds its (<= TREG) taps in registers (reduce); 0: taps
 // from the LDS table.
-template <int B, int RB, int MODE, bool DIRECT, int TREG>
+template <int B, int RB, int MODE, int DW, int TREG>
 __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
+    constexpr bool DIRECT = DW != 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t hsm[];
     float *ctab = reinterpret_cast<float *>(hsm);
     uint32_t *spx = hsm + a.ntab;
@@ -321,28 +388,46 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
     const int y_first = rb * RB;
     const int nr = min(RB, a.rows - y_first);
     const int cl = max(lo, 0), ch = min(hi, a.wl - 1);  // pixels actually inside the row
+    const int org = DW == 16 ? (lo & ~3) : lo;           // pixel of LDS slot 0 (floor for lo < 0)
     const u8 *img_base = a.in + img * a.in_img;
     const long long row0 = a.in_base + static_cast<long long>(y_first) * a.in_pitch;
     int delta = 0;
-    if (DIRECT) {  // B = 4, rows dword aligned: pixels straight into their LDS slots
+    // (row, chunk) pairs dealt to the 4 waves round robin, walked without divisions
+    auto for_chunks = [&](int chunks, auto &&issue) {
+        int rr = 0, q = wave;
+        while (q >= chunks) q -= chunks, ++rr;
+        while (rr < nr) {
+            issue(rr, q);
+            q += 4;
+            while (q >= chunks) q -= chunks, ++rr;
+        }
+    };
+    if (DW == 16) {  // B = 4, rows 16-byte aligned: 4 pixels per lane straight into their slots
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(img_base, a.in_img);
+        const int cl4 = cl & ~3;
+        const int chunks = (((ch - cl4 + 4) >> 2) + 63) >> 6;
+        for_chunks(chunks, [&](int rr, int q) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, to_lds(spx + rr * a.span_max + (cl4 - org) + q * 256), 16,
+                static_cast<int>(row0) + 4 * cl4 + 16 * (q * 64 + lane), rr * a.in_pitch, 0, 0);
+        });
+    } else if (DW == 4) {  // B = 4, rows dword aligned
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(img_base, a.in_img);
         const int chunks = (ch - cl + 1 + 63) >> 6;
-        for (int idx = wave; idx < nr * chunks; idx += 4) {
-            const int rr = idx / chunks, q = idx - rr * chunks;
+        for_chunks(chunks, [&](int rr, int q) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rs, to_lds(spx + rr * a.span_max + (cl - lo) + q * 64), 4,
+                rs, to_lds(spx + rr * a.span_max + (cl - org) + q * 64), 4,
                 static_cast<int>(row0) + 4 * (cl + q * 64 + lane), rr * a.in_pitch, 0, 0);
-        }
+        });
     } else {  // any alignment: each row's raw bytes from its dword-aligned-down start
         const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(img_base, a.in_img, &delta);
         const int nd = (B * (ch - cl + 1) + 3 + 3) >> 2;
         const int chunks = (nd + 63) >> 6;
-        for (int idx = wave; idx < nr * chunks; idx += 4) {
-            const int rr = idx / chunks, q = idx - rr * chunks;
+        for_chunks(chunks, [&](int rr, int q) {
             const int a4 = static_cast<int>(delta + row0 + static_cast<long long>(rr) * a.in_pitch + B * cl) & ~3;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + rr * a.raw_max + q * 64), 4,
                                                      4 * (q * 64 + lane), a4, 0, 0);
-        }
+        });
     }
     // this lane's taps
     const int x = x0 + tid;
@@ -363,9 +448,9 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
             const int nl = cl - lo, nrt = hi - ch;
             for (int i = tid; i < nr * (nl + nrt); i += 256) {
                 const int rr = i / (nl + nrt), f = i - rr * (nl + nrt);
-                uint32_t *row = spx + rr * a.span_max;
-                if (f < nl) row[f] = row[nl];
-                else row[ch - lo + 1 + (f - nl)] = row[ch - lo];
+                uint32_t *row = spx + rr * a.span_max - org;  // indexed by pixel
+                if (f < nl) row[lo + f] = row[cl];
+                else row[ch + 1 + (f - nl)] = row[ch];
             }
         } else {
             const u8 *rb8 = reinterpret_cast<const u8 *>(raw);
@@ -384,7 +469,7 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
         __syncthreads();
     }
     if (x > x_last) return;
-    const uint32_t *sp = spx + (s - lo);
+    const uint32_t *sp = spx + (s - org);
     float acc[RB][B];
 #pragma unroll
     for (int r = 0; r < RB; ++r)
@@ -403,6 +488,45 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
             }
         }
     };
+    if (MODE == kSepReduce && TREG > 0 && a.tp.dot) {  // reduce: this lane's taps as int16 pairs
+        uint32_t cp[TREG > 0 ? TREG / 2 : 1];
+#pragma unroll
+        for (int m = 0; m < TREG / 2; ++m) cp[m] = pack_pair(cr[2 * m], cr[2 * m + 1]);
+        int iacc[RB][B];
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int z = 0; z < B; ++z) iacc[r][z] = 0;
+#pragma unroll
+        for (int m = 0; m < TREG / 2; ++m) {
+            if (2 * m < taps) {
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    if (r < nr) {
+                        const uint32_t *pr = sp + r * a.span_max + 2 * m;
+                        const uint32_t v0 = pr[0], v1 = pr[1];
+#pragma unroll
+                        for (int z = 0; z < B; ++z) iacc[r][z] = dot2_byte(v0, v1, z, cp[m], iacc[r][z]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            if (r >= nr) continue;
+            u8 *q = a.out + img * a.out_img + (static_cast<long long>(y_first + r) * a.ow + x) * B;
+            if (B == 4) {
+                uint32_t o = 0;
+#pragma unroll
+                for (int z = 0; z < B; ++z) o |= fixed_round_i(iacc[r][z]) << (8 * z);
+                *reinterpret_cast<uint32_t *>(q) = o;
+            } else {
+#pragma unroll
+                for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_i(iacc[r][z]));
+            }
+        }
+        return;
+    }
     if (MODE == kSepConv && a.tp.dot) {  // conv: one phase, taps packed u8 (uniform)
         uint32_t iacc[RB][4];
 #pragma unroll
@@ -659,7 +783,7 @@ SepTaps make_taps(const SepSpec &s) {
     t.rounding = static_cast<float>((s.scale + 1) / 2);
     t.inv_scale = s.scale > 0 ? 1.0f / s.scale : 1.0f;
     const char *e = std::getenv("MIPX_SEP_DOT");
-    t.dot = s.mode == kSepConv && !(e && *e == '0');
+    t.dot = !(e && *e == '0');
     return t;
 }
 
@@ -705,7 +829,7 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     a.kr_blocks = (a.oh + kr - 1) / kr;
     const dim3 blk(256);
     const size_t lds = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * taps * 4 + kr * 4 +
-                       static_cast<size_t>((taps + 3) / 4) * 4;
+                       static_cast<size_t>(std::max((taps + 3) / 4, kr * ((taps + 1) / 2))) * 4;
     if (a.lrows > kRowMax || lds > 64 * 1024) {  // very tall masks: gather through L1
         const dim3 grid((a.row_bytes + 1023) / 1024, a.oh, n);
         if (spec.mode == kSepReduce) hipLaunchKernelGGL(k_vpass_gather<kSepReduce>, grid, blk, 0, st, a);
@@ -760,11 +884,20 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     a.raw_max = (a.span_max * b + 8 + 3) / 4 + 64;
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     const bool dw = b == 4 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0 && aligned4(in);
+    const char *ehd = std::getenv("MIPX_HP_DMA");  // A/B: cap the DMA width (16 / 4)
+    const bool dw16 = dw && (a.in_pitch % 16) == 0 && (a.in_base % 16) == 0 && (a.in_img % 16) == 0 &&
+                      (reinterpret_cast<uintptr_t>(in) % 16) == 0 && !(ehd && *ehd && std::atoi(ehd) < 16);
+    if (dw16) {  // rows staged in whole 256-pixel dwordx4 waves from a 4-pixel-aligned origin
+        const int span_px = static_cast<int>(std::ceil(255 * s)) + a.tp.taps + 2;
+        const int per_row = ((span_px + 3 + 3) / 4 + 63) / 64;
+        a.span_max = ((a.tp.taps + 4 + per_row * 256 + 4) + 3) & ~3;
+    }
     if (b == 4 && !aligned4(out)) return MIPX_EINVAL;
     auto lds_for = [&](int rb) {
         return (static_cast<size_t>(a.ntab) + static_cast<size_t>(rb) * a.span_max +
                 (!dw ? static_cast<size_t>(rb) * a.raw_max : 0)) * 4;
     };
+    const int dwv = dw16 ? 16 : dw ? 4 : 0;
     constexpr size_t kLdsBudget = 40 * 1024;
     int rb = 8;
     while (rb > 1 && lds_for(rb) > kLdsBudget) rb >>= 1;
@@ -781,18 +914,16 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
 #define MIPX_HP3(RB_, MODE_, DW_, TR_) \
     MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_hpass<B_, RB_, MODE_, DW_, TR_>), grid, blk, lds, st, a))
+#define MIPX_HPW(RB_, MODE_, TR_)                                       \
+    if (dwv == 16) { MIPX_HP3(RB_, MODE_, 16, TR_) }                    \
+    else if (dwv == 4) { MIPX_HP3(RB_, MODE_, 4, TR_) }                 \
+    else { MIPX_HP3(RB_, MODE_, 0, TR_) }
 #define MIPX_HP2(RB_)                                                   \
     if (spec.mode == kSepReduce) {                                      \
-        if (treg) {                                                     \
-            if (dw) { MIPX_HP3(RB_, kSepReduce, true, kTReg) }          \
-            else { MIPX_HP3(RB_, kSepReduce, false, kTReg) }            \
-        } else {                                                        \
-            if (dw) { MIPX_HP3(RB_, kSepReduce, true, 0) }              \
-            else { MIPX_HP3(RB_, kSepReduce, false, 0) }                \
-        }                                                               \
+        if (treg) { MIPX_HPW(RB_, kSepReduce, kTReg) }                  \
+        else { MIPX_HPW(RB_, kSepReduce, 0) }                           \
     } else {                                                            \
-        if (dw) { MIPX_HP3(RB_, kSepConv, true, 0) }                    \
-        else { MIPX_HP3(RB_, kSepConv, false, 0) }                      \
+        MIPX_HPW(RB_, kSepConv, 0)                                      \
     }
     switch (rb) {
         case 8: MIPX_HP2(8) break;
@@ -801,6 +932,7 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
         default: MIPX_HP2(1) break;
     }
 #undef MIPX_HP2
+#undef MIPX_HPW
 #undef MIPX_HP3
     return launch_check("k_hpass");
 }

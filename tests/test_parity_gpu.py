@@ -207,6 +207,46 @@ def test_gaussblur_dot4_and_float_paths(gpu, oracle, rng, monkeypatch, dot, sigm
             assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur {sigma} {h}x{w}x{b} dot={dot} img{i}")
 
 
+@pytest.mark.parametrize("hdma", ["16", "4"])
+def test_hpass_dma_widths(gpu, oracle, rng, monkeypatch, hdma):
+    """Horizontal passes on RGBA with 16-byte-aligned rows stage through dwordx4
+    DMA by default (MIPX_HP_DMA=4 caps it at dword DMA): reduceh at several
+    shrinks, blur, and a whole reduce -> extract plan (window origin off the
+    16-byte grid), each against the oracle, with both image edges inside a block."""
+    monkeypatch.setenv("MIPX_HP_DMA", hdma)
+    for h, w, s in ((23, 256, 1.3333333333333333), (19, 300, 2.5), (11, 1028, 1.1), (9, 64, 3.0)):
+        imgs = np.stack([rand_img(rng, h, w, 4), smooth_img(rng, h, w, 4)])
+        got = gpu.run_op("reduceh", imgs, hshrink=s)
+        for i in range(2):
+            assert_same(got[i], oracle.reduceh(imgs[i], s), f"reduceh {w} {s} dma={hdma}")
+        got = gpu.run_op("gaussblur", imgs, sigma=2.4, min_ampl=0.2)
+        for i in range(2):
+            assert_same(got[i], oracle.gaussblur(imgs[i], 2.4, 0.2), f"blur {w} dma={hdma}")
+    opts = dict(width=300, height=200, crop=1)
+    p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(640, 520, 4, "png"))
+    e, rp = oracle.plan(opts, dict(w=640, h=520, bands=4, type=3))
+    assert e == 0
+    imgs = rng.integers(0, 256, (2, 520, 640, 4), dtype=np.uint8)
+    got = gpu.execute(p, imgs)
+    for i in range(2):
+        assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract dma={hdma}")
+
+
+@pytest.mark.parametrize("dot", ["1", "0"])
+@pytest.mark.parametrize("s", [1.1, 1.3333333333333333, 2.5, 3.7])
+def test_reduce_passes_dot2_and_float_paths(gpu, oracle, rng, monkeypatch, dot, s):
+    """Generic reduce passes: the int16 v_dot2 path (default) and the float path
+    (MIPX_SEP_DOT=0), every band count, odd sizes, unaligned batches."""
+    monkeypatch.setenv("MIPX_SEP_DOT", dot)
+    for h, w, b in ((41, 57, 1), (37, 43, 2), (64, 90, 3), (50, 128, 4), (31, 17, 3)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
+        gv = gpu.run_op("reducev", imgs, vshrink=s)
+        gh = gpu.run_op("reduceh", imgs, hshrink=s)
+        for i in range(3):
+            assert_same(gv[i], oracle.reducev(imgs[i], s), f"reducev {s} {h}x{w}x{b} dot={dot}")
+            assert_same(gh[i], oracle.reduceh(imgs[i], s), f"reduceh {s} {h}x{w}x{b} dot={dot}")
+
+
 # ---------------------------------------------------------------- affine (enlarge) / zoom / flatten / B_W
 @pytest.mark.parametrize("h,w,b,xs,ys,extend", [(30, 40, 3, 2.0, 2.0, 1), (17, 23, 4, 3.004291845493562, 3.004291845493562, 1),
                                               (33, 29, 1, 1.7, 0.8, 1), (20, 20, 3, 2.5, 2.5, 0), (15, 31, 2, 1.3, 4.1, 3),
