@@ -100,3 +100,26 @@ def test_request_api_before_init():
     t = C.c_uint64()
     assert ia.lib.mipx_wait(12345, 0) == -8           # unknown ticket
     assert ia.lib.mipx_stats(0, C.byref(t), C.byref(t)) in (-7, -1, 0)
+
+
+def test_code_object_avoids_known_bad_gfx950_fusion(tmp_path):
+    """The gfx950 backend can fuse shift + clamp + byte packing into
+    v_ashr_pk_u8_i32 and then treat its unwritten upper half as zero (a
+    channel-2 error found by the whole-plan fuzz).  k_sep.hip guards against it;
+    this keeps any kernel from reintroducing the instruction."""
+    import shutil
+    import imaginary_amd as ia
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    so = tmp_path / "libmipx.so"
+    shutil.copy(ia.LIB_PATH, so)
+    subprocess.run([objdump, "--offloading", str(so)], cwd=tmp_path, check=True, capture_output=True)
+    objs = [p for p in tmp_path.iterdir() if "gfx950" in p.name]
+    assert objs, "no gfx950 code object in libmipx.so"
+    seen_dot2 = False
+    for p in objs:
+        dis = subprocess.run([objdump, "-d", "--mcpu=gfx950", str(p)], check=True, capture_output=True, text=True).stdout
+        seen_dot2 |= "v_dot2_i32_i16" in dis or "v_dot2c_i32_i16" in dis
+        assert "v_ashr_pk_u8_i32" not in dis, f"{p.name}: v_ashr_pk_u8_i32 present"
+    assert seen_dot2, "disassembly lacks the reduce passes' dot2 (extraction failed?)"
