@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 
@@ -111,6 +112,98 @@ __global__ void __launch_bounds__(256) k_shrink_lds(ShrinkArgs a) {
     for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(div_floor(static_cast<float>(acc[z] + half), a.inv_hs));
 }
 
+// Rows dword aligned and vs <= 257: lanes own 16-byte chunks of the span
+// (buffer_load_dwordx4, 4x the bytes in flight per instruction) and sum byte
+// columns as packed u16 pairs (bytes 0/2 and 1/3 of each dword: every column
+// sum <= 257 * 255 < 2^16, so the pairs never carry into each other).
+template <int B>
+__global__ void __launch_bounds__(256) k_shrink_x4(ShrinkArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    u8 *col = reinterpret_cast<u8 *>(smem);
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int y = rest % a.oh;
+    const int img = rest / a.oh;
+    const int x0 = xb * a.tws;
+    const int nx = min(a.tws, a.ow - x0);
+    const int row_bytes = a.w * B;
+    const int span = nx * a.hs * B;
+    const int sb = x0 * a.hs * B;  // multiple of 4: x0 is a multiple of tws >= 4
+    const u8 *src = a.in + img * a.in_img;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
+    const uint32_t half = a.vs / 2;
+    const int r0 = y * a.vs;
+    for (int d = threadIdx.x * 16; d < span; d += 4096) {
+        const int g = sb + d;
+        uint32_t m[4];
+        if (g + 16 <= row_bytes) {
+            uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
+            for (int k0 = 0; k0 < a.vs; k0 += 8) {
+                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                u4v v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int r = min(r0 + min(k0 + q, a.vs - 1), a.h - 1);
+                    v[q] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, g, r * row_bytes, 0));
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    if (k0 + q < a.vs) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            lo[j] += v[q][j] & 0x00ff00ffu;
+                            hi[j] += (v[q][j] >> 8) & 0x00ff00ffu;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                m[j] = div_floor(static_cast<float>((lo[j] & 0xffffu) + half), a.inv_vs) |
+                       (div_floor(static_cast<float>((hi[j] & 0xffffu) + half), a.inv_vs) << 8) |
+                       (div_floor(static_cast<float>((lo[j] >> 16) + half), a.inv_vs) << 16) |
+                       (div_floor(static_cast<float>((hi[j] >> 16) + half), a.inv_vs) << 24);
+            }
+        } else {  // the chunk reaches past the row end: COPY border, byte by byte
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t sum[4] = {0u, 0u, 0u, 0u};
+                int off[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int gb = g + 4 * j + k;
+                    const int p = gb / B, c = gb - p * B;
+                    off[k] = min(p, a.w - 1) * B + c;
+                }
+                for (int k = 0; k < a.vs; ++k) {
+                    const u8 *p = src + static_cast<size_t>(min(r0 + k, a.h - 1)) * row_bytes;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) sum[b] += p[off[b]];
+                }
+                m[j] = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) m[j] |= div_floor(static_cast<float>(sum[b] + half), a.inv_vs) << (8 * b);
+            }
+        }
+        *reinterpret_cast<uint4 *>(smem + (d >> 2)) = uint4{m[0], m[1], m[2], m[3]};
+    }
+    __syncthreads();
+    const int x = threadIdx.x;
+    if (x >= nx) return;
+    const u8 *c = col + x * a.hs * B;
+    uint32_t acc[B];
+#pragma unroll
+    for (int z = 0; z < B; ++z) acc[z] = 0;
+    for (int j = 0; j < a.hs; ++j)
+#pragma unroll
+        for (int z = 0; z < B; ++z) acc[z] += c[j * B + z];
+    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x0 + x) * B;
+    const uint32_t hh = a.hs / 2;
+#pragma unroll
+    for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(div_floor(static_cast<float>(acc[z] + hh), a.inv_hs));
+}
+
 }  // namespace
 
 int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int vs, hipStream_t st) {
@@ -139,6 +232,15 @@ int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     const long long blocks = static_cast<long long>(a.x_blocks) * a.oh * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
+    const char *ex = std::getenv("MIPX_SHRINK_X4");  // A/B: 0 selects the dword kernel
+    const bool x4 = (w * b) % 4 == 0 && a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0 &&
+                    vs <= 257 && tws >= 4 && !(ex && *ex == '0');
+    if (x4) {  // chunks may run up to 16 bytes past the span: LDS rounded up to whole chunks
+        const size_t lds16 = ((static_cast<size_t>(tws) * hs * b + 15) / 16 + 1) * 16;
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_shrink_x4<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256),
+                                                  lds16, st, a));
+        return launch_check("k_shrink_x4");
+    }
     const size_t lds = ((static_cast<size_t>(tws) * hs * b + 3) / 4 + 1) * 4;
     MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_shrink_lds<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds,
                                               st, a));

@@ -184,6 +184,20 @@ def test_rot_tiles_and_aligned_extract(gpu, oracle, rng, h, w, b):
                     oracle.extract(img, left, top, ew, eh), f"extract {left},{top}")
 
 
+@pytest.mark.parametrize("x4", ["1", "0"])
+def test_shrink_x4_and_dword_kernels(gpu, oracle, rng, monkeypatch, x4):
+    """Box shrink: the 16-byte-per-lane kernel (dword-aligned rows, vs <= 257) and
+    the dword kernel (MIPX_SHRINK_X4=0, and any odd row), vs above one load batch,
+    spans past the row end (COPY border), every band count."""
+    monkeypatch.setenv("MIPX_SHRINK_X4", x4)
+    for h, w, b, hs, vs in ((64, 400, 3, 8, 8), (70, 333, 3, 3, 11), (300, 64, 4, 7, 260), (45, 1000, 1, 9, 5),
+                            (33, 66, 2, 5, 17), (100, 1024, 4, 16, 3), (50, 4000 // 8, 3, 11, 11)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("shrink", imgs, hshrink=hs, vshrink=vs)
+        for i in range(2):
+            assert_same(got[i], oracle.shrink(imgs[i], hs, vs), f"shrink {h}x{w}x{b} {hs}x{vs} x4={x4}")
+
+
 # ---------------------------------------------------------------- gaussian blur
 @pytest.mark.parametrize("sigma", [0.8, 1.0, 3.0, 5.0, 12.5])
 @pytest.mark.parametrize("b", [1, 3, 4])
