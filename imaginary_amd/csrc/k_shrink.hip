@@ -24,6 +24,7 @@ struct ShrinkArgs {
     const u8 *in;
     u8 *out;
     int w, h, ow, oh, hs, vs, tws, x_blocks;
+    int ry, y_blocks, lstride;  // k_shrink_x4: output rows per block, row blocks, LDS dwords per row
     float inv_hs, inv_vs;
     long long in_img, out_img;
 };
@@ -116,15 +117,15 @@ __global__ void __launch_bounds__(256) k_shrink_lds(ShrinkArgs a) {
 // (buffer_load_dwordx4, 4x the bytes in flight per instruction) and sum byte
 // columns as packed u16 pairs (bytes 0/2 and 1/3 of each dword: every column
 // sum <= 257 * 255 < 2^16, so the pairs never carry into each other).
-template <int B>
+template <int B, bool ROWS>
 __global__ void __launch_bounds__(256) k_shrink_x4(ShrinkArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     u8 *col = reinterpret_cast<u8 *>(smem);
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int xb = t % a.x_blocks;
     const int rest = t / a.x_blocks;
-    const int y = rest % a.oh;
-    const int img = rest / a.oh;
+    const int yb = rest % a.y_blocks;
+    const int img = rest / a.y_blocks;
     const int x0 = xb * a.tws;
     const int nx = min(a.tws, a.ow - x0);
     const int row_bytes = a.w * B;
@@ -133,9 +134,12 @@ __global__ void __launch_bounds__(256) k_shrink_x4(ShrinkArgs a) {
     const u8 *src = a.in + img * a.in_img;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
     const uint32_t half = a.vs / 2;
-    const int r0 = y * a.vs;
-    for (int d = threadIdx.x * 16; d < span; d += 4096) {
+    const int y0 = ROWS ? yb * a.ry : yb;
+    const int ny = ROWS ? min(a.ry, a.oh - y0) : 1;
+    // phase 1: 16 bytes x vs rows -> 16 rounded column means in LDS
+    auto chunk = [&](int yy, int d) {
         const int g = sb + d;
+        const int r0 = (y0 + yy) * a.vs;
         uint32_t m[4];
         if (g + 16 <= row_bytes) {
             uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
@@ -186,22 +190,37 @@ __global__ void __launch_bounds__(256) k_shrink_x4(ShrinkArgs a) {
                 for (int b = 0; b < 4; ++b) m[j] |= div_floor(static_cast<float>(sum[b] + half), a.inv_vs) << (8 * b);
             }
         }
-        *reinterpret_cast<uint4 *>(smem + (d >> 2)) = uint4{m[0], m[1], m[2], m[3]};
-    }
-    __syncthreads();
-    const int x = threadIdx.x;
-    if (x >= nx) return;
-    const u8 *c = col + x * a.hs * B;
-    uint32_t acc[B];
-#pragma unroll
-    for (int z = 0; z < B; ++z) acc[z] = 0;
-    for (int j = 0; j < a.hs; ++j)
-#pragma unroll
-        for (int z = 0; z < B; ++z) acc[z] += c[j * B + z];
-    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x0 + x) * B;
+        *reinterpret_cast<uint4 *>(smem + yy * a.lstride + (d >> 2)) = uint4{m[0], m[1], m[2], m[3]};
+    };
     const uint32_t hh = a.hs / 2;
+    // phase 2: one output pixel -> hs LDS pixels averaged
+    auto pixel = [&](int yy, int x) {
+        const u8 *c = col + yy * a.lstride * 4 + x * a.hs * B;
+        uint32_t acc[B];
 #pragma unroll
-    for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(div_floor(static_cast<float>(acc[z] + hh), a.inv_hs));
+        for (int z = 0; z < B; ++z) acc[z] = 0;
+        for (int j = 0; j < a.hs; ++j)
+#pragma unroll
+            for (int z = 0; z < B; ++z) acc[z] += c[j * B + z];
+        u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y0 + yy) * a.ow + x0 + x) * B;
+#pragma unroll
+        for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(div_floor(static_cast<float>(acc[z] + hh), a.inv_hs));
+    };
+    if (!ROWS) {
+        for (int d = threadIdx.x * 16; d < span; d += 4096) chunk(0, d);
+        __syncthreads();
+        if (static_cast<int>(threadIdx.x) < nx) pixel(0, threadIdx.x);
+        return;
+    }
+    // several output rows: (row, chunk) items stepped by 256 without a division per item
+    const int chunks = (span + 15) >> 4;
+    const int dy = 256 / chunks, dq = 256 - dy * chunks;
+    int yy = threadIdx.x / chunks, q = threadIdx.x - yy * chunks;
+    for (; yy < ny; yy += dy, q += dq, yy += q >= chunks ? 1 : 0, q -= q >= chunks ? chunks : 0) chunk(yy, q * 16);
+    __syncthreads();
+    const int py = 256 / nx, px = 256 - py * nx;
+    int y2 = threadIdx.x / nx, x2 = threadIdx.x - y2 * nx;
+    for (; y2 < ny; y2 += py, x2 += px, y2 += x2 >= nx ? 1 : 0, x2 -= x2 >= nx ? nx : 0) pixel(y2, x2);
 }
 
 }  // namespace
@@ -235,10 +254,26 @@ int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int
     const char *ex = std::getenv("MIPX_SHRINK_X4");  // A/B: 0 selects the dword kernel
     const bool x4 = (w * b) % 4 == 0 && a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0 &&
                     vs <= 257 && tws >= 4 && !(ex && *ex == '0');
-    if (x4) {  // chunks may run up to 16 bytes past the span: LDS rounded up to whole chunks
-        const size_t lds16 = ((static_cast<size_t>(tws) * hs * b + 15) / 16 + 1) * 16;
-        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_shrink_x4<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256),
-                                                  lds16, st, a));
+    if (x4) {
+        // output rows per block (small vs: enough to stream ~8 input rows), within 32 KB of LDS;
+        // each row's chunks may run up to 16 bytes past its span (LDS rows rounded to whole chunks)
+        a.lstride = static_cast<int>(((static_cast<size_t>(tws) * hs * b + 15) / 16 + 1) * 4);
+        const char *ery = std::getenv("MIPX_SHRINK_RY");
+        // measured (profiles/r01/v14/ab_shrink_rows.log): only vs <= 3 gains from several rows per block
+        int ry = (ery && *ery) ? std::max(1, std::atoi(ery)) : vs <= 3 ? (8 + vs - 1) / vs : 1;
+        while (ry > 1 && static_cast<size_t>(ry) * a.lstride * 4 > 32768) --ry;
+        a.ry = std::min(ry, a.oh);
+        a.y_blocks = (a.oh + a.ry - 1) / a.ry;
+        const long long blocks4 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
+        if (!grid_ok(blocks4)) return MIPX_EINVAL;
+        const size_t lds16 = static_cast<size_t>(a.ry) * a.lstride * 4;
+        if (a.ry > 1) {
+            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_shrink_x4<B_, true>), dim3(static_cast<unsigned>(blocks4)),
+                                                      dim3(256), lds16, st, a));
+        } else {
+            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_shrink_x4<B_, false>), dim3(static_cast<unsigned>(blocks4)),
+                                                      dim3(256), lds16, st, a));
+        }
         return launch_check("k_shrink_x4");
     }
     const size_t lds = ((static_cast<size_t>(tws) * hs * b + 3) / 4 + 1) * 4;
