@@ -22,7 +22,7 @@ if [ "${SKIP_BENCH:-0}" != 1 ]; then
 fi
 if [ "${SKIP_PROF:-0}" != 1 ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
-      python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu --no-verify > "$OUT/prof_$TAG.log" 2>&1
+      python3 "$R/bench.py" --steps 100 --warmup 20 --no-cpu --no-verify > "$OUT/prof_$TAG.log" 2>&1
   rc=$?; tail -5 "$OUT/prof_$TAG.log"; stop_if_fatal $rc rocprof
   find "$OUT/prof_$TAG" -name "*stats*" | head
 fi
