@@ -344,6 +344,7 @@ struct HPassArgs {
     int span_max;         // LDS pixels per staged row (incl. 64 of DMA overrun)
     int raw_max;          // LDS dwords per staged raw row (B < 4; incl. 64 of overrun)
     int ntab;             // floats of the tap table staged in LDS (0: taps in registers)
+    int repack4;          // raw path: 4-pixel vector repack (MIPX_HP_REPACK=0: one pixel per item)
     SepTaps tp;
 };
 
@@ -454,8 +455,7 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
             }
         } else {
             const u8 *rb8 = reinterpret_cast<const u8 *>(raw);
-            for (int i = tid; i < nr * span; i += 256) {
-                const int rr = i / span, p = i - rr * span;
+            auto repack1 = [&](int rr, int p) {  // one pixel, COPY edge by clamping
                 const int c = clampi(lo + p, 0, a.wl - 1);
                 const int skew = static_cast<int>(delta + row0 + static_cast<long long>(rr) * a.in_pitch + B * cl) & 3;
                 const u8 *q = rb8 + rr * a.raw_max * 4 + (c - cl) * B + skew;
@@ -464,6 +464,46 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
                 if (B > 2) v |= static_cast<uint32_t>(q[2]) << 16;
                 if (B > 3) v |= static_cast<uint32_t>(q[3]) << 24;
                 spx[rr * a.span_max + p] = v;
+            };
+            if (a.repack4) {
+                // 4 pixels per item: 4 B bytes from the raw row as 4 dword reads + v_alignbyte,
+                // split into one u32 per pixel with v_perm_b32, one 16-byte LDS write
+                const int groups = (span + 3) >> 2;
+                const int dy = 256 / groups, dq = 256 - dy * groups;
+                int rr = tid / groups, g = tid - rr * groups;
+                for (; rr < nr; rr += dy, g += dq, rr += g >= groups ? 1 : 0, g -= g >= groups ? groups : 0) {
+                    const int p0 = 4 * g, c0 = lo + p0;
+                    if (c0 < 0 || c0 + 3 > a.wl - 1 || p0 + 3 >= span) {
+                        for (int k = 0; k < 4 && p0 + k < span; ++k) repack1(rr, p0 + k);
+                        continue;
+                    }
+                    const int skew = static_cast<int>(delta + row0 + static_cast<long long>(rr) * a.in_pitch + B * cl) & 3;
+                    const int o = (c0 - cl) * B + skew;
+                    const uint32_t *rw = raw + rr * a.raw_max + (o >> 2);
+                    const int sh = o & 3;
+                    uint32_t d[B];
+#pragma unroll
+                    for (int k = 0; k < B; ++k) d[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], sh);
+                    uint4 px4;
+                    if (B == 1) {
+                        px4 = uint4{d[0] & 0xffu, (d[0] >> 8) & 0xffu, (d[0] >> 16) & 0xffu, d[0] >> 24};
+                    } else if (B == 2) {
+                        px4 = uint4{d[0] & 0xffffu, d[0] >> 16, d[B - 1] & 0xffffu, d[B - 1] >> 16};
+                    } else if (B == 3) {
+                        px4 = uint4{__builtin_amdgcn_perm(d[1], d[0], 0x0C020100u),
+                                    __builtin_amdgcn_perm(d[1], d[0], 0x0C050403u),
+                                    __builtin_amdgcn_perm(d[B - 1], d[1], 0x0C040302u),
+                                    __builtin_amdgcn_perm(d[B - 1], d[B - 1], 0x0C030201u)};
+                    } else {
+                        px4 = uint4{d[0], d[1 % B], d[2 % B], d[3 % B]};
+                    }
+                    *reinterpret_cast<uint4 *>(spx + rr * a.span_max + p0) = px4;
+                }
+            } else {
+                for (int i = tid; i < nr * span; i += 256) {
+                    const int rr = i / span;
+                    repack1(rr, i - rr * span);
+                }
             }
         }
         __syncthreads();
@@ -880,7 +920,9 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     const bool treg = a.tp.phased && a.tp.taps <= kTReg;
     a.ntab = treg ? 0 : (((a.tp.phased ? kTransformScale + 1 : 1) * a.tp.taps + 3) & ~3);
     const double s = a.tp.phased ? spec.shrink : 1.0;
-    a.span_max = static_cast<int>(std::ceil(255 * s)) + a.tp.taps + 2 + 64;
+    a.span_max = (static_cast<int>(std::ceil(255 * s)) + a.tp.taps + 2 + 64 + 3) & ~3;  // 16-byte rows
+    const char *erp = std::getenv("MIPX_HP_REPACK");
+    a.repack4 = !(erp && *erp == '0');
     a.raw_max = (a.span_max * b + 8 + 3) / 4 + 64;
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     const bool dw = b == 4 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0 && aligned4(in);

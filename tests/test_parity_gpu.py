@@ -261,6 +261,23 @@ def test_reduce_passes_dot2_and_float_paths(gpu, oracle, rng, monkeypatch, dot, 
             assert_same(gh[i], oracle.reduceh(imgs[i], s), f"reduceh {s} {h}x{w}x{b} dot={dot}")
 
 
+@pytest.mark.parametrize("repack", ["1", "0"])
+def test_hpass_raw_repack_paths(gpu, oracle, rng, monkeypatch, repack):
+    """Horizontal passes on rows that are not 16/4-byte aligned stage raw bytes and
+    repack them per pixel: 4 pixels per item with v_alignbyte / v_perm (default) or
+    one per item (MIPX_HP_REPACK=0); every band count, both image edges in a block."""
+    monkeypatch.setenv("MIPX_HP_REPACK", repack)
+    for h, w, b in ((9, 301, 3), (7, 517, 1), (6, 259, 2), (5, 263, 4), (11, 37, 3)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
+        for s in (1.6, 2.9):
+            got = gpu.run_op("reduceh", imgs, hshrink=s)
+            for i in range(3):
+                assert_same(got[i], oracle.reduceh(imgs[i], s), f"reduceh {h}x{w}x{b} {s} repack={repack}")
+        got = gpu.run_op("gaussblur", imgs, sigma=1.5, min_ampl=0.2)
+        for i in range(3):
+            assert_same(got[i], oracle.gaussblur(imgs[i], 1.5, 0.2), f"blur {h}x{w}x{b} repack={repack}")
+
+
 # ---------------------------------------------------------------- affine (enlarge) / zoom / flatten / B_W
 @pytest.mark.parametrize("h,w,b,xs,ys,extend", [(30, 40, 3, 2.0, 2.0, 1), (17, 23, 4, 3.004291845493562, 3.004291845493562, 1),
                                               (33, 29, 1, 1.7, 0.8, 1), (20, 20, 3, 2.5, 2.5, 0), (15, 31, 2, 1.3, 4.1, 3),
