@@ -207,7 +207,7 @@ def e2e(args, dev, sp, stream):
     n = args.e2e_requests
     plan = plan_for(dict(width=1920, height=1080, embed=1), 3840, 2160, 3)
     rng = np.random.default_rng(6)
-    srcs = [rng.integers(0, 256, (2160, 3840, 3), dtype=np.uint8) for _ in range(8)]
+    srcs = [rng.integers(0, 256, (2160, 3840, 3), dtype=np.uint8) for _ in range(8)]  # shared inputs, any thread count
     eng = ia.Engine(devices=[local], max_batch=args.e2e_batch, batch_wait_us=1000)
     try:
         def one(i):
@@ -215,7 +215,7 @@ def e2e(args, dev, sp, stream):
             eng.wait(t)
             return out
 
-        with ThreadPoolExecutor(8) as ex:
+        with ThreadPoolExecutor(args.e2e_threads) as ex:
             first = list(ex.map(one, range(2 * args.e2e_batch)))  # warm: buffers, pinned pool
             b0, r0 = eng.stats(local)
             t0 = time.perf_counter()
@@ -227,7 +227,7 @@ def e2e(args, dev, sp, stream):
             bool(np.array_equal(first[1], o.reduce(srcs[1], 2.0, 2.0)))
         link = n * (3840 * 2160 * 3 + 1920 * 1080 * 3)
         print(json.dumps({"config": "E2E", "workload": "request path: 4K RGB -> 1080p from host memory, "
-                          "8 submitting threads, pinned staging + H2D/compute/D2H streams",
+                          f"{args.e2e_threads} submitting threads, pinned staging + H2D/compute/D2H streams",
                           "images_per_sec": round(n / dt, 1), "requests": n, "wall_s": round(dt, 3),
                           "host_link_gbs": round(link / dt / 1e9, 2),
                           "batches": int(b1 - b0), "mean_batch": round((r1 - r0) / max(1, b1 - b0), 2),
@@ -245,6 +245,7 @@ def main():
     ap.add_argument("--c4-batch", type=int, default=64)
     ap.add_argument("--e2e-requests", type=int, default=256)
     ap.add_argument("--e2e-batch", type=int, default=16)
+    ap.add_argument("--e2e-threads", type=int, default=16, help="submitting threads (requests in flight)")
     ap.add_argument("--c5-requests", type=int, default=512 * int(os.environ.get("WORLD_SIZE", "1")),
                     help="total requests, sharded across ranks (4096 at 8 GPUs)")
     args = ap.parse_args()

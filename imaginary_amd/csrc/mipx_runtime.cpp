@@ -11,6 +11,7 @@
 // one queue per device with least-loaded dispatch — no collectives.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -18,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -388,6 +390,73 @@ PinnedPool &pool() {
     return *p;
 }
 
+// Host copies of the request path run on a few threads: one batch's outputs are
+// copied out of pinned staging into the callers' buffers in ~1 MiB pieces, which
+// also spreads the first-touch page faults of freshly allocated outputs.  The
+// calling thread works too, so a call never waits on an idle pool.
+class CopyPool {
+public:
+    explicit CopyPool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    void parallel_for(int n, const std::function<void(int)> &fn) {
+        if (n <= 0) return;
+        auto t = std::make_shared<Task>();
+        t->fn = &fn;
+        t->n = n;
+        t->left = n;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back(t);
+        }
+        cv_.notify_all();
+        work(*t);
+        std::unique_lock<std::mutex> lk(t->mu);
+        t->cv.wait(lk, [&] { return t->left.load() == 0; });
+    }
+
+private:
+    struct Task {
+        const std::function<void(int)> *fn = nullptr;
+        int n = 0;
+        std::atomic<int> next{0}, left{0};
+        std::mutex mu;
+        std::condition_variable cv;
+    };
+    static void work(Task &t) {
+        for (int i; (i = t.next.fetch_add(1)) < t.n;) {
+            (*t.fn)(i);
+            if (t.left.fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> lk(t.mu);
+                t.cv.notify_all();
+            }
+        }
+    }
+    void loop() {
+        for (;;) {
+            std::shared_ptr<Task> t;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return !q_.empty(); });
+                t = q_.front();
+                if (t->next.load() >= t->n) {  // exhausted: drop it and look again
+                    q_.pop_front();
+                    continue;
+                }
+            }
+            work(*t);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<Task>> q_;
+};
+CopyPool &copy_pool() {
+    static CopyPool *p = new CopyPool(std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2)));  // leaked: threads live with the process
+    return *p;
+}
+
 struct Job {
     uint64_t ticket = 0;
     mipx_plan plan{};
@@ -516,17 +585,25 @@ void retire_batch(Device &d, Slot &s) {
         (void)hipStreamSynchronize(d.s_d2h);
     }
     const size_t out1 = s.batch[0]->out_bytes;
-    for (size_t i = 0; i < s.batch.size(); ++i) {
-        auto &j = s.batch[i];
-        if (e == MIPX_OK) {
-            const mipx_img &o = j->out;
-            const size_t row = static_cast<size_t>(o.w) * o.bands;
+    if (e == MIPX_OK && out1 > 0) {  // outputs -> callers, in row-aligned pieces of ~1 MiB
+        const mipx_img &o0 = s.batch[0]->out;
+        const size_t row = static_cast<size_t>(o0.w) * o0.bands;
+        const int rows_per = static_cast<int>(std::max<size_t>(1, (size_t(1) << 20) / std::max<size_t>(1, row)));
+        const int pieces = (o0.h + rows_per - 1) / rows_per;
+        const int nb = static_cast<int>(s.batch.size());
+        copy_pool().parallel_for(nb * pieces, [&](int k) {
+            const int i = k / pieces, y0 = (k - i * pieces) * rows_per;
+            const mipx_img &o = s.batch[i]->out;
+            const int y1 = std::min(o.h, y0 + rows_per);
             const size_t stride = o.stride ? static_cast<size_t>(o.stride) : row;
             const uint8_t *src = s.h_out + out1 * i;
-            if (stride == row) std::memcpy(o.data, src, out1);
+            if (stride == row) std::memcpy(o.data + y0 * row, src + y0 * row, (y1 - y0) * row);
             else
-                for (int y = 0; y < o.h; ++y) std::memcpy(o.data + y * stride, src + y * row, row);
-        }
+                for (int y = y0; y < y1; ++y) std::memcpy(o.data + y * stride, src + y * row, row);
+        });
+    }
+    for (size_t i = 0; i < s.batch.size(); ++i) {
+        auto &j = s.batch[i];
         d.pending_bytes -= static_cast<int64_t>(j->in_bytes);
         pool().put(j->pin_in, j->in_cap);
         j->pin_in = nullptr;
