@@ -857,15 +857,21 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     const double s = spec.mode == kSepReduce ? spec.shrink : 1.0;
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     a.col_blocks = (a.row_bytes + 1023) / 1024;
-    // rows per block: fill ~40 staged input rows (40 KiB of LDS)
-    // staged input rows per block (LDS KiB); MIPX_VP_ROWS overrides for A/B runs
+    // staged input rows per block (1 KiB each); MIPX_VP_ROWS overrides for A/B runs
     const char *erb = std::getenv("MIPX_VP_ROWS");
-    const int kRowBudget = (erb && *erb) ? std::max(8, std::atoi(erb)) : 24;  // A/B: profiles/r01/v12_vpass_ab.log
+    // 24 rows measured best at 9-17 taps (v12_vpass_ab.log, v14/ab_vpass_rows_blur.log); taller
+    // masks need room for several output rows per block (25 taps: 40 rows 2.6 vs 1.7 TB/s,
+    // v14/ab_vpass_budget.log)
+    const int kRowBudget = (erb && *erb) ? std::max(8, std::atoi(erb)) : std::max(24, taps + 15);
     constexpr int kRowMax = 60;
     int kr = taps >= kRowBudget ? 1 : static_cast<int>(std::floor((kRowBudget - taps - 1) / s)) + 1;
     kr = std::max(1, std::min({kr, 32, a.oh}));
+    auto rows_for = [&](int k) {  // conv: taps read in 4s
+        return static_cast<int>(std::ceil((k - 1) * s)) + taps + 2 + (spec.mode == kSepConv ? 2 : 0);
+    };
+    while (kr > 1 && rows_for(kr) > kRowMax) --kr;  // stay on the staged path when one row fits
     a.kr = kr;
-    a.lrows = static_cast<int>(std::ceil((kr - 1) * s)) + taps + 2 + (spec.mode == kSepConv ? 2 : 0);  // conv: taps read in 4s
+    a.lrows = rows_for(kr);
     a.kr_blocks = (a.oh + kr - 1) / kr;
     const dim3 blk(256);
     const size_t lds = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * taps * 4 + kr * 4 +
