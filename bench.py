@@ -198,7 +198,7 @@ def main():
                          "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
             "verified_vs_oracle": verify,
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the CPU baseline is an N = 1 figure
             line["cpu_baseline"] = cpu_baseline(args, cpu_sample if verify is not None else
                                                 [np.random.default_rng(1).integers(0, 256, (H_IN, W_IN, BANDS),
                                                                                    dtype=np.uint8)])
