@@ -40,6 +40,7 @@ struct SepTaps {
     double shrink;
     float rounding, inv_scale;  // conv rounding
     int dot;                 // integer dot paths (MIPX_SEP_DOT=0 selects the float path)
+    int tq;                  // conv vpass: rows transposed once per 4-row quad (MIPX_SEP_TQ=0: per output row)
 };
 
 // Reduce masks are 12-bit signed integers (x 4096), so tap pairs fit packed
@@ -195,6 +196,19 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
     uint32_t *cpk = reinterpret_cast<uint32_t *>(soff + a.kr);  // conv: packed u8 taps; reduce: int16 pairs per row
     const int tq = (taps + 3) >> 2, tp2 = (taps + 1) >> 1;
     if (MODE == kSepConv && tid < tq) cpk[tid] = pack_taps(a.tp.tab, taps, tid);
+    // conv, quad-transposed rows: coefficient set p (output row k with k % 4 == p) for
+    // quad j holds taps 4j + b - p, b = 0..3 (0 outside the mask)
+    const int tqp = (taps + 6) >> 2;
+    if (MODE == kSepConv && tid < 4 * tqp) {
+        const int p = tid / tqp, j = tid - p * tqp;
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int t = 4 * j + b - p;
+            if (t >= 0 && t < taps) w |= static_cast<uint32_t>(a.tp.tab[t]) << (8 * b);
+        }
+        cpk[tq + tid] = w;
+    }
     if (MODE == kSepReduce && a.tp.dot) {
         for (int i = tid; i < nk * tp2; i += 256) {
             const int k = i / tp2, m = i - k * tp2;
@@ -211,6 +225,41 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
     const int nb = min(4, a.row_bytes - j);
     u8 *dst = a.out + img * a.out_img + static_cast<long long>(y0) * a.row_bytes + j;
     const long long skew0 = delta + col0;
+    if (MODE == kSepConv && a.tp.dot && DMA != 0 && a.tp.tq) {
+        // each lane transposes its own column's staged rows in place, 4-row quads at a time
+        // (no other lane touches them), so an output row costs 4 LDS reads + 4 v_dot4 per
+        // quad instead of 4 reads + 8 v_perm + 4 v_dot4 (conv: soff[k] == k)
+        const int nq = (nk + taps + 2) >> 2;
+        for (int m = 0; m < nq; ++m) {
+            uint32_t *rq = rows + 4 * m * kVStride + tid;
+            uint32_t t[4];
+            transpose4x4(rq[0], rq[kVStride], rq[2 * kVStride], rq[3 * kVStride], t);
+#pragma unroll
+            for (int z = 0; z < 4; ++z) rq[z * kVStride] = t[z];
+        }
+        const uint32_t *cph = cpk + tq;
+        for (int k = 0; k < nk; ++k) {
+            const int p = k & 3, nqk = (p + taps + 3) >> 2;
+            const uint32_t *rq = rows + 4 * (k >> 2) * kVStride + tid;
+            const uint32_t *cw = cph + p * tqp;
+            uint32_t acc[4] = {0u, 0u, 0u, 0u};
+            for (int j = 0; j < nqk; ++j) {
+                const uint32_t c = cw[j];
+#pragma unroll
+                for (int z = 0; z < 4; ++z) acc[z] = __builtin_amdgcn_udot4(rq[(4 * j + z) * kVStride], c, acc[z], false);
+            }
+            uint32_t o = 0;
+#pragma unroll
+            for (int z = 0; z < 4; ++z) o |= sep_round<MODE>(static_cast<float>(acc[z]), a.tp) << (8 * z);
+            u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
+            if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+                *reinterpret_cast<uint32_t *>(q) = o;
+            } else {
+                for (int z = 0; z < nb; ++z) q[z] = static_cast<u8>(o >> (8 * z));
+            }
+        }
+        return;
+    }
     if (MODE == kSepConv && a.tp.dot) {
         for (int k = 0; k < nk; ++k) {
             const uint32_t *rp = rows + soff[k] * kVStride + tid;
@@ -824,6 +873,8 @@ SepTaps make_taps(const SepSpec &s) {
     t.inv_scale = s.scale > 0 ? 1.0f / s.scale : 1.0f;
     const char *e = std::getenv("MIPX_SEP_DOT");
     t.dot = !(e && *e == '0');
+    const char *eq = std::getenv("MIPX_SEP_TQ");
+    t.tq = !(eq && *eq == '0');
     return t;
 }
 
@@ -875,7 +926,7 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     a.kr_blocks = (a.oh + kr - 1) / kr;
     const dim3 blk(256);
     const size_t lds = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * taps * 4 + kr * 4 +
-                       static_cast<size_t>(std::max((taps + 3) / 4, kr * ((taps + 1) / 2))) * 4;
+                       static_cast<size_t>(std::max((taps + 3) / 4 + 4 * ((taps + 6) / 4), kr * ((taps + 1) / 2))) * 4;
     if (a.lrows > kRowMax || lds > 64 * 1024) {  // very tall masks: gather through L1
         const dim3 grid((a.row_bytes + 1023) / 1024, a.oh, n);
         if (spec.mode == kSepReduce) hipLaunchKernelGGL(k_vpass_gather<kSepReduce>, grid, blk, 0, st, a);
