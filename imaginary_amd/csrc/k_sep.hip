@@ -490,8 +490,25 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
         for (int i = 0; i < TREG; ++i) cr[i] = i < taps ? c[i] : 0.f;
     } else {
         const int nt = (a.tp.phased ? kTransformScale + 1 : 1) * taps;
-        for (int i = tid; i < a.ntab; i += 256) ctab[i] = i < nt ? a.tp.tab[i] : 0.f;
+        const int nfl = MODE == kSepConv ? ((taps + 3) & ~3) : a.ntab;  // conv: packed phase sets follow
+        for (int i = tid; i < nfl; i += 256) ctab[i] = i < nt ? a.tp.tab[i] : 0.f;
+        if (MODE == kSepConv) {
+            const int tqp = (taps + 6) >> 2;
+            for (int i = tid; i < 4 * tqp; i += 256) {
+                const int p = i / tqp, j = i - p * tqp;
+                uint32_t w = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int t = 4 * j + b - p;
+                    if (t >= 0 && t < taps) w |= static_cast<uint32_t>(a.tp.tab[t]) << (8 * b);
+                }
+                reinterpret_cast<uint32_t *>(ctab)[nfl + i] = w;
+            }
+        }
     }
+    // conv: staged pixels transposed per 4-slot group (channel-major dwords), so an
+    // output pixel costs B LDS reads + B v_dot4 per group, no per-pixel v_perm
+    const bool htq = MODE == kSepConv && a.tp.dot && a.tp.tq && (DIRECT || a.repack4);
     __syncthreads();
     {  // COPY edges (direct) or the repack of the raw bytes with each row's skew
         if (DIRECT) {
@@ -504,7 +521,7 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
             }
         } else {
             const u8 *rb8 = reinterpret_cast<const u8 *>(raw);
-            auto repack1 = [&](int rr, int p) {  // one pixel, COPY edge by clamping
+            auto px1 = [&](int rr, int p) -> uint32_t {  // one pixel, COPY edge by clamping
                 const int c = clampi(lo + p, 0, a.wl - 1);
                 const int skew = static_cast<int>(delta + row0 + static_cast<long long>(rr) * a.in_pitch + B * cl) & 3;
                 const u8 *q = rb8 + rr * a.raw_max * 4 + (c - cl) * B + skew;
@@ -512,8 +529,9 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
                 if (B > 1) v |= static_cast<uint32_t>(q[1]) << 8;
                 if (B > 2) v |= static_cast<uint32_t>(q[2]) << 16;
                 if (B > 3) v |= static_cast<uint32_t>(q[3]) << 24;
-                spx[rr * a.span_max + p] = v;
+                return v;
             };
+            auto repack1 = [&](int rr, int p) { spx[rr * a.span_max + p] = px1(rr, p); };
             if (a.repack4) {
                 // 4 pixels per item: 4 B bytes from the raw row as 4 dword reads + v_alignbyte,
                 // split into one u32 per pixel with v_perm_b32, one 16-byte LDS write
@@ -523,7 +541,13 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
                 for (; rr < nr; rr += dy, g += dq, rr += g >= groups ? 1 : 0, g -= g >= groups ? groups : 0) {
                     const int p0 = 4 * g, c0 = lo + p0;
                     if (c0 < 0 || c0 + 3 > a.wl - 1 || p0 + 3 >= span) {
-                        for (int k = 0; k < 4 && p0 + k < span; ++k) repack1(rr, p0 + k);
+                        if (htq) {  // whole group (clamped past the span) so it can be transposed
+                            uint32_t t[4];
+                            transpose4x4(px1(rr, p0), px1(rr, p0 + 1), px1(rr, p0 + 2), px1(rr, p0 + 3), t);
+                            *reinterpret_cast<uint4 *>(spx + rr * a.span_max + p0) = uint4{t[0], t[1], t[2], t[3]};
+                        } else {
+                            for (int k = 0; k < 4 && p0 + k < span; ++k) repack1(rr, p0 + k);
+                        }
                         continue;
                     }
                     const int skew = static_cast<int>(delta + row0 + static_cast<long long>(rr) * a.in_pitch + B * cl) & 3;
@@ -546,6 +570,11 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
                     } else {
                         px4 = uint4{d[0], d[1 % B], d[2 % B], d[3 % B]};
                     }
+                    if (htq) {
+                        uint32_t t[4];
+                        transpose4x4(px4.x, px4.y, px4.z, px4.w, t);
+                        px4 = uint4{t[0], t[1], t[2], t[3]};
+                    }
                     *reinterpret_cast<uint4 *>(spx + rr * a.span_max + p0) = px4;
                 }
             } else {
@@ -556,6 +585,19 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
             }
         }
         __syncthreads();
+        if (DIRECT && htq) {  // transpose the DMA'd (and edge-filled) slots in place, 4 at a time
+            const int groups = (hi - org + 4) >> 2;
+            const int dy = 256 / groups, dq = 256 - dy * groups;
+            int rr = tid / groups, g = tid - rr * groups;
+            for (; rr < nr; rr += dy, g += dq, rr += g >= groups ? 1 : 0, g -= g >= groups ? groups : 0) {
+                uint4 *q4 = reinterpret_cast<uint4 *>(spx + rr * a.span_max + 4 * g);
+                const uint4 v = *q4;
+                uint32_t t[4];
+                transpose4x4(v.x, v.y, v.z, v.w, t);
+                *q4 = uint4{t[0], t[1], t[2], t[3]};
+            }
+            __syncthreads();
+        }
     }
     if (x > x_last) return;
     const uint32_t *sp = spx + (s - org);
@@ -616,7 +658,30 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
         }
         return;
     }
-    if (MODE == kSepConv && a.tp.dot) {  // conv: one phase, taps packed u8 (uniform)
+    if (MODE == kSepConv && htq) {  // conv on transposed groups: phase set by this lane's slot
+        const int base = s - org, p = base & 3, nqk = (p + taps + 3) >> 2;
+        const uint32_t *cph = reinterpret_cast<const uint32_t *>(ctab) + ((taps + 3) & ~3) + p * ((taps + 6) >> 2);
+        uint32_t iacc[RB][4];
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int z = 0; z < 4; ++z) iacc[r][z] = 0u;
+        for (int j = 0; j < nqk; ++j) {
+            const uint32_t c = cph[j];
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                if (r < nr) {
+                    const uint32_t *qd = spx + r * a.span_max + 4 * ((base >> 2) + j);
+#pragma unroll
+                    for (int z = 0; z < B; ++z) iacc[r][z] = __builtin_amdgcn_udot4(qd[z], c, iacc[r][z], false);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int z = 0; z < B; ++z) acc[r][z] = static_cast<float>(iacc[r][z]);
+    } else if (MODE == kSepConv && a.tp.dot) {  // conv: one phase, taps packed u8 (uniform)
         uint32_t iacc[RB][4];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
@@ -874,7 +939,7 @@ SepTaps make_taps(const SepSpec &s) {
     const char *e = std::getenv("MIPX_SEP_DOT");
     t.dot = !(e && *e == '0');
     const char *eq = std::getenv("MIPX_SEP_TQ");
-    t.tq = !(eq && *eq == '0');
+    t.tq = !(eq && *eq == '0') && s.taps >= 7;  // 3-tap masks lose to the transpose (v14/ab_conv_quad_transpose.log)
     return t;
 }
 
@@ -976,6 +1041,7 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     constexpr int kTReg = 16;
     const bool treg = a.tp.phased && a.tp.taps <= kTReg;
     a.ntab = treg ? 0 : (((a.tp.phased ? kTransformScale + 1 : 1) * a.tp.taps + 3) & ~3);
+    if (spec.mode != kSepReduce) a.ntab += 4 * ((a.tp.taps + 6) / 4);  // conv: packed phase-shifted tap sets
     const double s = a.tp.phased ? spec.shrink : 1.0;
     a.span_max = (static_cast<int>(std::ceil(255 * s)) + a.tp.taps + 2 + 64 + 3) & ~3;  // 16-byte rows
     const char *erp = std::getenv("MIPX_HP_REPACK");
