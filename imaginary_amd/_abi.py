@@ -9,7 +9,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmipx.so")
+# MIPX_LIB_PATH: load another build of the same library (same-box A/B of two builds);
+# unset, the in-tree libmipx.so is the product
+LIB_PATH = os.environ.get("MIPX_LIB_PATH") or os.path.join(_HERE, "libmipx.so")
 
 MIPX_OK = 0
 MIPX_EINVAL = -1

@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
 template <int B, bool MIRROR>
 __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
                                                    int vflip, long long img_bytes_) {
-    __shared__ uint32_t seg[1024 + 8];
+    __shared__ __attribute__((aligned(16))) uint32_t seg[1024 + 8];
     const int Y = blockIdx.y;
     const int img = blockIdx.z;
     const int row_bytes = w * B;
@@ -197,9 +197,17 @@ __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8
     const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, img_bytes_, &delta);
     const int abs0 = delta + sy * row_bytes + s0;
     const int a4 = abs0 & ~3, skew = abs0 - a4;
-    const int nd = (s1 - s0 + skew + 3) >> 2;
-    for (int d = threadIdx.x; d < nd; d += 256)
-        seg[d] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4 * d, 0, 0));
+    const int nd = (s1 - s0 + skew + 3) >> 2;  // <= 1026
+    {  // one dwordx4 per lane (all in flight at once), the <= 3 spill dwords by lanes 0-2
+        const int t = threadIdx.x;
+        if (4 * t < nd) {
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+            const u4v v = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, a4 + 16 * t, 0, 0));
+            *reinterpret_cast<uint4 *>(seg + 4 * t) = uint4{v[0], v[1], v[2], v[3]};
+        }
+        if (t < nd - 1024)
+            seg[1024 + t] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4096 + 4 * t, 0, 0));
+    }
     __syncthreads();
     const u8 *sb = reinterpret_cast<const u8 *>(seg) + skew;
     const int jl = j0 + threadIdx.x * 16;
@@ -239,11 +247,25 @@ __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8
     const u8 *src = in + img * img_bytes_;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, img_bytes_, &delta);
     const int nd = (tw * B + 3 + 3) >> 2;
-    for (int i = threadIdx.x; i < th * nd; i += 256) {
-        const int r = i / nd, d = i - r * nd;
-        const int abs0 = delta + ((ty0 + r) * w + tx0) * B;
-        tile[r * RS + d] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, (abs0 & ~3) + 4 * d, 0, 0));
-        if (d == 0) skews[r] = abs0 & 3;
+    {  // every load of the tile in flight before the LDS writes (not one round trip each)
+        constexpr int kPer = (T * ((T * B + 6) / 4) + 255) / 256;
+        uint32_t v[kPer];
+        int slot[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            slot[k] = -1;
+            if (i < th * nd) {
+                const int r = i / nd, d = i - r * nd;
+                const int abs0 = delta + ((ty0 + r) * w + tx0) * B;
+                v[k] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, (abs0 & ~3) + 4 * d, 0, 0));
+                slot[k] = r * RS + d;
+                if (d == 0) skews[r] = abs0 & 3;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+            if (slot[k] >= 0) tile[slot[k]] = v[k];
     }
     __syncthreads();
     const u8 *t8 = reinterpret_cast<const u8 *>(tile);
