@@ -231,24 +231,26 @@ __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8
     }
 }
 
-// 90 / 270 via 64 x 64 pixel tiles: input tile rows staged in LDS with dword
-// loads, output rows gathered from LDS 16 bytes per lane.
+// 90 / 270 via 64 x 64 pixel tiles.  Staging: every tile row de-skewed on the way
+// into LDS (one b64 load per dword + v_alignbyte, all loads in flight before the
+// LDS writes), so a staged row starts exactly at the tile's first pixel.  Gather:
+// a task builds 4 output pixels from aligned LDS dword reads, packs them into B
+// dwords (v_perm) and stores them as one aligned B-dword write.
 template <int B, bool CW>
 __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
                                                    long long img_bytes_) {
     constexpr int T = 64;
-    constexpr int RS = (T * B + 8 + 3) / 4;  // dwords per staged row (skew + spill)
+    constexpr int RS = (T * B + 3) / 4 + 1;  // dwords per staged row (+1: the unaligned pixel read spills)
     __shared__ uint32_t tile[T * RS];
-    __shared__ int skews[T];
     const int img = blockIdx.z;
     const int tx0 = blockIdx.x * T, ty0 = blockIdx.y * T;  // input tile origin
     const int tw = min(T, w - tx0), th = min(T, h - ty0);
     int delta = 0;
     const u8 *src = in + img * img_bytes_;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, img_bytes_, &delta);
-    const int nd = (tw * B + 3 + 3) >> 2;
-    {  // every load of the tile in flight before the LDS writes (not one round trip each)
-        constexpr int kPer = (T * ((T * B + 6) / 4) + 255) / 256;
+    const int nd = (tw * B + 3) >> 2;
+    {
+        constexpr int kPer = (T * ((T * B + 3) / 4) + 255) / 256;
         uint32_t v[kPer];
         int slot[kPer];
 #pragma unroll
@@ -258,9 +260,10 @@ __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8
             if (i < th * nd) {
                 const int r = i / nd, d = i - r * nd;
                 const int abs0 = delta + ((ty0 + r) * w + tx0) * B;
-                v[k] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, (abs0 & ~3) + 4 * d, 0, 0));
+                typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+                const u2v p = __builtin_bit_cast(u2v, __builtin_amdgcn_raw_buffer_load_b64(rs, (abs0 & ~3) + 4 * d, 0, 0));
+                v[k] = __builtin_amdgcn_alignbyte(p[1], p[0], abs0 & 3);
                 slot[k] = r * RS + d;
-                if (d == 0) skews[r] = abs0 & 3;
             }
         }
 #pragma unroll
@@ -268,41 +271,50 @@ __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8
             if (slot[k] >= 0) tile[slot[k]] = v[k];
     }
     __syncthreads();
-    const u8 *t8 = reinterpret_cast<const u8 *>(tile);
-    // output tile: th columns wide (output x <- input y), tw rows tall
-    const int orow_bytes = th * B;
-    const int tasks_per_row = (orow_bytes + 15) / 16;
+    // output tile: th columns wide (output x <- input y), tw rows tall; 4 output pixels per task
+    const int quads = (th + 3) >> 2;
     u8 *dst = out + img * img_bytes_;
-    for (int task = threadIdx.x; task < tw * tasks_per_row; task += 256) {
-        const int orr = task / tasks_per_row, q16 = task - orr * tasks_per_row;
-        // output row within the tile -> input column; output columns -> input rows
-        const int icol = CW ? orr : tw - 1 - orr;
+    for (int task = threadIdx.x; task < tw * quads; task += 256) {
+        const int orr = task / quads, q = task - orr * quads;
+        const int icol = CW ? orr : tw - 1 - orr;  // output row within the tile -> input column
         int ox, oy;
         if (CW) {  // out(x, y) = in(y, h-1-x): output row oy = input col, output col ox = h-1-input row
             oy = tx0 + icol;
-            ox = h - (ty0 + th);  // output column of the tile's first byte (input row ty0 + th - 1)
+            ox = h - (ty0 + th);  // output column of the tile's first pixel (input row ty0 + th - 1)
         } else {   // out(x, y) = in(w-1-y, x): output row oy = w-1-input col, output col ox = input row
             oy = w - 1 - (tx0 + icol);
             ox = ty0;
         }
-        const int jb0 = q16 * 16;
-        const int nb = min(16, orow_bytes - jb0);
-        uint32_t v[4] = {0, 0, 0, 0};
+        const int px0 = 4 * q, npx = min(4, th - px0);
+        uint32_t P[4];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (k < nb) {
-                const int jb = jb0 + k;
-                const int px = jb / B, c = jb - px * B;
-                const int ir = CW ? th - 1 - px : px;  // input row within the tile
-                v[k >> 2] |= static_cast<uint32_t>(t8[ir * RS * 4 + skews[ir] + icol * B + c]) << (8 * (k & 3));
-            }
+        for (int k = 0; k < 4; ++k) {
+            const int ir = CW ? th - 1 - min(px0 + k, th - 1) : min(px0 + k, th - 1);  // input row within the tile
+            const int b0 = icol * B;
+            const uint32_t *row = tile + ir * RS + (b0 >> 2);
+            P[k] = B == 4 ? row[0] : __builtin_amdgcn_alignbyte(row[1], row[0], b0 & 3);
         }
-        u8 *q = dst + (static_cast<long long>(oy) * h + ox) * B + jb0;
-        if (nb == 16 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
-            uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
-            q32[0] = v[0], q32[1] = v[1], q32[2] = v[2], q32[3] = v[3];
+        uint32_t o[B];
+        if (B == 4) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) o[k] = P[k];
+        } else if (B == 3) {
+            o[0] = __builtin_amdgcn_perm(P[1], P[0], 0x04020100u);
+            o[1 % B] = __builtin_amdgcn_perm(P[2], P[1], 0x05040201u);
+            o[2 % B] = __builtin_amdgcn_perm(P[3], P[2], 0x06050402u);
+        } else if (B == 2) {
+            o[0] = (P[0] & 0xffffu) | (P[1] << 16);
+            o[1 % B] = (P[2] & 0xffffu) | (P[3] << 16);
         } else {
-            for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
+            o[0] = (P[0] & 0xffu) | ((P[1] & 0xffu) << 8) | ((P[2] & 0xffu) << 16) | (P[3] << 24);
+        }
+        u8 *qd = dst + (static_cast<long long>(oy) * h + ox + px0) * B;
+        if (npx == 4 && (reinterpret_cast<uintptr_t>(qd) & 3u) == 0) {
+            uint32_t *q32 = reinterpret_cast<uint32_t *>(qd);
+#pragma unroll
+            for (int k = 0; k < B; ++k) q32[k] = o[k];
+        } else {
+            for (int k = 0; k < npx * B; ++k) qd[k] = static_cast<u8>(o[k >> 2] >> (8 * (k & 3)));
         }
     }
 }
