@@ -509,6 +509,10 @@ int extract_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, 
                    hipStream_t st) {
     const int in_row = w * b, out_row = ow * b, lb = left * b;
     const int dword = (in_row % 4 == 0) && (out_row % 4 == 0) && (lb % 4 == 0) && aligned4(in) && aligned4(out);
+    // any other alignment: an embed whose window lies inside the image (every byte from the
+    // interior path, 16 bytes per lane) rather than one byte per thread
+    if (!dword && (b != 4 || (aligned4(in) && aligned4(out))))
+        return embed_launch(in, out, n, w, h, b, -left, -top, ow, oh, MIPX_EXTEND_COPY, nullptr, nullptr, st);
     dim3 grid(std::max(1, std::min((out_row / (dword ? 4 : 1) + 255) / 256, 64)), oh, n);
     hipLaunchKernelGGL(k_extract_rows, grid, dim3(256), 0, st, in, out, in_row, out_row, lb, top, img_bytes(w, h, b),
                        img_bytes(ow, oh, b), dword);

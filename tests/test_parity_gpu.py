@@ -174,6 +174,17 @@ def test_extract_rot_flip(gpu, oracle, rng, b):
     assert_same(r, img, "rot90^4 == identity")
 
 
+@pytest.mark.parametrize("b", [1, 2, 3, 4])
+def test_extract_batches_any_alignment(gpu, oracle, rng, b):
+    """Extract over batches of odd-size images (later images start unaligned) and odd
+    windows: the dword copy, the embed-interior path and the per-pixel remap."""
+    for h, w, left, top, ow, oh in ((37, 53, 5, 7, 31, 20), (40, 64, 4, 3, 32, 16), (29, 301, 101, 2, 157, 25)):
+        imgs = np.stack([rand_img(rng, h, w, b) for _ in range(3)])
+        got = gpu.run_op("extract", imgs, left=left, top=top, width=ow, height=oh)
+        for i in range(3):
+            assert_same(got[i], oracle.extract(imgs[i], left, top, ow, oh), f"extract {h}x{w}x{b} img{i}")
+
+
 @pytest.mark.parametrize("h,w,b", [(33, 65, 3), (64, 96, 4), (100, 31, 1), (70, 71, 2), (128, 256, 4)])
 def test_rot_tiles_and_aligned_extract(gpu, oracle, rng, h, w, b):
     img = rand_img(rng, h, w, b)
