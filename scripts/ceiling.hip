@@ -63,6 +63,40 @@ __global__ void __launch_bounds__(256) rd4wr1_x4u2(const uint4 *p, uint4 *q, siz
     }
 }
 
+// 4:1 with dword accesses: lane reads one dword from each of 4 rows (each row
+// contiguous across the wave, 256 B per instruction) and writes one dword
+__global__ void __launch_bounds__(256) rd4wr1_dw(const uint32_t *p, uint32_t *q, size_t nout) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * 256;
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < nout; i += stride) {
+        const uint32_t *s = p + 4 * (i - i % 256) + i % 256;
+        q[i] = s[0] ^ s[256] ^ s[512] ^ s[768];
+    }
+}
+// the same with 8 rows per lane in flight (2 outputs)
+__global__ void __launch_bounds__(256) rd4wr1_dw2(const uint32_t *p, uint32_t *q, size_t nout) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * 512;
+    for (size_t i0 = blockIdx.x * 512 + threadIdx.x; i0 < nout; i0 += stride) {
+        const size_t i1 = i0 + 256;
+        const uint32_t *s0 = p + 4 * (i0 - i0 % 256) + i0 % 256, *s1 = p + 4 * (i1 - i1 % 256) + i1 % 256;
+        const uint32_t a = s0[0] ^ s0[256] ^ s0[512] ^ s0[768];
+        const uint32_t b = i1 < nout ? (s1[0] ^ s1[256] ^ s1[512] ^ s1[768]) : 0u;
+        q[i0] = a;
+        if (i1 < nout) q[i1] = b;
+    }
+}
+
+// C2's access pattern as a short-lived stream: one output dword (of a 1920x1080x3
+// row) per lane from a 2 x 2 block of dwords in two rows of the 3840x2160x3 input
+__global__ void __launch_bounds__(256) box2x2_dw(const uint32_t *p, uint32_t *q, long long nout) {
+    const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= nout) return;
+    constexpr int OPW = 1440, OPH = 1080, IPW = 2880;  // dwords per output / input row
+    const long long img = i / (static_cast<long long>(OPW) * OPH);
+    const int rem = static_cast<int>(i - img * OPW * OPH), y = rem / OPW, x = rem - y * OPW;
+    const uint32_t *s = p + img * (static_cast<long long>(IPW) * 2 * OPH) + static_cast<long long>(2 * y) * IPW + 2 * x;
+    q[i] = s[0] ^ s[1] ^ s[IPW] ^ s[IPW + 1];
+}
+
 // k_reduce2x2 geometry, memory only: tile = (img, band, strip), strip fastest
 __global__ void __launch_bounds__(256) rows_dw(const uint8_t *in, uint8_t *out, int w, int h, int n_strips,
                                                int n_bands, long long in_img, long long out_img) {
@@ -140,6 +174,20 @@ int main() {
         printf("{\"kernel\": \"rd4wr1_x4u2\", \"grid\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", grid, ms, 5.0 * nout16 * 16 / ms / 1e6);
         ms = time_it([&] { rd4wr1_x4u2<true><<<grid, 256>>>((const uint4 *)in, (uint4 *)out, nout16); });
         printf("{\"kernel\": \"rd4wr1_x4u2_nt\", \"grid\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", grid, ms, 5.0 * nout16 * 16 / ms / 1e6);
+    }
+    for (int grid : {65536, 262144, 1048576}) {
+        const size_t nout = (OUT / 4) / 256 * 256;
+        float ms = time_it([&] { rd4wr1_dw<<<grid, 256>>>((const uint32_t *)in, (uint32_t *)out, nout); });
+        printf("{\"kernel\": \"rd4wr1_dw\", \"grid\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", grid, ms, 5.0 * nout * 4 / ms / 1e6);
+        ms = time_it([&] { rd4wr1_dw2<<<grid / 2, 256>>>((const uint32_t *)in, (uint32_t *)out, nout); });
+        printf("{\"kernel\": \"rd4wr1_dw2\", \"grid\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", grid / 2, ms, 5.0 * nout * 4 / ms / 1e6);
+    }
+    {
+        const long long nout = static_cast<long long>(n) * 1440 * 1080;
+        const float ms = time_it([&] {
+            box2x2_dw<<<static_cast<unsigned>((nout + 255) / 256), 256>>>((const uint32_t *)in, (uint32_t *)out, nout);
+        });
+        printf("{\"kernel\": \"box2x2_dw\", \"ms\": %.4f, \"GBps\": %.1f}\n", ms, (IN + OUT) / ms / 1e6);
     }
     {
         const int n_strips = (W / 2 + 159) / 160, n_bands = (H / 2 + 23) / 24;
