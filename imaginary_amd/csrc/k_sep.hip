@@ -66,20 +66,6 @@ __device__ __forceinline__ uint32_t pack_pair(float c0, float c1) {
     return (static_cast<uint32_t>(static_cast<int>(c0)) & 0xffffu) | (static_cast<uint32_t>(static_cast<int>(c1)) << 16);
 }
 
-// Conv masks (vips_gaussmat integer: every coefficient rint(20 * e^-x^2/2s^2),
-// 0..20) fit packed u8, so 4 taps x 4 bytes are 8 v_perm_b32 (4 x 4 byte
-// transpose) + 4 v_dot4_u32_u8, exact integer sums, instead of 16 byte
-// conversions + 16 FMAs.  in[j] byte c -> out[c] byte j.
-__device__ __forceinline__ void transpose4x4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t t[4]) {
-    const uint32_t ab_lo = __builtin_amdgcn_perm(b, a, 0x05010400u);  // a0 b0 a1 b1
-    const uint32_t ab_hi = __builtin_amdgcn_perm(b, a, 0x07030602u);  // a2 b2 a3 b3
-    const uint32_t cd_lo = __builtin_amdgcn_perm(d, c, 0x05010400u);
-    const uint32_t cd_hi = __builtin_amdgcn_perm(d, c, 0x07030602u);
-    t[0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);  // a0 b0 c0 d0
-    t[1] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);
-    t[2] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
-    t[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
-}
 // taps 4q .. 4q+3 of a 1-phase table as packed u8 (0 past the last tap)
 __device__ __forceinline__ uint32_t pack_taps(const float *c, int taps, int q) {
     uint32_t w = 0;

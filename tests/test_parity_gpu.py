@@ -225,11 +225,28 @@ def test_gaussblur_dot4_and_float_paths(gpu, oracle, rng, monkeypatch, dot, sigm
     (MIPX_SEP_DOT=0) on every band count, odd widths and unaligned batches
     (3 images of an odd byte size: the DMA=0 vertical staging)."""
     monkeypatch.setenv("MIPX_SEP_DOT", dot)
+    monkeypatch.setenv("MIPX_BLUR2D", "0")  # the two separable passes, not the fused kernel
     for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
         got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
         for i in range(3):
             assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur {sigma} {h}x{w}x{b} dot={dot} img{i}")
+
+
+@pytest.mark.parametrize("rows", ["4", "64"])
+@pytest.mark.parametrize("sigma", [0.3, 1.0, 2.2, 5.0, 7.5])
+def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma):
+    """Fused gaussblur (k_blur2d: horizontal pass into a per-lane register ring,
+    vertical pass from it) for masks up to 27 taps: every band count, odd sizes,
+    unaligned batches (odd image byte sizes), several column blocks, images
+    shorter than the mask, band heights of 4 and 64 rows (MIPX_BLUR2D_ROWS)."""
+    monkeypatch.setenv("MIPX_BLUR2D_ROWS", rows)
+    for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3), (9, 600, 4), (130, 513, 3),
+                    (3, 5, 4), (70, 257, 2)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
+        got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
+        for i in range(3):
+            assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur2d {sigma} {h}x{w}x{b} rows={rows} img{i}")
 
 
 @pytest.mark.parametrize("hdma", ["16", "4"])
@@ -239,6 +256,7 @@ def test_hpass_dma_widths(gpu, oracle, rng, monkeypatch, hdma):
     shrinks, blur, and a whole reduce -> extract plan (window origin off the
     16-byte grid), each against the oracle, with both image edges inside a block."""
     monkeypatch.setenv("MIPX_HP_DMA", hdma)
+    monkeypatch.setenv("MIPX_BLUR2D", "0")
     for h, w, s in ((23, 256, 1.3333333333333333), (19, 300, 2.5), (11, 1028, 1.1), (9, 64, 3.0)):
         imgs = np.stack([rand_img(rng, h, w, 4), smooth_img(rng, h, w, 4)])
         got = gpu.run_op("reduceh", imgs, hshrink=s)
@@ -278,6 +296,7 @@ def test_hpass_raw_repack_paths(gpu, oracle, rng, monkeypatch, repack):
     repack them per pixel: 4 pixels per item with v_alignbyte / v_perm (default) or
     one per item (MIPX_HP_REPACK=0); every band count, both image edges in a block."""
     monkeypatch.setenv("MIPX_HP_REPACK", repack)
+    monkeypatch.setenv("MIPX_BLUR2D", "0")
     for h, w, b in ((9, 301, 3), (7, 517, 1), (6, 259, 2), (5, 263, 4), (11, 37, 3)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
         for s in (1.6, 2.9):
