@@ -414,6 +414,8 @@ int reduce_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     if (vs > 1.0 && hs > 1.0) {
         const int fe = reduce_fused_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
         if (fe != MIPX_EUNSUPPORTED) return fe;
+        const int f2 = reduce2d_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
+        if (f2 != MIPX_EUNSUPPORTED) return f2;
         const size_t need = align_up(static_cast<size_t>(n) * w * oh * b);
         if (!ws || ws_bytes < need) return MIPX_EINVAL;
         u8 *tmp = static_cast<u8 *>(ws);

@@ -911,6 +911,171 @@ __global__ void __launch_bounds__(256) k_reduce_fused(FusedArgs a) {
     }
 }
 
+// ===========================================================================
+// k_reduce2d<B>: reducev -> reduceh in one launch for any shrink pair, sized for
+// large images.  A block = up to 256 output pixels (one per lane) x kr output
+// rows of one image.  The input rows it needs over the block's column span are
+// DMA'd to LDS (dwords from each row's aligned-down start, any alignment); the
+// vertical pass runs on dword lanes (channel agnostic, int16 v_dot2 on byte
+// pairs, integer (sum + 2048) >> 12) into kr rounded uchar rows kept in LDS as
+// raw bytes; the horizontal pass reads each pixel's bytes back with
+// v_alignbyte and sums its <= 16 taps with v_dot2.  The intermediate never
+// reaches HBM (libvips materialises it; the values are the same).
+// ===========================================================================
+constexpr int kR2MaxTaps = 16;   // horizontal taps held per lane
+
+struct R2DArgs {
+    const u8 *in;
+    u8 *out;
+    int w, h, in_pitch;
+    long long in_img, out_img;
+    int ox0, oy0, ow, oh;        // output window (op-output coordinates) and its size
+    int bw, kr;                  // output pixels / rows per block
+    int x_blocks, y_blocks;
+    int raw_stride;              // LDS dwords per staged input row (multiple of 64)
+    int mid_stride;              // LDS dwords per intermediate row
+    int lrows;                   // staged input rows capacity (+1 for the odd tap pair)
+    SepTaps tv, thz;
+};
+
+template <int B>
+__global__ void __launch_bounds__(256) k_reduce2d(R2DArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t r2sm[];
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int yb = rest % a.y_blocks;
+    const int img = rest / a.y_blocks;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tv = a.tv.taps, thz = a.thz.taps;
+    const int tp2 = (tv + 1) >> 1;
+    const int x0 = xb * a.bw, y0 = yb * a.kr;
+    const int nx = min(a.bw, a.ow - x0), ny = min(a.kr, a.oh - y0);
+    int lo, hi, r_lo, r_last, ph;
+    sep_position(a.thz, a.ox0 + x0, &lo, &ph);
+    sep_position(a.thz, a.ox0 + x0 + nx - 1, &hi, &ph);
+    hi += thz - 1;
+    sep_position(a.tv, a.oy0 + y0, &r_lo, &ph);
+    sep_position(a.tv, a.oy0 + y0 + ny - 1, &r_last, &ph);
+    const int L = r_last + tv - r_lo;
+    const int cl = max(lo, 0), ch = min(hi, a.w - 1);   // intermediate columns actually computed
+    const int ncol = ch - cl + 1;
+    const int nd = (B * ncol + 3) >> 2;                 // intermediate dwords per row
+    uint32_t *raw = r2sm;                                // lrows x raw_stride
+    uint32_t *mid = raw + a.lrows * a.raw_stride;        // kr x mid_stride
+    uint32_t *cpv = mid + a.kr * a.mid_stride;           // kr x tp2 packed int16 tap pairs
+    int *vso = reinterpret_cast<int *>(cpv + a.kr * tp2);  // kr start rows
+    int *rsk = vso + a.kr;                                 // lrows byte skews
+    // ---- DMA the input rows: dwords from each row's aligned-down start ----
+    int delta = 0;
+    const u8 *src = a.in + img * a.in_img;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, &delta);
+    const int ndl = nd + 1;                              // + the dword a skewed row spills into
+    const int chunks = (ndl + 63) >> 6;
+    {
+        int l = 0, q = wave;
+        while (q >= chunks) q -= chunks, ++l;
+        while (l < L) {
+            const int r = clampi(r_lo + l, 0, a.h - 1);
+            const int a4 = static_cast<int>(delta + static_cast<long long>(r) * a.in_pitch + B * cl) & ~3;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * a.raw_stride + q * 64), 4,
+                                                     4 * (q * 64 + lane), a4, 0, 0);
+            q += 4;
+            while (q >= chunks) q -= chunks, ++l;
+        }
+    }
+    for (int i = tid; i < L + 1; i += 256) {
+        const int r = clampi(r_lo + min(i, L - 1), 0, a.h - 1);
+        rsk[i] = static_cast<int>(delta + static_cast<long long>(r) * a.in_pitch + B * cl) & 3;
+    }
+    for (int i = tid; i < ny * tp2; i += 256) {
+        const int k = i / tp2, m = i - k * tp2;
+        int s2;
+        sep_position(a.tv, a.oy0 + y0 + k, &s2, &ph);
+        const float *c = a.tv.tab + ph * tv;
+        cpv[i] = pack_pair(c[2 * m], 2 * m + 1 < tv ? c[2 * m + 1] : 0.f);
+    }
+    if (tid < ny) {
+        int s2;
+        sep_position(a.tv, a.oy0 + y0 + tid, &s2, &ph);
+        vso[tid] = s2 - r_lo;
+    }
+    // this lane's horizontal taps (int16 pairs) and the byte offsets of its pixels
+    const int xi = tid;
+    int xs = 0, xph = 0;
+    sep_position(a.thz, a.ox0 + x0 + min(xi, nx - 1), &xs, &xph);
+    uint32_t cp[kR2MaxTaps / 2];
+    int boff[kR2MaxTaps];
+    {
+        const float *c = a.thz.tab + xph * thz;
+#pragma unroll
+        for (int m = 0; m < kR2MaxTaps / 2; ++m)
+            cp[m] = pack_pair(2 * m < thz ? c[2 * m] : 0.f, 2 * m + 1 < thz ? c[2 * m + 1] : 0.f);
+#pragma unroll
+        for (int i = 0; i < kR2MaxTaps; ++i) boff[i] = B * (clampi(xs + min(i, thz - 1), 0, a.w - 1) - cl);
+    }
+    __syncthreads();
+    // ---- vertical pass: ny intermediate rows x nd dwords ----
+    for (int k = 0; k < ny; ++k) {
+        const int s0 = vso[k];
+        const uint32_t *ck = cpv + k * tp2;
+        for (int d = tid; d < nd; d += 256) {
+            int acc[4] = {0, 0, 0, 0};
+            for (int m = 0; m < tp2; ++m) {
+                const int l0 = s0 + 2 * m;
+                const uint32_t *p0 = raw + l0 * a.raw_stride + d;
+                const uint32_t v0 = __builtin_amdgcn_alignbyte(p0[1], p0[0], rsk[l0]);
+                const uint32_t v1 = __builtin_amdgcn_alignbyte(p0[a.raw_stride + 1], p0[a.raw_stride], rsk[l0 + 1]);
+                const uint32_t cw = ck[m];
+#pragma unroll
+                for (int z = 0; z < 4; ++z) acc[z] = dot2_byte(v0, v1, z, cw, acc[z]);
+            }
+            uint32_t o = 0;
+#pragma unroll
+            for (int z = 0; z < 4; ++z) o |= fixed_round_i(acc[z]) << (8 * z);
+            mid[k * a.mid_stride + d] = o;
+        }
+    }
+    __syncthreads();
+    // ---- horizontal pass: lane = output column x0 + xi ----
+    if (xi >= nx) return;
+    u8 *q = a.out + img * a.out_img + (static_cast<long long>(y0) * a.ow + x0 + xi) * B;
+    for (int k = 0; k < ny; ++k) {
+        const uint32_t *mr = mid + k * a.mid_stride;
+        int acc[B];
+#pragma unroll
+        for (int z = 0; z < B; ++z) acc[z] = 0;
+#pragma unroll
+        for (int m = 0; m < kR2MaxTaps / 2; ++m) {
+            if (2 * m < thz) {
+                uint32_t v[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int bo = boff[2 * m + u];
+                    if (B == 4) {
+                        v[u] = mr[bo >> 2];
+                    } else {
+                        v[u] = __builtin_amdgcn_alignbyte(mr[(bo >> 2) + 1], mr[bo >> 2], bo & 3);
+                    }
+                }
+#pragma unroll
+                for (int z = 0; z < B; ++z) acc[z] = dot2_byte(v[0], v[1], z, cp[m], acc[z]);
+            }
+        }
+        u8 *p = q + static_cast<long long>(k) * a.ow * B;
+        if (B == 4 && (reinterpret_cast<uintptr_t>(p) & 3u) == 0) {
+            uint32_t o = 0;
+#pragma unroll
+            for (int z = 0; z < B; ++z) o |= fixed_round_i(acc[z]) << (8 * z);
+            *reinterpret_cast<uint32_t *>(p) = o;
+        } else {
+#pragma unroll
+            for (int z = 0; z < B; ++z) p[z] = static_cast<u8>(fixed_round_i(acc[z]));
+        }
+    }
+}
+
 bool aligned4(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
 
 SepTaps make_taps(const SepSpec &s) {
@@ -1141,6 +1306,68 @@ int reduce_fused_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
     MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduce_fused<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds,
                                               st, a));
     return launch_check("k_reduce_fused");
+}
+
+// Fused reducev -> reduceh of the output window for large images (k_reduce2d);
+// MIPX_EUNSUPPORTED when a mask or the tile does not fit (caller runs two
+// passes).  Off unless MIPX_REDUCE2D=1: it loses to the two DMA-staged passes
+// (C3's 1024^2 RGBA / 1.333: 2.90 vs 1.95 ms, 1080p RGB / 2.47: 0.68 vs 0.33 ms,
+// profiles/r01/v17/ab_reduce2d_*.log); occupancy (3 workgroups per CU at 45 KB of
+// LDS) and the serial stage -> vertical -> horizontal chain per block bound it.
+// MIPX_REDUCE2D_ROWS sets rows per block.
+int reduce2d_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
+                    int ow, int oh, hipStream_t st) {
+    const char *ef = std::getenv("MIPX_REDUCE2D");
+    if (!(ef && *ef == '1')) return MIPX_EUNSUPPORTED;
+    SepSpec sh, sv;
+    if (!sep_spec_reduce(hs, &sh) || !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
+    if (sh.taps > kR2MaxTaps || sv.taps > 48) return MIPX_EUNSUPPORTED;
+    R2DArgs a{};
+    a.in = in;
+    a.out = out;
+    a.w = w;
+    a.h = h;
+    a.in_pitch = w * b;
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = img_bytes(ow, oh, b);
+    if (a.in_img >= 0x7fffffffLL - 16) return MIPX_EUNSUPPORTED;
+    a.ox0 = ox0;
+    a.oy0 = oy0;
+    a.ow = ow;
+    a.oh = oh;
+    a.tv = make_taps(sv);
+    a.thz = make_taps(sh);
+    // column span of a block: <= 2 KiB of input bytes, <= 256 output pixels
+    constexpr int kSpanBytes = 2048;
+    int bw = static_cast<int>(std::floor((kSpanBytes / b - sh.taps - 3) / hs)) + 1;
+    bw = std::max(1, std::min(bw, 256));
+    const int xblk = (ow + bw - 1) / bw;
+    a.bw = (ow + xblk - 1) / xblk;
+    a.x_blocks = (ow + a.bw - 1) / a.bw;
+    const int span_px = static_cast<int>(std::ceil((a.bw - 1) * hs)) + sh.taps + 2;
+    const int nd = (span_px * b + 3) / 4;
+    a.mid_stride = nd + 2;
+    a.raw_stride = ((nd + 1 + 63) / 64) * 64;
+    const int tp2 = (sv.taps + 1) / 2;
+    auto lrows_for = [&](int kr) { return static_cast<int>(std::ceil((kr - 1) * vs)) + sv.taps + 3; };
+    auto lds_for = [&](int kr) {
+        return (static_cast<size_t>(lrows_for(kr)) * a.raw_stride + static_cast<size_t>(kr) * a.mid_stride +
+                static_cast<size_t>(kr) * (tp2 + 1) + lrows_for(kr) + 1) * 4;
+    };
+    const char *er = std::getenv("MIPX_REDUCE2D_ROWS");
+    int kr = (er && *er) ? std::max(1, std::atoi(er)) : 8;
+    constexpr size_t kBudget = 64 * 1024;
+    while (kr > 1 && lds_for(kr) > kBudget) --kr;
+    if (lds_for(kr) > kBudget) return MIPX_EUNSUPPORTED;
+    a.kr = std::min(kr, oh);
+    a.lrows = lrows_for(a.kr);
+    a.y_blocks = (oh + a.kr - 1) / a.kr;
+    const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
+    if (!grid_ok(blocks)) return MIPX_EINVAL;
+    const size_t lds = lds_for(a.kr);
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduce2d<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds,
+                                              st, a));
+    return launch_check("k_reduce2d");
 }
 
 }  // namespace mipx

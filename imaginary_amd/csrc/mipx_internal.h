@@ -82,6 +82,8 @@ bool sep_spec_reduce(double shrink, SepSpec *s);
 bool sep_spec_gauss(double sigma, double min_ampl, SepSpec *s);
 int vpass_launch(const uint8_t *in, uint8_t *out, int n, const SepSpec &spec, const SepWindow &w, hipStream_t st);
 int hpass_launch(const uint8_t *in, uint8_t *out, int n, const SepSpec &spec, const SepWindow &w, hipStream_t st);
+int reduce2d_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
+                    int oy0, int ow, int oh, hipStream_t st);
 int reduce_fused_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                         int oy0, int ow, int oh, hipStream_t st);
 

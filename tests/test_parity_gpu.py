@@ -87,8 +87,10 @@ def test_reduce2x2_variants_exact(gpu, oracle, rng, var, monkeypatch):
 @pytest.mark.parametrize("fused", ["0", "1"])
 def test_reduce_fused_and_two_pass_paths(gpu, oracle, rng, fused, monkeypatch):
     """Both generic reduce paths (one fused launch / two DMA-staged passes) on the
-    same shapes, including output windows (reduce -> extract plans)."""
+    same shapes, including output windows (reduce -> extract plans).  "0" turns
+    the small-image fused kernel off (k_reduce2d is off unless asked for)."""
     monkeypatch.setenv("MIPX_FUSED_REDUCE", fused)
+    monkeypatch.setenv("MIPX_REDUCE2D", "0")
     for h, w, b, hs, vs in ((240, 427, 3, 1.4233, 1.4233), (273, 364, 3, 1.421875, 1.06640625),
                             (97, 130, 4, 1.3333333333333333, 1.3333333333333333), (45, 61, 1, 2.9, 1.7),
                             (60, 90, 2, 1.05, 3.3), (300, 200, 3, 2.4666666666666666, 2.4666666666666666)):
@@ -288,6 +290,33 @@ def test_reduce_passes_dot2_and_float_paths(gpu, oracle, rng, monkeypatch, dot, 
         for i in range(3):
             assert_same(gv[i], oracle.reducev(imgs[i], s), f"reducev {s} {h}x{w}x{b} dot={dot}")
             assert_same(gh[i], oracle.reduceh(imgs[i], s), f"reduceh {s} {h}x{w}x{b} dot={dot}")
+
+
+@pytest.mark.parametrize("rows", ["1", "8", "13"])
+def test_reduce2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows):
+    """Fused generic reduce (k_reduce2d, an A/B variant behind MIPX_REDUCE2D=1:
+    DMA-staged rows, dot2 vertical pass into LDS, dot2 horizontal pass from it) on every band count, odd sizes, unaligned
+    batches, several column blocks, unequal shrinks and masks up to 16 horizontal
+    taps; the small-image fused kernel is switched off so this path runs."""
+    monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
+    monkeypatch.setenv("MIPX_REDUCE2D", "1")  # A/B variant, off by default
+    monkeypatch.setenv("MIPX_REDUCE2D_ROWS", rows)
+    for h, w, b, hs, vs in ((41, 57, 1, 1.1, 1.1), (37, 43, 2, 1.3333333333333333, 1.6), (64, 90, 3, 1.6, 1.6),
+                            (50, 128, 4, 2.5, 1.3333333333333333), (31, 17, 3, 1.3, 2.9), (40, 1100, 3, 1.3333333333333333, 1.4),
+                            (30, 700, 4, 1.75, 3.7), (23, 2100, 1, 2.4, 1.05), (19, 301, 2, 1.01, 6.5)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
+        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+        for i in range(3):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"reduce2d {h}x{w}x{b} {hs}x{vs} rows={rows} img{i}")
+    # a reduce -> extract window (C3's crop) through a whole plan
+    opts = dict(width=300, height=200, crop=1)
+    p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(640, 520, 4, "png"))
+    e, rp = oracle.plan(opts, dict(w=640, h=520, bands=4, type=3))
+    assert e == 0
+    imgs = rng.integers(0, 256, (2, 520, 640, 4), dtype=np.uint8)
+    got = gpu.execute(p, imgs)
+    for i in range(2):
+        assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce2d window rows={rows}")
 
 
 @pytest.mark.parametrize("repack", ["1", "0"])
