@@ -52,6 +52,7 @@ struct Blur2DArgs {
     int pad, padg;               // taps / 2, and pad rounded up to a whole group
     int out_al4;                 // output rows start dword aligned (B == 4 dword stores)
     uint32_t rnd, mag;           // convi rounding: (acc + rnd) / scale == mulhi(acc + rnd, mag)
+    float inv, fofs;             // the same in fp32: floor(acc * inv + fofs), fofs = (rnd + 0.5) * inv
     uint32_t cph[4][kB2MaxQ];    // tap set p: group j, byte b holds tap 4j + b - p
 };
 
@@ -139,8 +140,31 @@ __device__ __forceinline__ uint4 b2_finish(long long row, int w, int x, const B2
 __device__ __forceinline__ uint32_t b2_round(uint32_t acc, const Blur2DArgs &a) {
     return __umulhi(acc + a.rnd, a.mag);
 }
+// The same in three full-rate fp32 ops (v_mul_hi_u32 is quarter rate): every
+// (acc + rnd + 0.5) / scale sits at least 0.5 / scale from an integer, far above
+// the error of one fma and one rounded constant (< 2^-15 below 256), so the floor
+// is exact; v_cvt_pk_u8_f32 then packs the exact integer into byte C.
+template <int C>
+__device__ __forceinline__ uint32_t b2_pack_f(uint32_t acc, const Blur2DArgs &a, uint32_t prev) {
+    const float v = floorf(__builtin_fmaf(static_cast<float>(acc), a.inv, a.fofs));
+    return __builtin_amdgcn_cvt_pk_u8_f32(v, C, prev);
+}
+template <int B, bool FR>
+__device__ __forceinline__ uint32_t b2_pack(const uint32_t *acc, const Blur2DArgs &a) {
+    uint32_t m = 0;
+    if (FR) {
+        m = b2_pack_f<0>(acc[0], a, 0u);
+        if (B > 1) m = b2_pack_f<1>(acc[1], a, m);
+        if (B > 2) m = b2_pack_f<2>(acc[2], a, m);
+        if (B > 3) m = b2_pack_f<3>(acc[3], a, m);
+    } else {
+#pragma unroll
+        for (int c = 0; c < B; ++c) m |= b2_round(acc[c], a) << (8 * c);
+    }
+    return m;
+}
 
-template <int B, int NQ>
+template <int B, int NQ, bool FR>
 __global__ void __launch_bounds__(256) k_blur2d(Blur2DArgs a) {
     __shared__ uint4 stg[4][kB2MaxG];
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
@@ -220,10 +244,7 @@ __global__ void __launch_bounds__(256) k_blur2d(Blur2DArgs a) {
 #pragma unroll
                 for (int c = 0; c < B; ++c) acc[c] = __builtin_amdgcn_udot4(vc[c], hc[j], acc[c], false);
             }
-            uint32_t m = 0;
-#pragma unroll
-            for (int c = 0; c < B; ++c) m |= b2_round(acc[c], a) << (8 * c);
-            mid[r] = m;
+            mid[r] = b2_pack<B, FR>(acc, a);
         }
         __syncthreads();  // stg is rewritten next iteration
         // ---- the quad joins the ring: one dword per channel, 4 rows ----
@@ -252,14 +273,12 @@ __global__ void __launch_bounds__(256) k_blur2d(Blur2DArgs a) {
 #pragma unroll
                 for (int c = 0; c < B; ++c) acc[c] = __builtin_amdgcn_udot4(ring[j][c], a.cph[k][j], acc[c], false);
             u8 *p = dst + static_cast<long long>(y) * a.w * B;
+            const uint32_t ov = b2_pack<B, FR>(acc, a);
             if (B == 4 && a.out_al4) {
-                uint32_t ov = 0;
-#pragma unroll
-                for (int c = 0; c < B; ++c) ov |= b2_round(acc[c], a) << (8 * c);
                 *reinterpret_cast<uint32_t *>(p) = ov;
             } else {
 #pragma unroll
-                for (int c = 0; c < B; ++c) p[c] = static_cast<u8>(b2_round(acc[c], a));
+                for (int c = 0; c < B; ++c) p[c] = static_cast<u8>(ov >> (8 * c));
             }
         }
     }
@@ -303,6 +322,10 @@ int blur2d_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, i
     a.out_al4 = (reinterpret_cast<uintptr_t>(out) & 3u) == 0;
     a.rnd = static_cast<uint32_t>((scale + 1) / 2);
     a.mag = static_cast<uint32_t>(((1ULL << 32) + scale - 1) / scale);
+    a.inv = 1.0f / static_cast<float>(scale);
+    a.fofs = (static_cast<float>(a.rnd) + 0.5f) * a.inv;
+    const char *efr = std::getenv("MIPX_BLUR2D_FROUND");
+    const bool fr = efr && *efr == '1';  // fp32 rounding: 2-3 % slower (v17/ab_blur2d_fround_*.log)
     for (int p = 0; p < 4; ++p)
         for (int j = 0; j < kB2MaxQ; ++j) {
             uint32_t v = 0;
@@ -315,7 +338,9 @@ int blur2d_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, i
     const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
-#define MIPX_B2(NQ_) MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_blur2d<B_, NQ_>), grid, blk, 0, st, a))
+#define MIPX_B2(NQ_)                                                                                  \
+    if (fr) { MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_blur2d<B_, NQ_, true>), grid, blk, 0, st, a)) } \
+    else { MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_blur2d<B_, NQ_, false>), grid, blk, 0, st, a)) }
     switch (nq) {
         case 1:
         case 2: MIPX_B2(2) break;

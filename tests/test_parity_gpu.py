@@ -235,20 +235,23 @@ def test_gaussblur_dot4_and_float_paths(gpu, oracle, rng, monkeypatch, dot, sigm
             assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur {sigma} {h}x{w}x{b} dot={dot} img{i}")
 
 
+@pytest.mark.parametrize("fround", ["1", "0"])
 @pytest.mark.parametrize("rows", ["4", "64"])
 @pytest.mark.parametrize("sigma", [0.3, 1.0, 2.2, 5.0, 7.5])
-def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma):
+def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma, fround):
     """Fused gaussblur (k_blur2d: horizontal pass into a per-lane register ring,
     vertical pass from it) for masks up to 27 taps: every band count, odd sizes,
     unaligned batches (odd image byte sizes), several column blocks, images
-    shorter than the mask, band heights of 4 and 64 rows (MIPX_BLUR2D_ROWS)."""
+    shorter than the mask, band heights of 4 and 64 rows (MIPX_BLUR2D_ROWS), integer
+    mul-hi (default) and fp32 rounding (MIPX_BLUR2D_FROUND=1)."""
     monkeypatch.setenv("MIPX_BLUR2D_ROWS", rows)
+    monkeypatch.setenv("MIPX_BLUR2D_FROUND", fround)
     for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3), (9, 600, 4), (130, 513, 3),
                     (3, 5, 4), (70, 257, 2)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
         got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
         for i in range(3):
-            assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur2d {sigma} {h}x{w}x{b} rows={rows} img{i}")
+            assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur2d {sigma} {h}x{w}x{b} rows={rows} fr={fround} img{i}")
 
 
 @pytest.mark.parametrize("hdma", ["16", "4"])
