@@ -60,7 +60,7 @@ def cpu_baseline(args, sample):
                       f"(reducev+reduceh Lanczos3 2x2), {threads} OpenMP threads, {dt:.2f} s wall"}
 
 
-TRAFFIC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "traffic_v16.json")
+TRAFFIC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "traffic_v17.json")
 
 
 def pmc_traffic(kernel_name_hint):
