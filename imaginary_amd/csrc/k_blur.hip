@@ -37,7 +37,7 @@ using namespace dev;
 // for the vertical pass and no HBM intermediate (libvips materialises one; the
 // values are the same).
 // ===========================================================================
-constexpr int kB2MaxQ = 8;               // taps <= 4 * kB2MaxQ - 6
+constexpr int kB2MaxQ = 12;              // taps <= 4 * kB2MaxQ - 6 (sigma <= 12.5 at min_ampl 0.2)
 constexpr int kB2MaxG = 64 + kB2MaxQ + 1;  // staged groups per row
 
 struct Blur2DArgs {
@@ -349,7 +349,11 @@ int blur2d_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, i
         case 5: MIPX_B2(5) break;
         case 6: MIPX_B2(6) break;
         case 7: MIPX_B2(7) break;
-        default: MIPX_B2(8) break;
+        case 8: MIPX_B2(8) break;
+        case 9: MIPX_B2(9) break;
+        case 10: MIPX_B2(10) break;
+        case 11: MIPX_B2(11) break;
+        default: MIPX_B2(12) break;
     }
 #undef MIPX_B2
     return launch_check("k_blur2d");

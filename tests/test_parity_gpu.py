@@ -237,10 +237,10 @@ def test_gaussblur_dot4_and_float_paths(gpu, oracle, rng, monkeypatch, dot, sigm
 
 @pytest.mark.parametrize("fround", ["1", "0"])
 @pytest.mark.parametrize("rows", ["4", "64"])
-@pytest.mark.parametrize("sigma", [0.3, 1.0, 2.2, 5.0, 7.5])
+@pytest.mark.parametrize("sigma", [0.3, 1.0, 2.2, 5.0, 7.5, 9.0, 12.5])
 def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma, fround):
     """Fused gaussblur (k_blur2d: horizontal pass into a per-lane register ring,
-    vertical pass from it) for masks up to 27 taps: every band count, odd sizes,
+    vertical pass from it) for masks up to 45 taps: every band count, odd sizes,
     unaligned batches (odd image byte sizes), several column blocks, images
     shorter than the mask, band heights of 4 and 64 rows (MIPX_BLUR2D_ROWS), integer
     mul-hi (default) and fp32 rounding (MIPX_BLUR2D_FROUND=1)."""
