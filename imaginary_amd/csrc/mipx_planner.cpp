@@ -516,6 +516,13 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
     plan->out_w = pb.w();
     plan->out_h = pb.h();
     plan->out_bands = pb.b();
+    // libvips fails a resample whose output has no pixels ("image has shrunk to nothing"),
+    // e.g. height=4 with force on a 16 px wide image: bimg derives width floor(16 / 92) = 0
+    for (int i = 0; i < plan->n_steps; ++i) {
+        const mipx_step &st = plan->steps[i];
+        if (st.out_w <= 0 || st.out_h <= 0) return MIPX_EINVAL;
+        if (st.op == MIPX_OP_REDUCE && !(std::isfinite(st.d[0]) && std::isfinite(st.d[1]))) return MIPX_EINVAL;
+    }
     return MIPX_OK;
 }
 

@@ -1098,6 +1098,14 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
     plan->out_w = cw;
     plan->out_h = ch;
     plan->out_bands = cb;
+    /* libvips fails a resample whose output has no pixels ("image has shrunk to
+     * nothing", resample/shrinkh.c, reduceh.cpp and the v twins), e.g. height=4 with
+     * force on a 16 px wide image: bimg derives width floor(16 / 92) = 0 */
+    for (int i = 0; i < plan->n_steps; ++i) {
+        const ref_step *s = &plan->steps[i];
+        if (s->out_w <= 0 || s->out_h <= 0) return REF_EINVAL;
+        if (s->op == REF_OP_REDUCE && !(isfinite(s->d[0]) && isfinite(s->d[1]))) return REF_EINVAL;
+    }
     return REF_OK;
 }
 

@@ -202,6 +202,20 @@ def test_extract_out_of_bounds_is_einval():
     assert e.value.code == -1
 
 
+def test_shrunk_to_nothing_is_einval(oracle):
+    """height=4 with force on a 16 x 368 image: bimg derives width floor(16 / 92) = 0,
+    which libvips' resample ops refuse ("image has shrunk to nothing"); both planners
+    return EINVAL (found by the 400-seed whole-plan GPU fuzz, seed 110)."""
+    opts = dict(height=4, force=1)
+    with pytest.raises(ia.MipxError) as e:
+        ia.plan_make(ia.make_opts(**opts), ia.make_input(16, 368, 3, "png"))
+    assert e.value.code == -1
+    e2, _ = oracle.plan(opts, dict(w=16, h=368, bands=3, type=3))
+    assert e2 != 0
+    ok = ia.plan_make(ia.make_opts(height=4, force=1), ia.make_input(160, 368, 3, "png"))
+    assert ok.out_w >= 1 and ok.out_h == 4
+
+
 def test_embed_modes_and_background_mapping(oracle):
     for mode in range(7):
         opts = dict(width=100, height=100, embed=1, extend=mode, background=(10, 20, 30))
