@@ -380,6 +380,7 @@ struct HPassArgs {
     int raw_max;          // LDS dwords per staged raw row (B < 4; incl. 64 of overrun)
     int ntab;             // floats of the tap table staged in LDS (0: taps in registers)
     int repack4;          // raw path: 4-pixel vector repack (MIPX_HP_REPACK=0: one pixel per item)
+    int pack3;            // B = 3: 4 lanes' pixels stored as 3 dwords (MIPX_HP_PACK3=1/0 forces; default: reduce, shrink >= 2)
     SepTaps tp;
 };
 
@@ -390,6 +391,27 @@ __device__ __forceinline__ uint32_t load_px_g(const u8 *p) {
     if (B > 2) v |= static_cast<uint32_t>(p[2]) << 16;
     if (B > 3) v |= static_cast<uint32_t>(p[3]) << 24;
     return v;
+}
+
+// One 3-band output pixel per lane (o: 24 bits). pack3: the 4 lanes of an
+// aligned 4-pixel group exchange neighbours (one ds_bpermute) and store the
+// group's 12 bytes as 3 dwords instead of 12 byte stores; groups that are
+// partial (row end) or not dword aligned fall back to bytes.  j = x & 3 is the
+// lane's slot in its group (x0 is a multiple of 256, so lanes of a group are
+// adjacent lanes of one wave).  Every lane of the wave must call it.
+__device__ __forceinline__ void store_rgb_px(u8 *q, uint32_t o, int j, bool full, bool pack3) {
+    const uint32_t nx = __shfl_down(o, 1, 64);
+    u8 *qg = q - 3 * j;
+    if (pack3 && full && (reinterpret_cast<uintptr_t>(qg) & 3u) == 0) {
+        if (j < 3) {
+            const uint32_t w = j == 0 ? (o | (nx << 24)) : j == 1 ? ((o >> 8) | (nx << 16)) : ((o >> 16) | (nx << 8));
+            *reinterpret_cast<uint32_t *>(qg + 4 * j) = w;
+        }
+    } else {
+        q[0] = static_cast<u8>(o);
+        q[1] = static_cast<u8>(o >> 8);
+        q[2] = static_cast<u8>(o >> 16);
+    }
 }
 
 // DW = 16 / 4 (B = 4, rows 16 / 4 byte aligned): direct-to-LDS dwordx4 / dword
@@ -637,6 +659,10 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
 #pragma unroll
                 for (int z = 0; z < B; ++z) o |= fixed_round_i(iacc[r][z]) << (8 * z);
                 *reinterpret_cast<uint32_t *>(q) = o;
+            } else if (B == 3) {
+                store_rgb_px(q, fixed_round_i(iacc[r][0]) | (fixed_round_i(iacc[r][1 % B]) << 8) |
+                                    (fixed_round_i(iacc[r][2 % B]) << 16),
+                             tid & 3, (x | 3) <= x_last, a.pack3 != 0);
             } else {
 #pragma unroll
                 for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(fixed_round_i(iacc[r][z]));
@@ -708,6 +734,10 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
 #pragma unroll
             for (int z = 0; z < B; ++z) o |= sep_round<MODE>(acc[r][z], a.tp) << (8 * z);
             *reinterpret_cast<uint32_t *>(q) = o;
+        } else if (B == 3) {
+            store_rgb_px(q, sep_round<MODE>(acc[r][0], a.tp) | (sep_round<MODE>(acc[r][1 % B], a.tp) << 8) |
+                                (sep_round<MODE>(acc[r][2 % B], a.tp) << 16),
+                         tid & 3, (x | 3) <= x_last, a.pack3 != 0);
         } else {
 #pragma unroll
             for (int z = 0; z < B; ++z) q[z] = static_cast<u8>(sep_round<MODE>(acc[r][z], a.tp));
@@ -1197,6 +1227,10 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     a.span_max = (static_cast<int>(std::ceil(255 * s)) + a.tp.taps + 2 + 64 + 3) & ~3;  // 16-byte rows
     const char *erp = std::getenv("MIPX_HP_REPACK");
     a.repack4 = !(erp && *erp == '0');
+    const char *ep3 = std::getenv("MIPX_HP_PACK3");
+    // A/B (profiles/r01/v18/pack3_ab.jsonl): packed stores win 7% on reduceh / 2.4 and
+    // lose 3% on / 1.6 and on the two-pass blur, so they are on for shrinks >= 2 only
+    a.pack3 = ep3 && *ep3 ? *ep3 != '0' : (spec.mode == kSepReduce && spec.shrink >= 2.0);
     a.raw_max = (a.span_max * b + 8 + 3) / 4 + 64;
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     const bool dw = b == 4 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0 && aligned4(in);

@@ -340,6 +340,24 @@ def test_hpass_raw_repack_paths(gpu, oracle, rng, monkeypatch, repack):
             assert_same(got[i], oracle.gaussblur(imgs[i], 1.5, 0.2), f"blur {h}x{w}x{b} repack={repack}")
 
 
+@pytest.mark.parametrize("pack3", ["1", "0"])
+def test_hpass_rgb_packed_stores(gpu, oracle, rng, monkeypatch, pack3):
+    """3-band horizontal passes store each aligned 4-pixel group as 3 dwords (lanes
+    exchange neighbours) or per byte (MIPX_HP_PACK3=0); output widths with and without
+    dword-aligned rows, partial groups at the row end, several x blocks per row."""
+    monkeypatch.setenv("MIPX_HP_PACK3", pack3)
+    monkeypatch.setenv("MIPX_BLUR2D", "0")
+    for h, w in ((5, 1280), (4, 1283), (3, 1922), (6, 17), (2, 1041)):
+        imgs = np.stack([rand_img(rng, h, w, 3), smooth_img(rng, h, w, 3)])
+        for s in (1.6, 2.4, 1.0 + 1.0 / 3.0):
+            got = gpu.run_op("reduceh", imgs, hshrink=s)
+            for i in range(2):
+                assert_same(got[i], oracle.reduceh(imgs[i], s), f"reduceh {h}x{w} {s} pack3={pack3}")
+        got = gpu.run_op("gaussblur", imgs, sigma=2.0, min_ampl=0.2)
+        for i in range(2):
+            assert_same(got[i], oracle.gaussblur(imgs[i], 2.0, 0.2), f"blur {h}x{w} pack3={pack3}")
+
+
 # ---------------------------------------------------------------- affine (enlarge) / zoom / flatten / B_W
 @pytest.mark.parametrize("h,w,b,xs,ys,extend", [(30, 40, 3, 2.0, 2.0, 1), (17, 23, 4, 3.004291845493562, 3.004291845493562, 1),
                                               (33, 29, 1, 1.7, 0.8, 1), (20, 20, 3, 2.5, 2.5, 0), (15, 31, 2, 1.3, 4.1, 3),
