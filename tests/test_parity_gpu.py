@@ -197,6 +197,19 @@ def test_rot_tiles_and_aligned_extract(gpu, oracle, rng, h, w, b):
                     oracle.extract(img, left, top, ew, eh), f"extract {left},{top}")
 
 
+@pytest.mark.parametrize("xcd", ["1", "0"])
+def test_rot90_tile_orders(gpu, oracle, rng, monkeypatch, xcd):
+    """The 64x64-tile rotation on its flat grid, XCD-contiguous (default for odd band counts) or x-fastest
+    round robin (MIPX_ROT_XCD=0): a batch of 3 with ragged edge tiles, every band count."""
+    monkeypatch.setenv("MIPX_ROT_XCD", xcd)
+    for h, w, b in ((130, 197, 3), (65, 300, 4), (200, 129, 1), (67, 131, 2)):
+        imgs = np.stack([rand_img(rng, h, w, b) for _ in range(3)])
+        for a in (90, 270):
+            got = gpu.run_op("rot", imgs, angle=a)
+            for i in range(3):
+                assert_same(got[i], oracle.rot(imgs[i], a), f"rot{a} {h}x{w}x{b} img{i} xcd={xcd}")
+
+
 @pytest.mark.parametrize("x4", ["1", "0"])
 def test_shrink_x4_and_dword_kernels(gpu, oracle, rng, monkeypatch, x4):
     """Box shrink: the 16-byte-per-lane kernel (dword-aligned rows, vs <= 257) and
