@@ -237,26 +237,27 @@ __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8
 // LDS writes), so a staged row starts exactly at the tile's first pixel.  Gather:
 // a task builds 4 output pixels from aligned LDS dword reads, packs them into B
 // dwords (v_perm) and stores them as one aligned B-dword write.
-template <int B, bool CW>
 // Flat grid, tiles x-fastest; xcd: blocks dealt so that each XCD walks a
 // contiguous run of tiles (neighbouring tiles share the 128-byte lines that a
-// 3-band tile edge splits, in one L2) instead of round robin.
+// 3-band tile edge splits, in one L2) instead of round robin.  TH: input rows
+// per tile (= contiguous output pixels per output row of the tile).
+template <int B, bool CW, int TH>
 __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
                                                    long long img_bytes_, int tiles_x, int tiles_y, int xcd) {
     constexpr int T = 64;
     constexpr int RS = (T * B + 3) / 4 + 1;  // dwords per staged row (+1: the unaligned pixel read spills)
-    __shared__ uint32_t tile[T * RS];
+    __shared__ uint32_t tile[TH * RS];
     const uint32_t t = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
     const int bx = static_cast<int>(t % tiles_x), rest = static_cast<int>(t / tiles_x);
     const int by = rest % tiles_y, img = rest / tiles_y;
-    const int tx0 = bx * T, ty0 = by * T;  // input tile origin
-    const int tw = min(T, w - tx0), th = min(T, h - ty0);
+    const int tx0 = bx * T, ty0 = by * TH;  // input tile origin
+    const int tw = min(T, w - tx0), th = min(TH, h - ty0);
     int delta = 0;
     const u8 *src = in + img * img_bytes_;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, img_bytes_, &delta);
     const int nd = (tw * B + 3) >> 2;
     {
-        constexpr int kPer = (T * ((T * B + 3) / 4) + 255) / 256;
+        constexpr int kPer = (TH * ((T * B + 3) / 4) + 255) / 256;
         uint32_t v[kPer];
         int slot[kPer];
 #pragma unroll
@@ -482,7 +483,9 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
     if (angle == 180 && img_bytes(w, h, b) < 0x7fffffffLL && h <= 65535)
         return flip_rows_launch(in, out, n, w, h, b, true, true, st);
     if ((angle == 90 || angle == 270) && img_bytes(w, h, b) < 0x7fffffffLL) {
-        const int tx = (w + 63) / 64, ty = (h + 63) / 64;
+        const char *eth = std::getenv("MIPX_ROT_TH");
+        const int th = eth && *eth ? (std::atoi(eth) == 128 ? 128 : 64) : 64;
+        const int tx = (w + 63) / 64, ty = (h + th - 1) / th;
         const long long nblk = static_cast<long long>(tx) * ty * n;
         if (nblk > 0x7fffffffLL) return MIPX_EUNSUPPORTED;
         const dim3 grid(static_cast<unsigned>(nblk));
@@ -491,13 +494,15 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
         // A/B (profiles/r01/v18/rotxcd_ab.jsonl): contiguous runs win 3-8% on 4K RGB, where a
         // 64-pixel tile row (192 B) splits a 128-byte line, and lose 2% on RGBA (whole lines)
         const int xcd = ex && *ex ? (*ex != '0') : ((64 * b) % 128 != 0);
-        if (angle == 90) {
-            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, true>), grid, dim3(256), 0, st, in, out, w, h, ib,
-                                                      tx, ty, xcd));
+#define MIPX_ROT(CW_, TH_)                                                                                     \
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, CW_, TH_>), grid, dim3(256), 0, st, in, out, w, h, ib, \
+                                              tx, ty, xcd))
+        if (th == 128) {
+            if (angle == 90) { MIPX_ROT(true, 128); } else { MIPX_ROT(false, 128); }
         } else {
-            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, false>), grid, dim3(256), 0, st, in, out, w, h, ib,
-                                                      tx, ty, xcd));
+            if (angle == 90) { MIPX_ROT(true, 64); } else { MIPX_ROT(false, 64); }
         }
+#undef MIPX_ROT
         return launch_check("k_rot90_lds");
     }
     if (angle == 180) {

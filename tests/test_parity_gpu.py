@@ -197,12 +197,15 @@ def test_rot_tiles_and_aligned_extract(gpu, oracle, rng, h, w, b):
                     oracle.extract(img, left, top, ew, eh), f"extract {left},{top}")
 
 
+@pytest.mark.parametrize("th", ["64", "128"])
 @pytest.mark.parametrize("xcd", ["1", "0"])
-def test_rot90_tile_orders(gpu, oracle, rng, monkeypatch, xcd):
+def test_rot90_tile_orders(gpu, oracle, rng, monkeypatch, xcd, th):
     """The 64x64-tile rotation on its flat grid, XCD-contiguous (default for odd band counts) or x-fastest
-    round robin (MIPX_ROT_XCD=0): a batch of 3 with ragged edge tiles, every band count."""
+    round robin (MIPX_ROT_XCD=0), 64 or 128 input rows per tile
+    (MIPX_ROT_TH): a batch of 3 with ragged edge tiles, every band count."""
     monkeypatch.setenv("MIPX_ROT_XCD", xcd)
-    for h, w, b in ((130, 197, 3), (65, 300, 4), (200, 129, 1), (67, 131, 2)):
+    monkeypatch.setenv("MIPX_ROT_TH", th)
+    for h, w, b in ((130, 197, 3), (65, 300, 4), (200, 129, 1), (67, 131, 2), (261, 70, 4)):
         imgs = np.stack([rand_img(rng, h, w, b) for _ in range(3)])
         for a in (90, 270):
             got = gpu.run_op("rot", imgs, angle=a)
