@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402  (before libmipx: one HIP runtime)
 
 import imaginary_amd as ia  # noqa: E402
+import workloads  # noqa: E402
 from imaginary_amd._abi import check, lib  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0
@@ -127,13 +128,11 @@ def c3(args, dev, sp, stream):
 
 def c4(args, dev, sp, stream):
     n = args.c4_batch // 2
-    rng = np.random.default_rng(4)
-    wm = rng.integers(0, 256, (128, 128, 4), dtype=np.uint8)
+    wm = workloads.c4_watermark()
     groups = []
-    for (w, h) in ((4000, 3000), (3000, 4000)):
-        for opts in (dict(width=256, height=256, crop=1, gravity=5),      # SmartCrop
-                     dict(width=256, height=256, wm_enable=1, wm_left=16, wm_top=16, wm_opacity=0.5)):
-            p = plan_for(opts, w, h, 3, wm_shape=(128, 128, 4) if opts.get("wm_enable") else None)
+    for (w, h) in workloads.C4_SIZES:
+        for opts in workloads.C4_OPTS:
+            p = plan_for(opts, w, h, 3, wm_shape=workloads.C4_WM_SHAPE if opts.get("wm_enable") else None)
             groups.append((Group(p, n, dev, 4 + len(groups), wm if opts.get("wm_enable") else None), opts))
 
     def run_all():
@@ -150,38 +149,15 @@ def c4(args, dev, sp, stream):
 
 
 def c5_requests(count, seed=5):
-    r = np.random.default_rng(seed)
-    sizes = [(1920, 1080), (3840, 2160), (4000, 3000)]
-    reqs = []
-    for _ in range(count):
-        w, h = sizes[r.integers(0, 3)]
-        u = r.random()
-        if u < 0.40:
-            opts = dict(width=int(r.choice([300, 640, 1280])), embed=1)
-        elif u < 0.60:
-            fw, fh = ia.fit_dimension(w, h, 800, 800)
-            opts = dict(width=fw, height=fh, embed=1)
-        elif u < 0.75:
-            opts = dict(rotate=int(r.choice([90, 180, 270])))
-        elif u < 0.90:
-            s = max(w, h)
-            opts = dict(width=s, height=s, embed=1, extend=int(r.choice([0, 1, 2, 3, 4, 5])))
-        else:
-            opts = dict(sigma=float(r.choice([1.0, 3.0, 5.0])))
-        reqs.append(((w, h), opts))
-    return reqs
+    return workloads.c5_requests(count, seed, ia.fit_dimension)
 
 
 def c5(args, dev, sp, stream):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     reqs = c5_requests(args.c5_requests)[rank::world]  # shard requests across ranks
-    buckets = {}
-    for (w, h), opts in reqs:
-        key = (w, h, json.dumps(opts, sort_keys=True))
-        buckets.setdefault(key, [0, opts, w, h])[0] += 1
     groups = []
-    for (w, h, _), (cnt, opts, _, _) in sorted(buckets.items()):
+    for (w, h), opts, cnt in workloads.c5_groups(reqs):
         groups.append((Group(plan_for(opts, w, h, 3), cnt, dev, 5 + len(groups)), opts))
 
     def run_all():

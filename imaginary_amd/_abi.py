@@ -101,7 +101,8 @@ class MipxImg(C.Structure):
 
 class MipxCfg(C.Structure):
     _fields_ = [("n_devices", C.c_int32), ("device_ids", C.c_int32 * 16),
-                ("staging_bytes", C.c_int64), ("max_batch", C.c_int32), ("batch_wait_us", C.c_int32)]
+                ("staging_bytes", C.c_int64), ("max_batch", C.c_int32), ("batch_wait_us", C.c_int32),
+                ("queues_per_device", C.c_int32)]
 
 
 # name -> (restype, argtypes): every symbol include/mipx.h declares
@@ -110,6 +111,11 @@ _U8P = C.c_void_p
 _I = C.c_int32
 _SIG = {
     "mipx_version": (C.c_char_p, []),
+    "mipx_build_id": (C.c_char_p, []),
+    "mipx_cancel": (C.c_int, [C.c_uint64]),
+    "mipx_queue_count": (C.c_int, []),
+    "mipx_queue_stats": (C.c_int, [C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_int64)]),
     "mipx_abi_version": (C.c_int, []),
     "mipx_plan_chain": (C.c_int, [C.POINTER(MipxPlan), C.c_int32, C.POINTER(MipxPlan)]),
     "mipx_strerror": (C.c_char_p, [C.c_int]),

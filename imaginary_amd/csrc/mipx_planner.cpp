@@ -458,9 +458,16 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
                 pb.geom(o.width, o.height, pb.b());
             }
         } else if (o.top != 0 || o.left != 0 || o.area_width != 0 || o.area_height != 0) {
-            const int aw = o.area_width ? o.area_width : o.width;
-            const int ah = o.area_height ? o.area_height : o.height;
-            if (aw == 0 || ah == 0) return MIPX_EINVAL;
+            // bimg 1.1.9: `if o.AreaWidth == 0 { o.AreaHeight = o.Width }` sets the
+            // height, so a zero AreaWidth stays zero and the extract is an error
+            // (PARITY_ASSUMPTIONS.md #11)
+            int aw = o.area_width, ah = o.area_height;
+            if (aw == 0) ah = o.width;
+            if (ah == 0) ah = o.height;
+            if (aw == 0 || ah == 0) {
+                mipx::set_error("Extract area width/height params are required");
+                return MIPX_EINVAL;
+            }
             if (o.left < 0 || o.top < 0 || o.left + aw > cw || o.top + ah > ch) {
                 mipx::set_error("bad extract area %d,%d %dx%d of %dx%d", o.left, o.top, aw, ah, cw, ch);
                 return MIPX_EINVAL;

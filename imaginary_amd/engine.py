@@ -116,8 +116,9 @@ class Engine:
     """Request path: pinned staging, per-device queues, batching (mipx_submit/mipx_wait)."""
 
     def __init__(self, devices: Optional[Sequence[int]] = None, max_batch: int = 64,
-                 batch_wait_us: int = 0):
+                 batch_wait_us: int = 0, queues_per_device: int = 1):
         cfg = MipxCfg()
+        cfg.queues_per_device = queues_per_device
         if devices:
             cfg.n_devices = len(devices)
             for i, d in enumerate(devices):
@@ -150,6 +151,18 @@ class Engine:
         b, r = C.c_uint64(), C.c_uint64()
         check(lib.mipx_stats(device, C.byref(b), C.byref(r)), "mipx_stats")
         return b.value, r.value
+
+    def queue_stats(self):
+        """[(device, batches, requests, pending_bytes)] for every request queue."""
+        out = []
+        for q in range(lib.mipx_queue_count()):
+            d, b, r, p = C.c_int32(), C.c_uint64(), C.c_uint64(), C.c_int64()
+            check(lib.mipx_queue_stats(q, C.byref(d), C.byref(b), C.byref(r), C.byref(p)), "mipx_queue_stats")
+            out.append((d.value, b.value, r.value, p.value))
+        return out
+
+    def cancel(self, ticket: int):
+        check(lib.mipx_cancel(ticket), "mipx_cancel")
 
     def shutdown(self):
         lib.mipx_shutdown()

@@ -18,7 +18,13 @@
  *    (stride 0 = w * bands).
  *  - mipx_submit copies the input into pinned staging before it returns (cgo
  *    pointer rule: no Go pointer is retained); the output buffer must stay
- *    valid until mipx_wait returns for the ticket.
+ *    valid until mipx_wait returns a FINAL status for the ticket (anything but
+ *    MIPX_ETIMEOUT) or mipx_cancel returns for it.  After MIPX_ETIMEOUT the
+ *    request is still queued or running and will still write the output: wait
+ *    again, or call mipx_cancel before freeing the buffer.
+ *  - Plans are validated before use: every step's out_w/out_h/out_bands must be
+ *    what its op makes from the previous step's geometry (MIPX_EINVAL otherwise),
+ *    and a watermark image must have the watermark step's geometry.
  *  - All mipx_op_* / mipx_execute_dev entry points take DEVICE pointers to a
  *    batch of n equally sized images packed back to back, and a hipStream_t
  *    passed as void* (NULL = the device's default engine stream).  They only
@@ -36,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MIPX_ABI_VERSION 3
+#define MIPX_ABI_VERSION 4
 
 /* ---- error codes ---- */
 #define MIPX_OK 0
@@ -140,10 +146,14 @@ typedef struct mipx_cfg {
     int64_t staging_bytes;          /* pinned staging kept cached for reuse; 0 = default (1 GiB) */
     int32_t max_batch;              /* requests fused into one launch; 0 = default (64) */
     int32_t batch_wait_us;          /* bounded wait for more requests; 0 = none */
+    int32_t queues_per_device;      /* request queues (worker + 3 streams each) per device; 0 = 1 */
 } mipx_cfg;
 
 /* ---- library / devices ---- */
 const char *mipx_version(void);
+/* Build identity: the first 16 hex digits of the SHA-256 of the engine sources this
+ * library was compiled from (imaginary_amd/csrc/ + include/mipx.h; imaginary_amd/srchash.py). */
+const char *mipx_build_id(void);
 int mipx_abi_version(void);
 const char *mipx_strerror(int code);
 const char *mipx_last_error(void);      /* thread-local detail of the last failure */
@@ -169,10 +179,19 @@ int mipx_fit_dimension(int32_t image_w, int32_t image_h, int32_t fit_w, int32_t 
 int mipx_submit(int device, const mipx_plan *plan, const mipx_img *in, const mipx_img *wm,
                 mipx_img *out, uint64_t *ticket);   /* device < 0 = least loaded */
 int mipx_wait(uint64_t ticket, int timeout_ms);      /* timeout < 0 = forever */
+/* Detach a submitted request's output: once this returns, the engine never writes
+ * the caller's output buffer for `ticket` (a copy already under way completes
+ * first) and the ticket is released.  MIPX_ESTALE for an unknown ticket. */
+int mipx_cancel(uint64_t ticket);
 int mipx_process(const mipx_plan *plan, const mipx_img *in, const mipx_img *wm,
                  mipx_img *out);                     /* submit + wait */
-/* Batches launched and requests retired so far on `device` (batching telemetry). */
+/* Batches launched and requests retired so far on `device`, summed over its
+ * queues (batching telemetry).  mipx_submit(device >= 0) picks the least-loaded
+ * queue of that device; device < 0 the least-loaded queue of all. */
 int mipx_stats(int device, uint64_t *batches, uint64_t *requests);
+int mipx_queue_count(void);                           /* 0 before mipx_init */
+int mipx_queue_stats(int queue, int32_t *device, uint64_t *batches, uint64_t *requests,
+                     int64_t *pending_bytes);         /* pending = queued input bytes */
 
 /* ---- device-resident batch API ---- */
 size_t mipx_workspace_bytes(const mipx_plan *plan, int32_t n);

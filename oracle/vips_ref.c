@@ -39,6 +39,8 @@ static struct {
     {"blur_honor_minampl", 0},   /* 1: bimg passes min_ampl (no NULL-terminator bug) */
     {"cast_round", 0},           /* 1: float->uchar cast rounds instead of truncating */
     {"affine_corner", 0},        /* 1: vips_affine corner convention (X = x / scale) */
+    {"webp_sol_bimg", 0},        /* 1: WEBP shrink-on-load loads at 1/shrink, factor kept */
+    {"extract_area_fallback", 0},/* 1: AreaWidth == 0 falls back to Width (no bimg typo) */
     {NULL, 0}};
 
 void ref_set_switch(const char *name, int value) {
@@ -909,11 +911,20 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
             o.height = hh;
         }
     }
+    /* shrinkOnLoad.  JPEG: libjpeg DCT scaling on the 8/4/2 ladder, factor divided.
+     * WEBP [U]: default as JPEG; switch webp_sol_bimg = bimg's vipsShrinkWebp(buf,
+     * input, shrink) as published: loaded at 1/shrink with the calculateShrink
+     * integer and the factor NOT divided (shrinkImage + residual then recompute from
+     * the decoded size). */
     plan->load_shrink = 1;
     if ((in->type == REF_TYPE_JPEG || in->type == REF_TYPE_WEBP) && shrink >= 2) {
-        int sol = shrink >= 8 ? 8 : (shrink >= 4 ? 4 : 2);
-        factor /= sol;
-        plan->load_shrink = sol;
+        if (in->type == REF_TYPE_WEBP && SW("webp_sol_bimg")) {
+            plan->load_shrink = shrink;
+        } else {
+            int sol = shrink >= 8 ? 8 : (shrink >= 4 ? 4 : 2);
+            factor /= sol;
+            plan->load_shrink = sol;
+        }
         if (factor < 1.0) factor = 1.0;
         shrink = (int)floor(factor);
         residual = (double)shrink / factor;
@@ -1045,8 +1056,16 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
                 set_geom(plan, cw, ch, cb);
             }
         } else if (o.top != 0 || o.left != 0 || o.area_width != 0 || o.area_height != 0) {
-            int aw = o.area_width ? o.area_width : o.width;
-            int ah = o.area_height ? o.area_height : o.height;
+            /* bimg 1.1.9 extractOrEmbedImage [U]: `if o.AreaWidth == 0 { o.AreaHeight =
+             * o.Width }` assigns the HEIGHT, so a zero AreaWidth stays zero and the
+             * "Extract area width/height params are required" error follows.  Switch
+             * extract_area_fallback = the evidently intended AreaWidth = Width. */
+            int aw = o.area_width, ah = o.area_height;
+            if (aw == 0) {
+                if (SW("extract_area_fallback")) aw = o.width;
+                else ah = o.width;
+            }
+            if (ah == 0) ah = o.height;
             if (aw == 0 || ah == 0) return REF_EINVAL;
             if (o.left < 0 || o.top < 0 || o.left + aw > cw || o.top + ah > ch) return REF_EINVAL;
             push(plan, REF_OP_EXTRACT, 0, 0, 0);

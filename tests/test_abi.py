@@ -5,6 +5,8 @@ import os
 import re
 import subprocess
 
+import numpy as np
+
 import pytest
 
 from conftest import ROOT
@@ -31,7 +33,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_version_and_errors_without_gpu():
     import imaginary_amd as ia
-    assert ia.lib.mipx_abi_version() == 3
+    assert ia.lib.mipx_abi_version() == 4
     assert b"gfx950" in ia.lib.mipx_version()
     assert ia.lib.mipx_strerror(-2).startswith(b"operation not supported")
 
@@ -123,3 +125,111 @@ def test_code_object_avoids_known_bad_gfx950_fusion(tmp_path):
         seen_dot2 |= "v_dot2_i32_i16" in dis or "v_dot2c_i32_i16" in dis
         assert "v_ashr_pk_u8_i32" not in dis, f"{p.name}: v_ashr_pk_u8_i32 present"
     assert seen_dot2, "disassembly lacks the reduce passes' dot2 (extraction failed?)"
+
+
+def test_build_id_is_the_hash_of_these_sources():
+    """Build provenance: libmipx.so carries the hash of the sources it was built
+    from (imaginary_amd/srchash.py); it must be the hash of this tree's sources."""
+    import imaginary_amd as ia
+    from imaginary_amd.srchash import source_hash
+    assert ia.lib.mipx_build_id().decode() == source_hash()
+    assert ia.lib.mipx_build_id() in ia.lib.mipx_version()
+
+
+def build_c_client(dst):
+    """gcc-compile tests/c/mipx_client.c against include/mipx.h (plain C, as the cgo
+    shim would), linked to libmipx.so and the oracle (checker)."""
+    from oracle import oracle as o
+    o.build()
+    exe = os.path.join(str(dst), "mipx_client")
+    subprocess.run(["gcc", "-O2", "-Wall", "-Wextra", "-Werror", "-std=c11", "-D_DEFAULT_SOURCE",
+                    "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
+                    os.path.join(ROOT, "tests", "c", "mipx_client.c"),
+                    "-L", os.path.join(ROOT, "imaginary_amd"), "-L", os.path.join(ROOT, "oracle", "_build"),
+                    "-lmipx", "-loracle", "-lpthread",
+                    "-Wl,-rpath," + os.path.join(ROOT, "imaginary_amd") + ":" + os.path.join(ROOT, "oracle", "_build"),
+                    "-o", exe], check=True)
+    return exe
+
+
+def test_c_client_builds_against_the_header(tmp_path):
+    exe = build_c_client(tmp_path)
+    import imaginary_amd as ia
+    if ia.device_count() == 0:
+        r = subprocess.run([exe], capture_output=True, text=True)
+        assert r.returncode == 77, r.stderr
+
+
+def _plan_reduce_2x(ia):
+    return ia.plan_make(ia.make_opts(width=160, height=120, embed=1), ia.make_input(320, 240, 3, "png"))
+
+
+def test_inconsistent_plans_are_rejected_before_any_device_work():
+    """plans are ABI data; a step whose stated geometry disagrees with
+    its op must be EINVAL at mipx_workspace_bytes / mipx_execute_dev / mipx_submit,
+    never a kernel writing past a buffer sized for the stated geometry."""
+    import ctypes as C
+    import imaginary_amd as ia
+    from imaginary_amd import _abi
+    L = ia.lib
+    good = _plan_reduce_2x(ia)
+    cases = []
+    p = _abi.MipxPlan.from_buffer_copy(good)          # reduce says 170 wide, makes 160
+    p.steps[0].out_w = 170
+    p.out_w = 170
+    cases.append(p)
+    p = _abi.MipxPlan.from_buffer_copy(good)          # embed step grows past the stated size
+    p.n_steps = 2
+    s = p.steps[1]
+    s.op = _abi.OP_EMBED
+    s.a[2], s.a[3], s.a[4] = 400, 300, 1
+    s.out_w, s.out_h, s.out_bands = 160, 120, 3
+    cases.append(p)
+    p = _abi.MipxPlan.from_buffer_copy(good)          # zoom writes w*xf x h*yf
+    p.n_steps = 1
+    p.steps[0].op = _abi.OP_ZOOM
+    p.steps[0].a[0] = p.steps[0].a[1] = 2
+    p.steps[0].out_w, p.steps[0].out_h = 160, 120
+    cases.append(p)
+    p = _abi.MipxPlan.from_buffer_copy(good)          # smartcrop larger than its input
+    p.n_steps = 1
+    p.steps[0].op = _abi.OP_SMARTCROP
+    p.steps[0].a[0], p.steps[0].a[1] = 400, 100
+    p.steps[0].out_w, p.steps[0].out_h = p.out_w, p.out_h = 400, 100
+    cases.append(p)
+    p = _abi.MipxPlan.from_buffer_copy(good)          # extract outside the image
+    p.n_steps = 1
+    p.steps[0].op = _abi.OP_EXTRACT
+    p.steps[0].a[:4] = [300, 0, 40, 40]
+    p.steps[0].out_w, p.steps[0].out_h = p.out_w, p.out_h = 40, 40
+    cases.append(p)
+    for bad in cases:
+        assert L.mipx_workspace_bytes(C.byref(bad), 1) == 0
+        assert L.mipx_execute_dev(C.byref(bad), 1, 16, 16, None, 16, 1 << 30, None) == -1
+        src = np.zeros((bad.in_h, bad.in_w, bad.in_bands), np.uint8)
+        dst = np.zeros((bad.out_h, bad.out_w, bad.out_bands), np.uint8)
+        t = C.c_uint64()
+        assert L.mipx_submit(-1, C.byref(bad), C.byref(_img(src)), None, C.byref(_img(dst)), C.byref(t)) == -1
+
+
+def _img(a):
+    from imaginary_amd._abi import MipxImg
+    return MipxImg(a.ctypes.data, a.shape[1], a.shape[0], a.shape[2], a.strides[0])
+
+
+def test_watermark_image_must_match_the_plan():
+    """the watermark kernel reads with the step's wm geometry, so a
+    caller's watermark of another size is EINVAL at submit."""
+    import ctypes as C
+    import imaginary_amd as ia
+    L = ia.lib
+    p = ia.plan_make(ia.make_opts(width=256, height=192, wm_enable=1, wm_left=16, wm_top=16, wm_opacity=0.5),
+                     ia.make_input(400, 300, 3, "png", 0, wm_w=128, wm_h=128, wm_bands=4))
+    src = np.zeros((300, 400, 3), np.uint8)
+    dst = np.zeros((p.out_h, p.out_w, p.out_bands), np.uint8)
+    t = C.c_uint64()
+    for shape in [(64, 64, 4), (128, 128, 3), (128, 127, 4)]:
+        wm = np.zeros(shape, np.uint8)
+        assert L.mipx_submit(-1, C.byref(p), C.byref(_img(src)), C.byref(_img(wm)), C.byref(_img(dst)),
+                             C.byref(t)) == -1
+    assert L.mipx_submit(-1, C.byref(p), C.byref(_img(src)), None, C.byref(_img(dst)), C.byref(t)) == -1

@@ -264,3 +264,49 @@ def test_random_plans_agree_with_oracle(oracle):
             assert (p.out_w, p.out_h, p.load_shrink) == (rp.out_w, rp.out_h, rp.load_shrink)
             agree += 1
     assert agree > 500
+
+
+def test_extract_area_branch_follows_bimg(oracle):
+    """PARITY_ASSUMPTIONS #11: bimg 1.1.9's extract branch assigns `o.AreaHeight =
+    o.Width` when AreaWidth is 0, so a zero AreaWidth is an error in both planners;
+    the oracle switch `extract_area_fallback` gives the intended fallback."""
+    hdr = dict(w=400, h=300, bands=3, type=3)
+    zero_w = dict(width=200, top=5, area_height=100)       # Thumbnail-style: force -> reduce -> area
+    with pytest.raises(ia.MipxError) as e:
+        ia.plan_make(ia.make_opts(**zero_w), ia.make_input(400, 300, 3, "png"))
+    assert e.value.code == -1 and b"Extract area" in ia.lib.mipx_last_error()
+    assert oracle.plan(zero_w, hdr)[0] != 0
+    assert oracle.plan(dict(zoom=1, top=5, left=7, area_height=20), dict(hdr, w=40, h=30))[0] != 0
+    # AreaHeight 0 still falls back to Height, in both planners
+    zero_h = dict(width=200, left=5, area_width=100)
+    p = ia.plan_make(ia.make_opts(**zero_h), ia.make_input(400, 300, 3, "png"))
+    e2, rp = oracle.plan(zero_h, hdr)
+    assert e2 == 0 and _steps(p) == _steps(rp) and (p.out_w, p.out_h) == (100, 150)
+    oracle.set_switch("extract_area_fallback", 1)
+    try:
+        e3, rp = oracle.plan(zero_w, hdr)
+        assert e3 == 0 and (rp.out_w, rp.out_h) == (200, 100)
+    finally:
+        oracle.set_switch("extract_area_fallback", 0)
+
+
+def test_webp_shrink_on_load_switch(oracle):
+    """PARITY_ASSUMPTIONS #10: by default WEBP shrinks on load like JPEG (8/4/2
+    ladder, factor divided); `webp_sol_bimg` loads at 1/shrink with the factor kept
+    and the residual recomputed from the decoded size."""
+    opts = dict(width=500)
+    hdr = dict(w=4000, h=3000, bands=3, type=2)
+    p = ia.plan_make(ia.make_opts(**opts), ia.make_input(4000, 3000, 3, "webp"))
+    e, rp = oracle.plan(opts, hdr)
+    assert e == 0 and _steps(p) == _steps(rp)
+    assert p.load_shrink == rp.load_shrink == 4 and (p.out_w, p.out_h) == (500, 375)
+    oracle.set_switch("webp_sol_bimg", 1)
+    try:
+        e, rp = oracle.plan(opts, hdr)
+        assert e == 0 and rp.load_shrink == 6                       # floor(8 * 3/4)
+        assert (rp.in_w, rp.in_h) == (667, 500)
+        ops = [rp.steps[i].op for i in range(rp.n_steps)]
+        assert ops[0] == 3 and (rp.out_w, rp.out_h) == (500, 375)   # shrinkImage again, then residual
+    finally:
+        oracle.set_switch("webp_sol_bimg", 0)
+    assert oracle.plan(opts, hdr)[1].load_shrink == 4
