@@ -157,7 +157,7 @@ const char *mipx_build_id(void);
 int mipx_abi_version(void);
 const char *mipx_strerror(int code);
 const char *mipx_last_error(void);      /* thread-local detail of the last failure */
-int mipx_init(const mipx_cfg *cfg);     /* NULL = defaults */
+int mipx_init(const mipx_cfg *cfg);     /* NULL = defaults; already up: MIPX_OK, running config kept */
 void mipx_shutdown(void);
 int mipx_device_count(void);
 

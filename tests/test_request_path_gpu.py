@@ -59,6 +59,7 @@ def test_multi_queue_least_loaded_dispatch(gpu, oracle):
     the oracle's, every queue takes work, per-queue stats add up to the requests,
     and nothing is left pending."""
     from concurrent.futures import ThreadPoolExecutor
+    gpu.lib.mipx_shutdown()   # mipx_init keeps a running engine's configuration (imaginary.py's may be up)
     eng = gpu.Engine(devices=[0], max_batch=8, batch_wait_us=300, queues_per_device=3)
     try:
         plans = _plans(gpu, oracle)
@@ -100,6 +101,7 @@ def test_cancel_after_timeout_detaches_the_output(gpu):
     """MIPX_ETIMEOUT leaves the request running; mipx_cancel detaches the output so
     the caller may free it, and the ticket is released."""
     import ctypes as C
+    gpu.lib.mipx_shutdown()
     eng = gpu.Engine(devices=[0], max_batch=4)
     try:
         p = gpu.plan_make(gpu.make_opts(width=1920, height=1080, embed=1), gpu.make_input(3840, 2160, 3, "png"))
@@ -131,6 +133,7 @@ def test_shutdown_during_traffic_is_safe(gpu):
     submit: each submit either is queued (and then completes) or gets ENOTINIT."""
     p = gpu.plan_make(gpu.make_opts(width=80, height=60, embed=1), gpu.make_input(160, 120, 3, "png"))
     img = np.random.default_rng(3).integers(0, 256, (120, 160, 3), dtype=np.uint8)
+    gpu.lib.mipx_shutdown()
     for _round in range(3):
         eng = gpu.Engine(devices=[0], max_batch=4, queues_per_device=2)
         results = {"ok": 0, "notinit": 0, "other": []}
