@@ -54,6 +54,8 @@ int resize_schedule(int w, int h, double hscale, double vscale, ResizeSchedule &
 // ---- device-side cached tables ----------------------------------------------
 // float copy of reduce_table(shrink) resident on the current device.
 const float *device_reduce_table(double shrink, int *n_taps);
+// the same taps packed as int16 pairs: [129][2 alignments][*tpa] (k_rstrip)
+const uint32_t *device_reduce_pairs(double shrink, int *n_taps, int *tpa);
 const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt | 257 y2v]
 const int *device_bicubic_table();     // 129 x 4
 // float copy of the integer gaussmat mask; *scale = mask sum
@@ -85,6 +87,9 @@ int hpass_launch(const uint8_t *in, uint8_t *out, int n, const SepSpec &spec, co
 int reduce2d_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                     int oy0, int ow, int oh, hipStream_t st);
 int reduce_fused_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
+                        int oy0, int ow, int oh, hipStream_t st);
+// k_rstrip.hip: streaming fused reduce (LDS row ring + LDS intermediate), any shrink pair
+int reduce_strip_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                         int oy0, int ow, int oh, hipStream_t st);
 
 // ---- kernel launchers (k_*.hip); batches of n images packed back to back -----

@@ -66,6 +66,9 @@ int mipx_op_reduce(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, in
     if (vshrink == 1.0) return mipx_op_reduceh(d_in, d_out, n, w, h, bands, hshrink, stream);
     if (hshrink == 1.0) return mipx_op_reducev(d_in, d_out, n, w, h, bands, vshrink, stream);
     {  // both axes: one fused launch, intermediate in LDS
+        const int es = reduce_strip_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
+                                           out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
+        if (es != MIPX_EUNSUPPORTED) return es;
         const int e = reduce_fused_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
                                           out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
         if (e != MIPX_EUNSUPPORTED) return e;

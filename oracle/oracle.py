@@ -95,6 +95,9 @@ def lib():
             "ref_execute": (C.c_int, [P(RefPlan), P(RefImg), P(RefImg), P(RefImg)]),
             "ref_reduce_batch": (C.c_int, [P(P(C.c_uint8)), P(P(C.c_uint8)), C.c_int, C.c_int, C.c_int,
                                            C.c_int, C.c_double, C.c_double, C.c_int]),
+            "ref_reduce_fast": (C.c_int, [P(RefImg), P(RefImg), C.c_double, C.c_double]),
+            "ref_reduce_fast_batch": (C.c_int, [P(P(C.c_uint8)), P(P(C.c_uint8)), C.c_int, C.c_int, C.c_int,
+                                                C.c_int, C.c_double, C.c_double, C.c_int]),
             "ref_set_switch": (None, [C.c_char_p, C.c_int]),
             "ref_get_switch": (C.c_int, [C.c_char_p]),
             "ref_free": (None, [C.c_void_p]),
@@ -269,6 +272,30 @@ def reduce_batch(imgs, hshrink, vshrink, threads):
     e = lib().ref_reduce_batch(ins, ous, n, w, h, b, hshrink, vshrink, threads)
     if e:
         raise OracleError(e, "ref_reduce_batch")
+    return outs
+
+
+def reduce_fast(img, hshrink, vshrink):
+    """The CPU baseline's reduce (vips_fast.c): same result as reduce(), fast loop order."""
+    o = RefImg()
+    e = lib().ref_reduce_fast(C.byref(_in(img)), C.byref(o), hshrink, vshrink)
+    if e:
+        raise OracleError(e, "ref_reduce_fast")
+    return _out(o)
+
+
+def reduce_fast_batch(imgs, hshrink, vshrink, threads):
+    """CPU baseline (bench.py): list of HxWxB uint8 arrays, OpenMP across images."""
+    n = len(imgs)
+    h, w, b = imgs[0].shape
+    oh, ow = lib().ref_out_size_reduce(h, vshrink), lib().ref_out_size_reduce(w, hshrink)
+    outs = [np.empty((oh, ow, b), np.uint8) for _ in range(n)]
+    PP = C.POINTER(C.c_uint8) * n
+    ins = PP(*[np.ascontiguousarray(a).ctypes.data_as(C.POINTER(C.c_uint8)) for a in imgs])
+    ous = PP(*[a.ctypes.data_as(C.POINTER(C.c_uint8)) for a in outs])
+    e = lib().ref_reduce_fast_batch(ins, ous, n, w, h, b, hshrink, vshrink, threads)
+    if e:
+        raise OracleError(e, "ref_reduce_fast_batch")
     return outs
 
 

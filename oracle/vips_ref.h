@@ -155,6 +155,11 @@ int ref_execute(const ref_plan *plan, const ref_img *in, const ref_img *wm, ref_
 int ref_reduce_batch(const uint8_t *const *in, uint8_t *const *out, int n, int w, int h,
                      int bands, double hshrink, double vshrink, int threads);
 
+/* ---- CPU baseline (vips_fast.c, -O3 x86-64-v3): the same reduce, cache-friendly loop order ---- */
+int ref_reduce_fast(const ref_img *in, ref_img *out, double hshrink, double vshrink);
+int ref_reduce_fast_batch(const uint8_t *const *in, uint8_t *const *out, int n, int w, int h,
+                          int bands, double hshrink, double vshrink, int threads);
+
 /* parity switches (PARITY_ASSUMPTIONS.md); 0 = default assumption */
 void ref_set_switch(const char *name, int value);
 int ref_get_switch(const char *name);

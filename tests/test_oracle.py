@@ -122,3 +122,16 @@ def test_cpu_baseline_batch_matches_single(oracle, rng):
     outs = oracle.reduce_batch(imgs, 2.0, 2.0, 3)
     for a, b in zip(imgs, outs):
         assert np.array_equal(oracle.reduce(a, 2.0, 2.0), b)
+
+
+@pytest.mark.parametrize("h,w,b,hs,vs", [(216, 384, 3, 2.0, 2.0), (270, 480, 3, 1.6, 1.5976331360946747),
+                                         (101, 131, 4, 4 / 3, 4 / 3), (37, 53, 1, 2.4, 1.0), (29, 31, 2, 1.0, 1.7),
+                                         (9, 7, 3, 3.7, 2.9), (64, 300, 4, 14.2, 1.3)])
+def test_fast_cpu_baseline_is_the_oracle(oracle, h, w, b, hs, vs):
+    """bench.py times vips_fast.c as the CPU baseline; it must compute exactly the
+    oracle's reduce (interior, clamped edges, one-axis and tiny images)."""
+    rng = np.random.default_rng(h * w + b)
+    img = rng.integers(0, 256, (h, w, b), dtype=np.uint8)
+    assert np.array_equal(oracle.reduce_fast(img, hs, vs), oracle.reduce(img, hs, vs))
+    outs = oracle.reduce_fast_batch([img, img[::-1].copy()], hs, vs, 2)
+    assert np.array_equal(outs[1], oracle.reduce(img[::-1].copy(), hs, vs))
