@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU (BASELINE C2: 256)")
-    ap.add_argument("--cpu-images", type=int, default=128, help="CPU baseline sample size (images)")
+    ap.add_argument("--cpu-images", type=int, default=384, help="CPU baseline sample size (images): ~20 CPU-seconds on 16 EPYC cores")
     ap.add_argument("--cpu-distinct", type=int, default=24, help="distinct images in the CPU sample")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPUs allotted to this process")
     ap.add_argument("--c1-seconds", type=float, default=4.0, help="C1 CPU reference: seconds of timing")
@@ -139,21 +139,24 @@ def c1_cpu_reference(args):
                      "end to end over HTTP on an i7 with libvips 7.42 (operation not stated)"}
 
 
-TRAFFIC_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "traffic_v17.json")
+# the newest committed PMC traffic record of the C2 kernel (profiles/<round>/traffic_*.json)
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", "r02", "traffic_r02.json"),
+                 os.path.join(ROOT, "profiles", "r01", "traffic_v17.json")]
 
 
 def pmc_traffic(kernel_name_hint):
     """HBM bytes per launch from the committed rocprofv3 PMC passes of this kernel
     (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections calibrated in
     profiles/r01/calib_*.csv); None when no matching summary exists."""
-    try:
-        with open(TRAFFIC_JSON) as f:
-            t = json.load(f)
-    except OSError:
-        return None, None
-    if t.get("kernel") != kernel_name_hint:
-        return None, None
-    return t["traffic_bytes"], os.path.relpath(TRAFFIC_JSON, ROOT)
+    for path in TRAFFIC_JSONS:
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except OSError:
+            continue
+        if t.get("kernel") == kernel_name_hint:
+            return t["traffic_bytes"], os.path.relpath(path, ROOT)
+    return None, None
 
 
 def dist_env():

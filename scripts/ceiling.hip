@@ -97,6 +97,32 @@ __global__ void __launch_bounds__(256) box2x2_dw(const uint32_t *p, uint32_t *q,
     q[i] = s[0] ^ s[1] ^ s[IPW] ^ s[IPW + 1];
 }
 
+// the same pattern at 16 B per lane: 2 output dwords (8 B stored) per lane from
+// 4 input dwords of each of two rows, and 4 output dwords (16 B) from 8 + 8
+__global__ void __launch_bounds__(256) box2x2_x2(const uint32_t *p, uint32_t *q, long long nout2) {
+    const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= nout2) return;
+    constexpr int OPW = 720, OPH = 1080, IPW = 2880;  // dword pairs per output row, dwords per input row
+    const long long img = i / (static_cast<long long>(OPW) * OPH);
+    const int rem = static_cast<int>(i - img * OPW * OPH), y = rem / OPW, x = rem - y * OPW;
+    const uint4 *s = reinterpret_cast<const uint4 *>(p + img * (static_cast<long long>(IPW) * 2 * OPH) +
+                                                     static_cast<long long>(2 * y) * IPW + 4 * x);
+    const uint4 a = s[0], b = s[IPW / 4];
+    reinterpret_cast<uint2 *>(q)[i] = uint2{a.x ^ a.y ^ b.x ^ b.y, a.z ^ a.w ^ b.z ^ b.w};
+}
+__global__ void __launch_bounds__(256) box2x2_x4(const uint32_t *p, uint32_t *q, long long nout4) {
+    const long long i = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= nout4) return;
+    constexpr int OPW = 360, OPH = 1080, IPW = 2880;
+    const long long img = i / (static_cast<long long>(OPW) * OPH);
+    const int rem = static_cast<int>(i - img * OPW * OPH), y = rem / OPW, x = rem - y * OPW;
+    const uint4 *s = reinterpret_cast<const uint4 *>(p + img * (static_cast<long long>(IPW) * 2 * OPH) +
+                                                     static_cast<long long>(2 * y) * IPW + 8 * x);
+    const uint4 a = s[0], b = s[1], c = s[IPW / 4], d = s[IPW / 4 + 1];
+    reinterpret_cast<uint4 *>(q)[i] = uint4{a.x ^ a.y ^ c.x ^ c.y, a.z ^ a.w ^ c.z ^ c.w, b.x ^ b.y ^ d.x ^ d.y,
+                                           b.z ^ b.w ^ d.z ^ d.w};
+}
+
 // k_reduce2x2 geometry, memory only: tile = (img, band, strip), strip fastest
 __global__ void __launch_bounds__(256) rows_dw(const uint8_t *in, uint8_t *out, int w, int h, int n_strips,
                                                int n_bands, long long in_img, long long out_img) {
@@ -188,6 +214,18 @@ int main() {
             box2x2_dw<<<static_cast<unsigned>((nout + 255) / 256), 256>>>((const uint32_t *)in, (uint32_t *)out, nout);
         });
         printf("{\"kernel\": \"box2x2_dw\", \"ms\": %.4f, \"GBps\": %.1f}\n", ms, (IN + OUT) / ms / 1e6);
+    }
+    {
+        const long long nout2 = static_cast<long long>(n) * 720 * 1080;
+        float ms = time_it([&] {
+            box2x2_x2<<<static_cast<unsigned>((nout2 + 255) / 256), 256>>>((const uint32_t *)in, (uint32_t *)out, nout2);
+        });
+        printf("{\"kernel\": \"box2x2_x2\", \"ms\": %.4f, \"GBps\": %.1f}\n", ms, (IN + OUT) / ms / 1e6);
+        const long long nout4 = static_cast<long long>(n) * 360 * 1080;
+        ms = time_it([&] {
+            box2x2_x4<<<static_cast<unsigned>((nout4 + 255) / 256), 256>>>((const uint32_t *)in, (uint32_t *)out, nout4);
+        });
+        printf("{\"kernel\": \"box2x2_x4\", \"ms\": %.4f, \"GBps\": %.1f}\n", ms, (IN + OUT) / ms / 1e6);
     }
     {
         const int n_strips = (W / 2 + 159) / 160, n_bands = (H / 2 + 23) / 24;
