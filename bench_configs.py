@@ -184,7 +184,8 @@ def e2e(args, dev, sp, stream):
     plan = plan_for(dict(width=1920, height=1080, embed=1), 3840, 2160, 3)
     rng = np.random.default_rng(6)
     srcs = [rng.integers(0, 256, (2160, 3840, 3), dtype=np.uint8) for _ in range(8)]  # shared inputs, any thread count
-    eng = ia.Engine(devices=[local], max_batch=args.e2e_batch, batch_wait_us=1000)
+    eng = ia.Engine(devices=[local], max_batch=args.e2e_batch, batch_wait_us=1000,
+                    queues_per_device=args.e2e_queues)
     try:
         def one(i):
             t, out = eng.submit(plan, srcs[i % len(srcs)])
@@ -198,6 +199,7 @@ def e2e(args, dev, sp, stream):
             outs = list(ex.map(one, range(n)))
             dt = time.perf_counter() - t0
         b1, r1 = eng.stats(local)
+        qs = eng.queue_stats()
         from oracle import oracle as o
         ok = bool(np.array_equal(outs[0], o.reduce(srcs[0], 2.0, 2.0))) and \
             bool(np.array_equal(first[1], o.reduce(srcs[1], 2.0, 2.0)))
@@ -207,6 +209,7 @@ def e2e(args, dev, sp, stream):
                           "images_per_sec": round(n / dt, 1), "requests": n, "wall_s": round(dt, 3),
                           "host_link_gbs": round(link / dt / 1e9, 2),
                           "batches": int(b1 - b0), "mean_batch": round((r1 - r0) / max(1, b1 - b0), 2),
+                          "queues": len(qs), "requests_per_queue": [int(r) for _, _, r, _ in qs],
                           "verified_vs_oracle": ok}), flush=True)
     finally:
         eng.shutdown()
@@ -222,6 +225,7 @@ def main():
     ap.add_argument("--e2e-requests", type=int, default=256)
     ap.add_argument("--e2e-batch", type=int, default=16)
     ap.add_argument("--e2e-threads", type=int, default=16, help="submitting threads (requests in flight)")
+    ap.add_argument("--e2e-queues", type=int, default=1, help="request queues (streams + worker) per device")
     ap.add_argument("--c5-requests", type=int, default=512 * int(os.environ.get("WORLD_SIZE", "1")),
                     help="total requests, sharded across ranks (4096 at 8 GPUs)")
     args = ap.parse_args()
