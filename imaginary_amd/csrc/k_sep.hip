@@ -41,7 +41,11 @@ struct SepTaps {
     float rounding, inv_scale;  // conv rounding
     int dot;                 // integer dot paths (MIPX_SEP_DOT=0 selects the float path)
     int tq;                  // conv vpass: rows transposed once per 4-row quad (MIPX_SEP_TQ=0: per output row)
+    int share;               // reduce vpass: byte pairs shared by the block's rows (MIPX_VP_SHARE=1, A/B)
 };
+
+constexpr int kShareRows = 12;  // output rows per block on the shared-pair reduce path
+constexpr int kVpPairs = 8;     // tap pairs of the unrolled vertical reduce (taps <= 16: shrink < 2.75)
 
 // Reduce masks are 12-bit signed integers (x 4096), so tap pairs fit packed
 // int16 and v_dot2_i32_i16 sums byte pairs zero-extended to int16 exactly:
@@ -61,6 +65,16 @@ __device__ __forceinline__ uint32_t fixed_round_i(int sum) {
     int v = clampi((sum + 2048) >> 12, 0, 255);
     asm("" : "+v"(v));
     return static_cast<uint32_t>(v);
+}
+// (acc0..3 + 2048) >> 12 clamped to 0..255, packed: gfx950's v_ashr_pk_u8_i32
+// does shift + saturate + pack for two channels (it writes only the low 16 bits
+// of its destination, so the halves are joined with a v_perm, never ORed).
+// The accumulators start at 2048, so the rounding add is free.
+__device__ __forceinline__ uint32_t round_pack4(int a0, int a1, int a2, int a3) {
+    uint32_t lo, hi;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(a0), "v"(a1));
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(a2), "v"(a3));
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 __device__ __forceinline__ uint32_t pack_pair(float c0, float c1) {
     return (static_cast<uint32_t>(static_cast<int>(c0)) & 0xffffu) | (static_cast<uint32_t>(static_cast<int>(c1)) << 16);
@@ -107,6 +121,7 @@ struct VPassArgs {
     int col_blocks, kr_blocks;
     int kr;               // output rows per block
     int lrows;            // LDS input-row capacity (>= (kr - 1) * shrink + taps + 1)
+    int np;               // shared-pair reduce: staged row pairs a block can touch
     SepTaps tp;
 };
 
@@ -114,6 +129,100 @@ constexpr int kVStride = 260;  // LDS dwords per staged row: 256 + 1 (skewed row
 
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ lds_void *to_lds(void *p) { return (lds_void *)p; }  // generic -> LDS addrspacecast
+
+// Stage input rows r_lo .. r_lo + L - 1 (COPY-clamped) of 1 KiB column block cb
+// into LDS rows of kVStride dwords with direct-to-LDS buffer loads (DMA bytes per
+// lane; DMA 0: dword loads from each row's aligned-down start plus one dword).
+template <int DMA>
+__device__ __forceinline__ void vstage_rows(const VPassArgs &a, uint32_t *rows, int img, int cb, int r_lo, int L,
+                                            int wave, int lane, int *delta) {
+    const u8 *src = a.in + img * a.in_img;
+    const long long col0 = a.in_base + static_cast<long long>(cb) * 1024;
+    if (DMA == 16) {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
+        for (int l = wave; l < L; l += 4) {
+            const int r = clampi(r_lo + l, 0, a.hl - 1);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride), 16,
+                                                     static_cast<int>(col0) + lane * 16, r * a.in_pitch, 0, 0);
+        }
+    } else if (DMA == 4) {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
+        for (int l = 0; l < L; ++l) {
+            const int r = clampi(r_lo + l, 0, a.hl - 1);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + wave * 64), 4,
+                                                     static_cast<int>(col0) + wave * 256 + lane * 4,
+                                                     r * a.in_pitch, 0, 0);
+        }
+    } else {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, delta);
+        for (int l = 0; l < L; ++l) {
+            const int r = clampi(r_lo + l, 0, a.hl - 1);
+            const int a4 = static_cast<int>(*delta + col0 + static_cast<long long>(r) * a.in_pitch) & ~3;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + wave * 64), 4,
+                                                     wave * 256 + lane * 4, a4, 0, 0);
+            if (wave == 0 && lane == 0)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + 256), 4, 1024, a4, 0, 0);
+        }
+    }
+}
+
+// Vertical reduce with TP2 tap pairs known at compile time (16 / 4-byte aligned
+// rows, 4-byte output rows): per output row and lane 2 TP2 LDS reads issued
+// together, 4 v_perm + 4 v_dot2 per pair, the rounding folded into the
+// accumulator seed and v_ashr_pk_u8_i32, one buffer store with the row offset in
+// an SGPR.  k_vpass's generic loop spent ~2x the VALU on loop, rounding and
+// address work (profiles/r02 pmc: 97.6M VALU for 1080p RGB /1.6 x 64).
+template <int TP2, int DMA>
+__global__ void __launch_bounds__(256) k_vreduce(VPassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t vsm[];
+    uint32_t *rows = vsm;                              // lrows x kVStride dwords
+    uint32_t *cpk = vsm + a.lrows * kVStride;          // kr x kVpPairs int16 tap pairs (16-byte aligned)
+    int *soff = reinterpret_cast<int *>(cpk + a.kr * kVpPairs);
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int cb = t % a.col_blocks;
+    const int rest = t / a.col_blocks;
+    const int kb = rest % a.kr_blocks;
+    const int img = rest / a.kr_blocks;
+    const int taps = a.tp.taps;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int y0 = kb * a.kr;
+    const int nk = min(a.kr, a.oh - y0);
+    int r_lo, r_last, ph;
+    sep_position(a.tp, a.oy0 + y0, &r_lo, &ph);
+    sep_position(a.tp, a.oy0 + y0 + nk - 1, &r_last, &ph);
+    int delta = 0;
+    vstage_rows<DMA>(a, rows, img, cb, r_lo, r_last + taps - r_lo, wave, lane, &delta);
+    for (int i = tid; i < nk * kVpPairs; i += 256) {
+        const int k = i / kVpPairs, m = i - k * kVpPairs;
+        int st;
+        sep_position(a.tp, a.oy0 + y0 + k, &st, &ph);
+        const float *c = a.tp.tab + ph * taps;
+        cpk[i] = m < TP2 ? pack_pair(2 * m < taps ? c[2 * m] : 0.f, 2 * m + 1 < taps ? c[2 * m + 1] : 0.f) : 0u;
+        if (m == 0) soff[k] = st - r_lo;
+    }
+    __syncthreads();
+    const int j = cb * 1024 + tid * 4;
+    if (j >= a.row_bytes) return;
+    const __amdgpu_buffer_rsrc_t os =
+        __builtin_amdgcn_make_buffer_rsrc(a.out + img * a.out_img, 0, static_cast<int>(a.out_img), 0x00020000);
+    for (int k = 0; k < nk; ++k) {
+        const uint32_t *rp = rows + __builtin_amdgcn_readfirstlane(soff[k]) * kVStride + tid;
+        uint32_t v[2 * TP2];
+#pragma unroll
+        for (int i = 0; i < 2 * TP2; ++i) v[i] = rp[i * kVStride];
+        const uint4 c0 = reinterpret_cast<const uint4 *>(cpk + k * kVpPairs)[0];
+        const uint4 c1 = reinterpret_cast<const uint4 *>(cpk + k * kVpPairs)[1];
+        const uint32_t cw[kVpPairs] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        int acc[4] = {2048, 2048, 2048, 2048};
+#pragma unroll
+        for (int m = 0; m < TP2; ++m)
+#pragma unroll
+            for (int z = 0; z < 4; ++z) acc[z] = dot2_byte(v[2 * m], v[2 * m + 1], z, cw[m], acc[z]);
+        __builtin_amdgcn_raw_buffer_store_b32(round_pack4(acc[0], acc[1], acc[2], acc[3]), os, j,
+                                              (y0 + k) * a.row_bytes, 0);
+    }
+}
 
 // DMA: 16 / 4 = bytes per lane of the direct-to-LDS buffer loads when rows are
 // 16 / 4 byte aligned; 0 = any alignment (dword DMA from each row's aligned-down
@@ -139,47 +248,24 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
     sep_position(a.tp, a.oy0 + y0 + nk - 1, &r_last, &ph);
     const int L = r_last + taps - r_lo;
     // ---- stage the L input rows of this 1 KiB column block in LDS ----
-    const u8 *src = a.in + img * a.in_img;
-    const long long col0 = a.in_base + static_cast<long long>(cb) * 1024;
     int delta = 0;
-    if (DMA == 16) {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
-        for (int l = wave; l < L; l += 4) {
-            const int r = clampi(r_lo + l, 0, a.hl - 1);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride), 16,
-                                                     static_cast<int>(col0) + lane * 16, r * a.in_pitch, 0, 0);
+    vstage_rows<DMA>(a, rows, img, cb, r_lo, L, wave, lane, &delta);
+    const long long col0 = a.in_base + static_cast<long long>(cb) * 1024;
+    if (!a.tp.dot) {
+        for (int i = tid; i < nk * taps; i += 256) {
+            const int k = i / taps;
+            int s;
+            sep_position(a.tp, a.oy0 + y0 + k, &s, &ph);
+            vcoef[i] = a.tp.tab[ph * taps + (i - k * taps)];
         }
-    } else if (DMA == 4) {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
-        for (int l = 0; l < L; ++l) {
-            const int r = clampi(r_lo + l, 0, a.hl - 1);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + wave * 64), 4,
-                                                     static_cast<int>(col0) + wave * 256 + lane * 4,
-                                                     r * a.in_pitch, 0, 0);
-        }
-    } else {  // any alignment: each row from its dword-aligned-down start, plus one dword
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, &delta);
-        for (int l = 0; l < L; ++l) {
-            const int r = clampi(r_lo + l, 0, a.hl - 1);
-            const int a4 = static_cast<int>(delta + col0 + static_cast<long long>(r) * a.in_pitch) & ~3;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + wave * 64), 4,
-                                                     wave * 256 + lane * 4, a4, 0, 0);
-            if (wave == 0 && lane == 0)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + 256), 4, 1024, a4, 0, 0);
-        }
-    }
-    for (int i = tid; i < nk * taps; i += 256) {
-        const int k = i / taps;
-        int s;
-        sep_position(a.tp, a.oy0 + y0 + k, &s, &ph);
-        vcoef[i] = a.tp.tab[ph * taps + (i - k * taps)];
     }
     if (tid < nk) {
         int s;
         sep_position(a.tp, a.oy0 + y0 + tid, &s, &ph);
         soff[tid] = s - r_lo;
     }
-    uint32_t *cpk = reinterpret_cast<uint32_t *>(soff + a.kr);  // conv: packed u8 taps; reduce: int16 pairs per row
+    // conv: packed u8 taps; reduce: int16 pairs per row (16-byte aligned for b128 reads)
+    uint32_t *cpk = vsm + ((a.lrows * kVStride + a.kr * (taps + 1) + 3) & ~3);
     const int tq = (taps + 3) >> 2, tp2 = (taps + 1) >> 1;
     if (MODE == kSepConv && tid < tq) cpk[tid] = pack_taps(a.tp.tab, taps, tid);
     // conv, quad-transposed rows: coefficient set p (output row k with k % 4 == p) for
@@ -195,7 +281,27 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
         }
         cpk[tq + tid] = w;
     }
-    if (MODE == kSepReduce && a.tp.dot) {
+    const int tpa = taps / 2 + 1;  // shared pairs: a row's window spans tpa staged-row pairs
+    if (MODE == kSepReduce && a.tp.dot && a.tp.share && DMA != 0) {
+        // row k starts at staged row soff[k]; staged pair jp = rows (2jp, 2jp + 1) is
+        // pair m = jp - (soff[k] >> 1) of row k, taps (2m - al, 2m + 1 - al) with
+        // al = soff[k] & 1.  Table [jp][kShareRows], 0 where the row does not cover jp.
+        for (int i = tid; i < a.np * kShareRows; i += 256) {
+            const int jp = i / kShareRows, k = i - jp * kShareRows;
+            uint32_t w = 0;
+            if (k < nk) {
+                int st;
+                sep_position(a.tp, a.oy0 + y0 + k, &st, &ph);
+                const int so = st - r_lo, m = jp - (so >> 1);
+                if (m >= 0 && m < tpa) {
+                    const float *c = a.tp.tab + ph * taps;
+                    const int t0 = 2 * m - (so & 1);
+                    w = pack_pair(t0 >= 0 && t0 < taps ? c[t0] : 0.f, t0 + 1 < taps ? c[t0 + 1] : 0.f);
+                }
+            }
+            cpk[i] = w;
+        }
+    } else if (MODE == kSepReduce && a.tp.dot) {
         for (int i = tid; i < nk * tp2; i += 256) {
             const int k = i / tp2, m = i - k * tp2;
             int st;
@@ -270,6 +376,57 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
             uint32_t o = 0;
 #pragma unroll
             for (int z = 0; z < 4; ++z) o |= sep_round<MODE>(static_cast<float>(acc[z]), a.tp) << (8 * z);
+            u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
+            if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+                *reinterpret_cast<uint32_t *>(q) = o;
+            } else {
+                for (int z = 0; z < nb; ++z) q[z] = static_cast<u8>(o >> (8 * z));
+            }
+        }
+        return;
+    }
+    if (MODE == kSepReduce && a.tp.dot && a.tp.share && DMA != 0) {
+        // Pair-outer: each staged row pair is read and byte-paired (2 LDS reads +
+        // 4 v_perm) once for all of the block's output rows whose window covers it,
+        // instead of once per output row; coverage tests are uniform (SGPR) branches.
+        int jk[kShareRows];
+#pragma unroll
+        for (int k = 0; k < kShareRows; ++k) jk[k] = __builtin_amdgcn_readfirstlane(k < nk ? soff[k] >> 1 : 1 << 20);
+        const int npair = __builtin_amdgcn_readfirstlane((soff[nk - 1] >> 1) + tpa);
+        int acc[kShareRows][4];
+#pragma unroll
+        for (int k = 0; k < kShareRows; ++k)
+#pragma unroll
+            for (int z = 0; z < 4; ++z) acc[k][z] = 0;
+        const uint32_t *rp = rows + tid;
+        for (int jp = 0; jp < npair; ++jp) {
+            const uint32_t v0 = rp[(2 * jp) * kVStride], v1 = rp[(2 * jp + 1) * kVStride];
+            uint32_t pr[4];
+#pragma unroll
+            for (int z = 0; z < 4; ++z) pr[z] = __builtin_amdgcn_perm(v1, v0, 0x0C040C00u + 0x00010001u * z);
+            uint32_t cw[kShareRows];  // this pair's coefficient for every row: 3 broadcast b128 reads
+            const uint4 *cq = reinterpret_cast<const uint4 *>(cpk + jp * kShareRows);
+#pragma unroll
+            for (int q = 0; q < kShareRows / 4; ++q) {
+                const uint4 c4 = cq[q];
+                cw[4 * q] = c4.x, cw[4 * q + 1] = c4.y, cw[4 * q + 2] = c4.z, cw[4 * q + 3] = c4.w;
+            }
+#pragma unroll
+            for (int k = 0; k < kShareRows; ++k) {
+                if (static_cast<unsigned>(jp - jk[k]) < static_cast<unsigned>(tpa)) {
+#pragma unroll
+                    for (int z = 0; z < 4; ++z)
+                        acc[k][z] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr[z]),
+                                                           __builtin_bit_cast(short2v, cw[k]), acc[k][z], false);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kShareRows; ++k) {
+            if (k >= nk) continue;
+            uint32_t o = 0;
+#pragma unroll
+            for (int z = 0; z < 4; ++z) o |= fixed_round_i(acc[k][z]) << (8 * z);
             u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
             if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
                 *reinterpret_cast<uint32_t *>(q) = o;
@@ -1163,6 +1320,13 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     constexpr int kRowMax = 60;
     int kr = taps >= kRowBudget ? 1 : static_cast<int>(std::floor((kRowBudget - taps - 1) / s)) + 1;
     kr = std::max(1, std::min({kr, 32, a.oh}));
+    const char *esh = std::getenv("MIPX_VP_SHARE");
+    // A/B variant, off by default: 2-15% slower than per-row pairs on the op_survey shapes
+    // (profiles/r02/vp_share_ab.jsonl) -- coefficient reads and coverage branches cost what
+    // the shared perms save
+    a.tp.share = spec.mode == kSepReduce && a.tp.dot && esh && *esh == '1';
+    if (a.tp.share) kr = std::min(kr, kShareRows);
+    a.np = static_cast<int>(std::ceil((kr - 1) * s)) / 2 + 1 + taps / 2 + 1;
     auto rows_for = [&](int k) {  // conv: taps read in 4s
         return static_cast<int>(std::ceil((k - 1) * s)) + taps + 2 + (spec.mode == kSepConv ? 2 : 0);
     };
@@ -1172,7 +1336,8 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     a.kr_blocks = (a.oh + kr - 1) / kr;
     const dim3 blk(256);
     const size_t lds = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * taps * 4 + kr * 4 +
-                       static_cast<size_t>(std::max((taps + 3) / 4 + 4 * ((taps + 6) / 4), kr * ((taps + 1) / 2))) * 4;
+                       static_cast<size_t>(std::max({(taps + 3) / 4 + 4 * ((taps + 6) / 4), kr * std::max((taps + 1) / 2, kVpPairs),
+                                                     a.tp.share ? a.np * kShareRows : 0}) + 4) * 4;
     if (a.lrows > kRowMax || lds > 64 * 1024) {  // very tall masks: gather through L1
         const dim3 grid((a.row_bytes + 1023) / 1024, a.oh, n);
         if (spec.mode == kSepReduce) hipLaunchKernelGGL(k_vpass_gather<kSepReduce>, grid, blk, 0, st, a);
@@ -1190,7 +1355,27 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
         al16 = al16 && cap >= 16;
         al4 = al4 && cap >= 4;
     }
+    if (!al4) a.tp.share = 0;  // byte-shifted (DMA 0) rows keep the per-row path
+    const char *evf = std::getenv("MIPX_VP_FAST");  // A/B: 0 keeps k_vpass's generic reduce loop
+    const int tp2 = (taps + 1) / 2;
+    const bool vfast = spec.mode == kSepReduce && a.tp.dot && !a.tp.share && !(evf && *evf == '0') &&
+                       tp2 <= kVpPairs && a.row_bytes % 4 == 0 && a.out_img % 4 == 0 &&
+                       reinterpret_cast<uintptr_t>(out) % 4 == 0 && a.out_img < 0x7fffffffLL;
     const dim3 grid(static_cast<unsigned>(blocks));
+    if (vfast && al4) {
+        const size_t lv = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * (kVpPairs + 1) * 4;
+#define MIPX_VR(T_)                                                                                     \
+    case T_:                                                                                            \
+        if (al16) hipLaunchKernelGGL((k_vreduce<T_, 16>), grid, blk, lv, st, a);                        \
+        else hipLaunchKernelGGL((k_vreduce<T_, 4>), grid, blk, lv, st, a);                              \
+        break;
+        switch (tp2) {
+            MIPX_VR(2) MIPX_VR(3) MIPX_VR(4) MIPX_VR(5) MIPX_VR(6) MIPX_VR(7) MIPX_VR(8)
+            default: return MIPX_EUNSUPPORTED;
+        }
+#undef MIPX_VR
+        return launch_check("k_vreduce");
+    }
 #define MIPX_VP(MODE)                                                                                   \
     if (al16) hipLaunchKernelGGL((k_vpass<MODE, 16>), grid, blk, lds, st, a);                           \
     else if (al4) hipLaunchKernelGGL((k_vpass<MODE, 4>), grid, blk, lds, st, a);                        \

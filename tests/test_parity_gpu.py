@@ -311,6 +311,35 @@ def test_reduce_passes_dot2_and_float_paths(gpu, oracle, rng, monkeypatch, dot, 
             assert_same(gh[i], oracle.reduceh(imgs[i], s), f"reduceh {s} {h}x{w}x{b} dot={dot}")
 
 
+@pytest.mark.parametrize("path", ["unrolled", "loop", "share"])
+@pytest.mark.parametrize("s", [1.02, 1.3333333333333333, 1.6, 2.4, 2.7, 3.7, 5.9])
+def test_reducev_paths(gpu, oracle, rng, monkeypatch, path, s):
+    """Vertical reduce kernels: k_vreduce with the tap pairs unrolled (default for
+    <= 16 taps on 4-byte rows), k_vpass's generic loop (MIPX_VP_FAST=0, and every
+    case k_vreduce does not take) and the A/B variant that shares staged row pairs
+    between a block's output rows (MIPX_VP_SHARE=1): 16- and 4-byte-aligned
+    batches (DMA 16 / 4), odd row bytes and an unaligned batch (DMA 0), many row
+    blocks, both pair alignments of each row, short images, windowed plans."""
+    monkeypatch.setenv("MIPX_VP_FAST", "0" if path == "loop" else "1")
+    monkeypatch.setenv("MIPX_VP_SHARE", "1" if path == "share" else "0")
+    monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
+    monkeypatch.setenv("MIPX_RSTRIP", "0")
+    for h, w, b in ((301, 64, 4), (257, 100, 3), (97, 1030, 4), (45, 301, 1), (7, 80, 4), (333, 33, 3),
+                    (120, 1111, 3), (64, 2, 2)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        gv = gpu.run_op("reducev", imgs, vshrink=s)
+        for i in range(2):
+            assert_same(gv[i], oracle.reducev(imgs[i], s), f"reducev {s} {h}x{w}x{b} {path}")
+    opts = dict(width=301, height=173, crop=1, gravity=3)  # south; reduce -> extract: window row offset
+    p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(640, 1020, 4, "png"))
+    e, rp = oracle.plan(opts, dict(w=640, h=1020, bands=4, type=3))
+    assert e == 0
+    imgs = rng.integers(0, 256, (2, 1020, 640, 4), dtype=np.uint8)
+    got = gpu.execute(p, imgs)
+    for i in range(2):
+        assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract {path}")
+
+
 @pytest.mark.parametrize("rows", ["1", "8", "13"])
 def test_reduce2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows):
     """Fused generic reduce (k_reduce2d, an A/B variant behind MIPX_REDUCE2D=1:
