@@ -539,6 +539,9 @@ struct HPassArgs {
     int repack4;          // raw path: 4-pixel vector repack (MIPX_HP_REPACK=0: one pixel per item)
     int pack3;            // B = 3: 4 lanes' pixels stored as 3 dwords (MIPX_HP_PACK3=1/0 forces; default: reduce, shrink >= 2)
     SepTaps tp;
+    const uint32_t *pairs;  // k_hreduce: int16 tap pairs [129][2][tpa] (device_reduce_pairs)
+    int tpa;
+    int rbn;                // k_hreduce: rows per block (runtime; k_hpass uses its RB)
 };
 
 template <int B>
@@ -571,28 +574,19 @@ __device__ __forceinline__ void store_rgb_px(u8 *q, uint32_t o, int j, bool full
     }
 }
 
-// DW = 16 / 4 (B = 4, rows 16 / 4 byte aligned): direct-to-LDS dwordx4 / dword
-// DMA of the span into the pixel slots (DW 16 stages from the 4-pixel-aligned
-// start, so each row's LDS origin is lo rounded down to 4 pixels); DW = 0: DMA
-// of each row's raw bytes from its aligned-down start, repacked to one u32 per
-// pixel in LDS (any alignment, any band count).
-// TREG > 0: each lane holds its (<= TREG) taps in registers (reduce); 0: taps
-// from the LDS table.
-template <int B, int RB, int MODE, int DW, int TREG>
-__global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
-    constexpr bool DIRECT = DW != 0;
-    extern __shared__ __attribute__((aligned(16))) uint32_t hsm[];
-    float *ctab = reinterpret_cast<float *>(hsm);
-    uint32_t *spx = hsm + a.ntab;
-    uint32_t *raw = spx + RB * a.span_max;
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int xb = t % a.x_blocks;
-    const int rest = t / a.x_blocks;
-    const int rb = rest % a.rb_blocks;
-    const int img = rest / a.rb_blocks;
+// Horizontal staging, shared by k_hpass and k_hreduce: rows y_first .. y_first +
+// nr - 1 of the input span feeding output columns [x0, x_last] of block xb,
+// DMA'd to LDS (hstage_issue), then edge-filled or repacked to one u32 per pixel
+// (hstage_finish: both barriers included; htq: conv's in-place 4x4 transposes).
+struct HStage {
+    int x0, x_last, lo, hi, span, y_first, nr, cl, ch, org, delta;
+    long long row0;
+};
+
+template <int B, int DW>
+__device__ __forceinline__ void hstage_issue(const HPassArgs &a, uint32_t *spx, uint32_t *raw, int xb, int rb,
+                                             int rbn, int img, int wave, int lane, HStage &g) {
     const int taps = a.tp.taps;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: no waterfall around the DMA
     const int x0 = xb * 256;
     const int x_last = min(x0 + 255, a.ow - 1);
     int lo, hi, ph;
@@ -600,8 +594,8 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
     sep_position(a.tp, a.ox0 + x_last, &hi, &ph);
     hi += taps - 1;
     const int span = hi - lo + 1;
-    const int y_first = rb * RB;
-    const int nr = min(RB, a.rows - y_first);
+    const int y_first = rb * rbn;
+    const int nr = min(rbn, a.rows - y_first);
     const int cl = max(lo, 0), ch = min(hi, a.wl - 1);  // pixels actually inside the row
     const int org = DW == 16 ? (lo & ~3) : lo;           // pixel of LDS slot 0 (floor for lo < 0)
     const u8 *img_base = a.in + img * a.in_img;
@@ -644,36 +638,15 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
                                                      4 * (q * 64 + lane), a4, 0, 0);
         });
     }
-    // this lane's taps
-    const int x = x0 + tid;
-    int s = 0, xph = 0;
-    sep_position(a.tp, a.ox0 + min(x, x_last), &s, &xph);
-    float cr[TREG > 0 ? TREG : 1];
-    if (TREG > 0) {
-        const float *c = a.tp.tab + xph * taps;
-#pragma unroll
-        for (int i = 0; i < TREG; ++i) cr[i] = i < taps ? c[i] : 0.f;
-    } else {
-        const int nt = (a.tp.phased ? kTransformScale + 1 : 1) * taps;
-        const int nfl = MODE == kSepConv ? ((taps + 3) & ~3) : a.ntab;  // conv: packed phase sets follow
-        for (int i = tid; i < nfl; i += 256) ctab[i] = i < nt ? a.tp.tab[i] : 0.f;
-        if (MODE == kSepConv) {
-            const int tqp = (taps + 6) >> 2;
-            for (int i = tid; i < 4 * tqp; i += 256) {
-                const int p = i / tqp, j = i - p * tqp;
-                uint32_t w = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int t = 4 * j + b - p;
-                    if (t >= 0 && t < taps) w |= static_cast<uint32_t>(a.tp.tab[t]) << (8 * b);
-                }
-                reinterpret_cast<uint32_t *>(ctab)[nfl + i] = w;
-            }
-        }
-    }
-    // conv: staged pixels transposed per 4-slot group (channel-major dwords), so an
-    // output pixel costs B LDS reads + B v_dot4 per group, no per-pixel v_perm
-    const bool htq = MODE == kSepConv && a.tp.dot && a.tp.tq && (DIRECT || a.repack4);
+    g = HStage{x0, x_last, lo, hi, span, y_first, nr, cl, ch, org, delta, row0};
+}
+
+template <int B, int DW>
+__device__ __forceinline__ void hstage_finish(const HPassArgs &a, uint32_t *spx, uint32_t *raw, const HStage &g,
+                                              int tid, bool htq) {
+    constexpr bool DIRECT = DW != 0;
+    const int lo = g.lo, hi = g.hi, span = g.span, nr = g.nr, cl = g.cl, ch = g.ch, org = g.org, delta = g.delta;
+    const long long row0 = g.row0;
     __syncthreads();
     {  // COPY edges (direct) or the repack of the raw bytes with each row's skew
         if (DIRECT) {
@@ -764,6 +737,65 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
             __syncthreads();
         }
     }
+}
+
+// DW = 16 / 4 (B = 4, rows 16 / 4 byte aligned): direct-to-LDS dwordx4 / dword
+// DMA of the span into the pixel slots (DW 16 stages from the 4-pixel-aligned
+// start, so each row's LDS origin is lo rounded down to 4 pixels); DW = 0: DMA
+// of each row's raw bytes from its aligned-down start, repacked to one u32 per
+// pixel in LDS (any alignment, any band count).
+// TREG > 0: each lane holds its (<= TREG) taps in registers (reduce); 0: taps
+// from the LDS table.
+template <int B, int RB, int MODE, int DW, int TREG>
+__global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
+    constexpr bool DIRECT = DW != 0;
+    extern __shared__ __attribute__((aligned(16))) uint32_t hsm[];
+    float *ctab = reinterpret_cast<float *>(hsm);
+    uint32_t *spx = hsm + a.ntab;
+    uint32_t *raw = spx + RB * a.span_max;
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int rb = rest % a.rb_blocks;
+    const int img = rest / a.rb_blocks;
+    const int taps = a.tp.taps;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: no waterfall around the DMA
+    HStage g;
+    hstage_issue<B, DW>(a, spx, raw, xb, rb, RB, img, wave, lane, g);
+    const int x0 = g.x0, x_last = g.x_last, org = g.org;
+    const int y_first = g.y_first, nr = g.nr;
+    // this lane's taps
+    const int x = x0 + tid;
+    int s = 0, xph = 0;
+    sep_position(a.tp, a.ox0 + min(x, x_last), &s, &xph);
+    float cr[TREG > 0 ? TREG : 1];
+    if (TREG > 0) {
+        const float *c = a.tp.tab + xph * taps;
+#pragma unroll
+        for (int i = 0; i < TREG; ++i) cr[i] = i < taps ? c[i] : 0.f;
+    } else {
+        const int nt = (a.tp.phased ? kTransformScale + 1 : 1) * taps;
+        const int nfl = MODE == kSepConv ? ((taps + 3) & ~3) : a.ntab;  // conv: packed phase sets follow
+        for (int i = tid; i < nfl; i += 256) ctab[i] = i < nt ? a.tp.tab[i] : 0.f;
+        if (MODE == kSepConv) {
+            const int tqp = (taps + 6) >> 2;
+            for (int i = tid; i < 4 * tqp; i += 256) {
+                const int p = i / tqp, j = i - p * tqp;
+                uint32_t w = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int t = 4 * j + b - p;
+                    if (t >= 0 && t < taps) w |= static_cast<uint32_t>(a.tp.tab[t]) << (8 * b);
+                }
+                reinterpret_cast<uint32_t *>(ctab)[nfl + i] = w;
+            }
+        }
+    }
+    // conv: staged pixels transposed per 4-slot group (channel-major dwords), so an
+    // output pixel costs B LDS reads + B v_dot4 per group, no per-pixel v_perm
+    const bool htq = MODE == kSepConv && a.tp.dot && a.tp.tq && (DIRECT || a.repack4);
+    hstage_finish<B, DW>(a, spx, raw, g, tid, htq);
     if (x > x_last) return;
     const uint32_t *sp = spx + (s - org);
     float acc[RB][B];
@@ -904,6 +936,70 @@ __global__ void __launch_bounds__(256) k_hpass(HPassArgs a) {
 
 // horizontal reduce without LDS staging, for shrinks whose span exceeds the
 // LDS budget: taps gathered through L1
+// Horizontal reduce with TP2 tap pairs known at compile time (B = 3 / 4): the
+// lane's tap pairs are TP2 dword loads from the int16 pair table (no float
+// conversion), rows are walked outermost with the pairs in registers, each row's
+// 2 TP2 pixel slots read together, rounding folded into the accumulator seed and
+// v_ashr_pk_u8_i32.  k_hpass's TREG path guarded every (pair, row) step with a
+// uniform branch and re-derived addresses (97M VALU + 70M SALU for 1080p RGB /1.6 x 64).
+template <int B, int DW, int TP2>
+__global__ void __launch_bounds__(256) k_hreduce(HPassArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hsm[];
+    uint32_t *spx = hsm;
+    uint32_t *raw = spx + a.rbn * a.span_max;
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int rb = rest % a.rb_blocks;
+    const int img = rest / a.rb_blocks;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    HStage g;
+    hstage_issue<B, DW>(a, spx, raw, xb, rb, a.rbn, img, wave, lane, g);
+    const int x = g.x0 + tid;
+    int s = 0, xph = 0;
+    sep_position(a.tp, a.ox0 + min(x, g.x_last), &s, &xph);
+    const uint32_t *pt = a.pairs + xph * 2 * a.tpa;  // alignment 0: (c[2m], c[2m + 1])
+    uint32_t cp[TP2];
+#pragma unroll
+    for (int m = 0; m < TP2; ++m) cp[m] = pt[m];
+    hstage_finish<B, DW>(a, spx, raw, g, tid, false);
+    if (x > g.x_last) return;
+    const uint32_t *sp = spx + (s - g.org);
+    u8 *ob = a.out + img * a.out_img;
+    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
+    for (int r = 0; r < g.nr; ++r) {
+        const uint32_t *pr = sp + r * a.span_max;
+        uint32_t v[2 * TP2];
+#pragma unroll
+        for (int i = 0; i < 2 * TP2; ++i) v[i] = pr[i];
+        int acc[4] = {2048, 2048, 2048, 2048};
+#pragma unroll
+        for (int m = 0; m < TP2; ++m)
+#pragma unroll
+            for (int z = 0; z < B; ++z) acc[z] = dot2_byte(v[2 * m], v[2 * m + 1], z, cp[m], acc[z]);
+        const uint32_t o = round_pack4(acc[0], acc[1], acc[2], acc[3]);
+        const long long row = static_cast<long long>(g.y_first + r) * a.ow;
+        if (B == 4) {
+            __builtin_amdgcn_raw_buffer_store_b32(o, os, x * 4, static_cast<int>(row * 4), 0);
+        } else {  // 3 bytes per lane: short + byte, or the 4-lane group's 12 bytes as 3 dwords
+            const int ro = static_cast<int>(row * 3);
+            const uint32_t nx = __shfl_down(o, 1, 64);
+            const int j = tid & 3;
+            const bool p3 = a.pack3 && ((reinterpret_cast<uintptr_t>(ob) + ro) & 3u) == 0;  // uniform
+            if (p3 && (x | 3) <= g.x_last) {
+                if (j < 3) {
+                    const uint32_t w = j == 0 ? (o | (nx << 24)) : j == 1 ? ((o >> 8) | (nx << 16)) : ((o >> 16) | (nx << 8));
+                    __builtin_amdgcn_raw_buffer_store_b32(w, os, 3 * x + j, ro, 0);
+                }
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(o), os, 3 * x, ro, 0);
+                __builtin_amdgcn_raw_buffer_store_b8(static_cast<unsigned char>(o >> 16), os, 3 * x + 2, ro, 0);
+            }
+        }
+    }
+}
+
 template <int B>
 __global__ void __launch_bounds__(256) k_hpass_gather(HPassArgs a) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1447,6 +1543,33 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const size_t lds = lds_for(rb);
     const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
+    const char *ehf = std::getenv("MIPX_HP_FAST");  // A/B: 0 keeps k_hpass's reduce path
+    const int tp2 = (a.tp.taps + 1) / 2;
+    if (spec.mode == kSepReduce && treg && a.tp.dot && (b == 3 || b == 4) && tp2 <= kVpPairs &&
+        !(ehf && *ehf == '0') && a.out_img < 0x7fffffffLL) {
+        int nt = 0;
+        a.pairs = device_reduce_pairs(spec.shrink, &nt, &a.tpa);
+        if (!a.pairs || nt != a.tp.taps) return MIPX_EDEVICE;
+        a.rbn = rb;
+#define MIPX_HR(B_, DW_, T_) hipLaunchKernelGGL((k_hreduce<B_, DW_, T_>), grid, blk, lds, st, a)
+#define MIPX_HRT(B_, DW_)                                                                                 \
+    switch (tp2) {                                                                                      \
+        case 2: MIPX_HR(B_, DW_, 2); break;                                                             \
+        case 3: MIPX_HR(B_, DW_, 3); break;                                                             \
+        case 4: MIPX_HR(B_, DW_, 4); break;                                                             \
+        case 5: MIPX_HR(B_, DW_, 5); break;                                                             \
+        case 6: MIPX_HR(B_, DW_, 6); break;                                                             \
+        case 7: MIPX_HR(B_, DW_, 7); break;                                                             \
+        default: MIPX_HR(B_, DW_, 8); break;                                                            \
+    }
+        if (b == 3) { MIPX_HRT(3, 0) }
+        else if (dwv == 16) { MIPX_HRT(4, 16) }
+        else if (dwv == 4) { MIPX_HRT(4, 4) }
+        else { MIPX_HRT(4, 0) }
+#undef MIPX_HRT
+#undef MIPX_HR
+        return launch_check("k_hreduce");
+    }
 #define MIPX_HP3(RB_, MODE_, DW_, TR_) \
     MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_hpass<B_, RB_, MODE_, DW_, TR_>), grid, blk, lds, st, a))
 #define MIPX_HPW(RB_, MODE_, TR_)                                       \
