@@ -1000,6 +1000,249 @@ __global__ void __launch_bounds__(256) k_hreduce(HPassArgs a) {
     }
 }
 
+// ===========================================================================
+// horizontal reduce on the matrix cores (k_hmfma)
+// ===========================================================================
+// A 16-pixel output group of 16 image rows is a banded product: out[px][row] =
+// sum_k C[px][k] * in[row][base + k], k over the 64-pixel K steps covering the
+// group's taps.  v_mfma_i32_16x16x64_i8 takes it exactly in integers:
+//  - pixels are staged channel-planar in LDS as p - 128 (XOR 0x80: signed i8);
+//  - the 12-bit taps split c = 64 hi + lo (hi = c >> 6, lo = c & 63, both i8),
+//    one MFMA each, the sums rejoined as (D_hi << 6) + D_lo;
+//  - the offset comes back as a bias 128 * sum(c) + 2048 seeded into D_lo.
+// Operand maps (checked by scripts/probe/mfma_i8_probe.hip): lane l holds
+// A[l & 15][16 (l >> 4) + j], B[16 (l >> 4) + j][l & 15] (byte j) and
+// D[4 (l >> 4) + i][l & 15] (register i).  A = taps of output pixel l & 15 from
+// the i8 table (row ph, bytes from kHmTabPad + k - start), B = 16 staged bytes
+// of image row l & 15, so each lane ends with 4 consecutive output pixels of one
+// row per channel: 12 / 16 contiguous bytes to store.
+constexpr int kHmRows = 16;  // image rows per block (the MFMA N)
+typedef int hm_v4i __attribute__((ext_vector_type(4)));
+
+struct HmArgs {
+    const u8 *in;
+    u8 *out;
+    int in_pitch;
+    long long in_base, in_img, out_img;
+    int wl, rows, ox0, ow;
+    int x_blocks, rb_blocks;
+    int plane_w;  // staged bytes per channel row (multiple of 16; covers every group's K steps)
+    int row_w;    // bytes per staged image row (B planes; / 16 odd: the 16 rows' b128 reads hit distinct banks)
+    int nks;      // 64-pixel K steps per group
+    int raw_max;  // LDS dwords per DMA-staged raw row
+    const signed char *tab;  // device_reduce_i8
+    const int *tsum;
+    SepTaps tp;
+};
+
+// The 16-byte fragment of an i8 tap row at window offset o (tap o + j in byte j,
+// 0 outside the taps): rows hold taps <= 16 after kHmTabPad zeros, so windows
+// further out than 16 bytes are all zero and o clamps to [-16, 16].
+__device__ __forceinline__ hm_v4i load_taps16(const signed char *row, int o) {
+    o = clampi(o - kHmTabPad, -16, 16) + kHmTabPad;
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (o & ~3));
+    const int sh = o & 3;
+    const uint4 d = *reinterpret_cast<const uint4 *>(p);
+    const uint32_t e = p[4];
+    hm_v4i r;
+    r[0] = static_cast<int>(__builtin_amdgcn_alignbyte(d.y, d.x, sh));
+    r[1] = static_cast<int>(__builtin_amdgcn_alignbyte(d.z, d.y, sh));
+    r[2] = static_cast<int>(__builtin_amdgcn_alignbyte(d.w, d.z, sh));
+    r[3] = static_cast<int>(__builtin_amdgcn_alignbyte(e, d.w, sh));
+    return r;
+}
+
+// XW output pixels per block (XW / 64 groups per wave)
+template <int B, int XW>
+__global__ void __launch_bounds__(256) k_hmfma(HmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hsm[];
+    constexpr int GPW = XW / 64;            // groups per wave
+    int *ps = reinterpret_cast<int *>(hsm);  // [XW] first tap pixel of each output pixel
+    int *pph = ps + XW;                      // [XW] phase
+    int *pbias = pph + XW;                   // [XW] 128 * tap sum + 2048
+    u8 *planes = reinterpret_cast<u8 *>(pbias + XW);  // [kHmRows][row_w: B x plane_w] pixel - 128
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int rb = rest % a.rb_blocks;
+    const int img = rest / a.rb_blocks;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int x0 = xb * XW;
+    const int x_last = min(x0 + XW - 1, a.ow - 1);
+    int lo, ph0;
+    sep_position(a.tp, a.ox0 + x0, &lo, &ph0);
+    const int org = lo & ~15;  // plane byte 0 = input pixel org (floor to 16)
+    int hi;
+    sep_position(a.tp, a.ox0 + x_last, &hi, &ph0);
+    hi += a.tp.taps - 1;
+    const int cl = max(lo, 0), ch = min(hi, a.wl - 1);  // pixels DMA'd per row
+    const int y_first = rb * kHmRows;
+    const int nr = min(kHmRows, a.rows - y_first);
+    uint32_t *raw = reinterpret_cast<uint32_t *>(planes + kHmRows * a.row_w);  // [kHmRows][raw_max]
+    // ---- raw bytes of the span, every row in flight (direct-to-LDS dword DMA) ----
+    // (byte offsets fit int: the launcher requires images < 2 GiB)
+    int delta = 0;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &delta);
+    const int row0 = delta + static_cast<int>(a.in_base) + y_first * a.in_pitch + B * cl;
+    const int chunks = ((B * (ch - cl + 1) + 6) / 4 + 63) >> 6;
+    for (int r = wave; r < nr; r += 4) {
+        const int a4 = (row0 + r * a.in_pitch) & ~3;
+        for (int c = 0; c < chunks; ++c)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + r * a.raw_max + c * 64), 4, 4 * (c * 64 + lane),
+                                                     a4, 0, 0);
+    }
+    if (tid < XW) {
+        int sp, ph;
+        sep_position(a.tp, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
+        ps[tid] = sp;
+        pph[tid] = ph;
+        pbias[tid] = 128 * a.tsum[ph] + 2048;
+    }
+    __syncthreads();
+    // this wave's 4 groups: first K step's taps requested now, consumed after the repack
+    const int n = lane & 15, kg = lane >> 4;
+    int go[GPW];
+    const signed char *gt[GPW];
+    hm_v4i ah0[GPW], al0[GPW];
+#pragma unroll
+    for (int gi = 0; gi < GPW; ++gi) {
+        const int g = wave * GPW + gi;
+        const int p = min(16 * g + n, x_last - x0);
+        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
+        go[gi] = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
+        gt[gi] = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
+        ah0[gi] = load_taps16(gt[gi], go[gi]);
+        al0[gi] = load_taps16(gt[gi] + kHmTabW, go[gi]);
+    }
+    // ---- channel-planar repack (pixel - 128), COPY edges by clamping into [cl, ch] ----
+    // rows per wave (uniform skew and shift), 4-pixel quads per lane
+    const int q_lo = (lo - org) >> 2, q_hi = (hi - org) >> 2;  // quads holding taps (the rest stays stale)
+    for (int r = wave; r < kHmRows; r += 4) {
+        const int rr = min(r, nr - 1);  // rows past the image: any staged row (never stored)
+        const int skew = (row0 + rr * a.in_pitch) & 3;
+        const int ob0 = (org - cl) * B + skew;  // raw byte of plane pixel 0 (may be < 0: clamped path)
+        const int sh = ob0 & 3;
+        const uint32_t *rwr = raw + rr * a.raw_max;
+        const u8 *rw8 = reinterpret_cast<const u8 *>(rwr) + skew;
+        u8 *pl = planes + r * a.row_w;
+        for (int q = q_lo + lane; q <= q_hi; q += 64) {
+            const int p0 = org + 4 * q;
+            uint32_t w[B];
+            // pixels outside [lo, hi] have zero taps, so only quads past an image edge
+            // need the clamp; inside a block the raw row (and its neighbours) is read as is
+            if (!((lo < 0 && p0 < 0) || (hi >= a.wl && p0 + 3 >= a.wl))) {
+                const uint32_t *rw = rwr + ((ob0 + 4 * B * q) >> 2);
+                uint32_t x[B];
+#pragma unroll
+                for (int k = 0; k < B; ++k) x[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], sh);
+                if (B == 3) {  // x = [r0 g0 b0 r1] [g1 b1 r2 g2] [b2 r3 g3 b3]
+                    w[0] = __builtin_amdgcn_perm(x[2 % B], __builtin_amdgcn_perm(x[1], x[0], 0x0c060300u), 0x05020100u);
+                    w[1] = __builtin_amdgcn_perm(x[2 % B], __builtin_amdgcn_perm(x[1], x[0], 0x0c070401u), 0x06020100u);
+                    w[2 % B] = __builtin_amdgcn_perm(x[2 % B], __builtin_amdgcn_perm(x[1], x[0], 0x0c0c0502u), 0x07040100u);
+                } else {
+                    uint32_t tt[4];
+                    transpose4x4(x[0], x[1 % B], x[2 % B], x[3 % B], tt);
+#pragma unroll
+                    for (int z = 0; z < B; ++z) w[z] = tt[z];
+                }
+            } else {
+#pragma unroll
+                for (int z = 0; z < B; ++z) w[z] = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const u8 *px = rw8 + (clampi(p0 + j, cl, ch) - cl) * B;
+#pragma unroll
+                    for (int z = 0; z < B; ++z) w[z] |= static_cast<uint32_t>(px[z]) << (8 * j);
+                }
+            }
+#pragma unroll
+            for (int z = 0; z < B; ++z) reinterpret_cast<uint32_t *>(pl + z * a.plane_w)[q] = w[z] ^ 0x80808080u;
+        }
+    }
+    __syncthreads();
+    // ---- GPW groups of 16 output pixels per wave ----
+    u8 *ob = a.out + img * a.out_img;
+    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
+#pragma unroll
+    for (int gi = 0; gi < GPW; ++gi) {
+        const int g = wave * GPW + gi;
+        if (x0 + 16 * g > x_last) break;
+        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
+        const int4 bias = *reinterpret_cast<const int4 *>(pbias + 16 * g + 4 * kg);
+        hm_v4i acc_h[B], acc_l[B];
+#pragma unroll
+        for (int z = 0; z < B; ++z) {
+            acc_h[z] = hm_v4i{0, 0, 0, 0};
+            acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
+        }
+        for (int ks = 0; ks < a.nks; ++ks) {
+            const hm_v4i ah = ks == 0 ? ah0[gi] : load_taps16(gt[gi], go[gi] + 64 * ks);
+            const hm_v4i al = ks == 0 ? al0[gi] : load_taps16(gt[gi] + kHmTabW, go[gi] + 64 * ks);
+#pragma unroll
+            for (int z = 0; z < B; ++z) {
+                const hm_v4i bz =
+                    *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 64 * ks + 16 * kg);
+                acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bz, acc_h[z], 0, 0, 0);
+                acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bz, acc_l[z], 0, 0, 0);
+            }
+        }
+        uint32_t wz[4];  // channel z of output pixels 4 kg .. 4 kg + 3 of row n
+#pragma unroll
+        for (int z = 0; z < B; ++z)
+            wz[z] = round_pack4((acc_h[z][0] << 6) + acc_l[z][0], (acc_h[z][1] << 6) + acc_l[z][1],
+                                (acc_h[z][2] << 6) + acc_l[z][2], (acc_h[z][3] << 6) + acc_l[z][3]);
+        if (n >= nr) continue;
+        const int x = x0 + 16 * g + 4 * kg;
+        if (x > x_last) continue;
+        uint32_t o[4];
+        if (B == 3) {  // [R G B] x 4 pixels -> [r0 g0 b0 r1] [g1 b1 r2 g2] [b2 r3 g3 b3]
+            o[0] = __builtin_amdgcn_perm(wz[2 % B], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
+            o[1] = __builtin_amdgcn_perm(wz[2 % B], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
+            o[2] = __builtin_amdgcn_perm(wz[2 % B], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
+        } else {
+            transpose4x4(wz[0], wz[1 % B], wz[2 % B], wz[3 % B], o);
+        }
+        if (B == 3) {  // into the block's output tile (the raw rows are dead after the repack)
+            uint32_t *tq = reinterpret_cast<uint32_t *>(reinterpret_cast<u8 *>(raw) + n * (XW * 3 + 4) + (x - x0) * 3);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) tq[k] = o[k];
+            continue;
+        }
+        const int qo = ((y_first + n) * a.ow + x) * B;  // byte offset in the output image
+        if (x + 3 <= x_last) {
+            __builtin_amdgcn_raw_buffer_store_b128(
+                hm_v4i{static_cast<int>(o[0]), static_cast<int>(o[1 % B]), static_cast<int>(o[2 % B]),
+                       static_cast<int>(o[3 % B])}, os, qo, 0, 0);
+        } else {
+            const int np = min(4, x_last - x + 1);
+            for (int k = 0; k < np * B; ++k) ob[qo + k] = static_cast<u8>(o[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+    if (B == 3) {  // each tile row to its output row as whole dwords at the row's own alignment
+        __syncthreads();
+        const int nb = (x_last - x0 + 1) * 3;
+        for (int r = wave; r < nr; r += 4) {
+            const u8 *tr = reinterpret_cast<const u8 *>(raw) + r * (XW * 3 + 4);
+            const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
+            const int qo0 = ((y_first + r) * a.ow + x0) * 3;
+            const int d0 = qo0 >> 2, nd = ((qo0 + nb + 3) >> 2) - d0;
+            const int sh = (4 - (qo0 & 3)) & 3;  // tile byte of dword i's first byte: 4 i - (qo0 & 3)
+            for (int i = lane; i < nd; i += 64) {
+                const int e = 4 * (d0 + i) - qo0;
+                if (e >= 0 && e + 4 <= nb) {
+                    const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
+                    __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i), 0, 0);
+                } else {
+                    for (int k = 0; k < 4; ++k)
+                        if (e + k >= 0 && e + k < nb)
+                            __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k, 0, 0);
+                }
+            }
+        }
+    }
+}
+
 template <int B>
 __global__ void __launch_bounds__(256) k_hpass_gather(HPassArgs a) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1543,6 +1786,53 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const size_t lds = lds_for(rb);
     const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
+    // i8 MFMA horizontal reduce, an A/B variant (MIPX_HP_MFMA=1): bit-exact, but it
+    // only ties k_hreduce (-8..+20 % by shape and box, slower on RGBA and on odd
+    // output widths; profiles/r02/hmfma_ab.jsonl) -- the pass is bound by staging
+    // latency and stores, not by the dot products the matrix cores take over
+    const char *ehm = std::getenv("MIPX_HP_MFMA");
+    const bool hm_on = ehm && *ehm == '1';
+    if (spec.mode == kSepReduce && a.tp.dot && (b == 3 || b == 4) && hm_on && a.out_img < 0x7fffffffLL) {
+        HmArgs m{};
+        m.in = in;
+        m.out = out;
+        m.in_pitch = a.in_pitch;
+        m.in_base = a.in_base;
+        m.in_img = a.in_img;
+        m.out_img = a.out_img;
+        m.wl = a.wl;
+        m.rows = a.rows;
+        m.ox0 = a.ox0;
+        m.ow = a.ow;
+        m.tp = a.tp;
+        const char *exw = std::getenv("MIPX_HM_XW");  // output pixels per block: 128 (default) / 256
+        const int xw = exw && *exw == '2' ? 256 : 128;
+        m.x_blocks = (a.ow + xw - 1) / xw;
+        m.rb_blocks = (a.rows + kHmRows - 1) / kHmRows;
+        m.nks = (static_cast<int>(std::ceil(15 * s)) + a.tp.taps + 16 + 63) / 64;
+        m.plane_w = ((static_cast<int>(std::ceil((xw - 16) * s)) + 32 + 64 * m.nks) + 15) & ~15;
+        int nt = 0;
+        m.tab = device_reduce_i8(spec.shrink, &nt, &m.tsum);
+        m.raw_max = std::max(((static_cast<int>(std::ceil((xw - 1) * s)) + a.tp.taps + 2) * b + 8 + 3) / 4 + 64,
+                             ((m.plane_w + 16) * b + 3) / 4 + 8);  // the repack may read a quad past the span
+        m.raw_max = std::max(m.raw_max, (xw * 3 + 4 + 3) / 4);      // RGB: output tile rows reuse the raw rows
+        m.row_w = b * m.plane_w + (((b * m.plane_w) / 16) % 2 == 0 ? 16 : 0);
+        const size_t lm = 3 * xw * 4 + static_cast<size_t>(kHmRows) * m.row_w +
+                          static_cast<size_t>(kHmRows) * m.raw_max * 4;
+        if (m.tab && nt == a.tp.taps && m.nks <= 4 && lm <= 64 * 1024) {
+            const long long hb = static_cast<long long>(m.x_blocks) * m.rb_blocks * n;
+            if (!grid_ok(hb)) return MIPX_EINVAL;
+            const dim3 hg(static_cast<unsigned>(hb));
+            if (xw == 256) {
+                if (b == 3) hipLaunchKernelGGL((k_hmfma<3, 256>), hg, dim3(256), lm, st, m);
+                else hipLaunchKernelGGL((k_hmfma<4, 256>), hg, dim3(256), lm, st, m);
+            } else {
+                if (b == 3) hipLaunchKernelGGL((k_hmfma<3, 128>), hg, dim3(256), lm, st, m);
+                else hipLaunchKernelGGL((k_hmfma<4, 128>), hg, dim3(256), lm, st, m);
+            }
+            return launch_check("k_hmfma");
+        }
+    }
     const char *ehf = std::getenv("MIPX_HP_FAST");  // A/B: 0 keeps k_hpass's reduce path
     const int tp2 = (a.tp.taps + 1) / 2;
     if (spec.mode == kSepReduce && treg && a.tp.dot && (b == 3 || b == 4) && tp2 <= kVpPairs &&

@@ -32,7 +32,18 @@ def vr(v):
 
 
 def main():
-    extra = [dict(kv.split("=") for kv in v.split(",")) for v in sys.argv[1:]]
+    global SHAPES
+    args = sys.argv[1:]
+    if args and args[0] == "--hshapes":  # horizontal-pass shapes (vshrink 1: reduceh alone)
+        args = args[1:]
+        SHAPES = [(w, h, b, n, s, 1.0) for (w, h, b, n, s) in (
+            (1920, 675, 3, 64, 1.6), (3840, 1350, 3, 16, 1.6), (2000, 1071, 3, 32, 1.4), (800, 462, 3, 128, 1.3),
+            (1920, 831, 3, 64, 1.3), (1280, 576, 3, 96, 1.25), (640, 320, 3, 256, 1.5), (500, 256, 3, 256, 1.46484375),
+            (1920, 450, 3, 64, 2.4), (1920, 675, 4, 64, 1.6), (1024, 768, 4, 128, 1.3333333333333333),
+            (1000, 480, 3, 128, 1.5625), (4000, 1500, 3, 8, 1.9))]
+    if os.environ.get("RS_SHAPES"):  # "w,h,b,n,hs,vs;..."
+        SHAPES = [tuple(float(t) if "." in t else int(t) for t in sh.split(",")) for sh in os.environ["RS_SHAPES"].split(";")]
+    extra = [dict(kv.split("=") for kv in v.split(",")) for v in args]
     variants = extra or VARIANTS
     dev = torch.device("cuda", 0)
     check(lib.mipx_set_device(0))

@@ -340,25 +340,27 @@ def test_reducev_paths(gpu, oracle, rng, monkeypatch, path, s):
         assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract {path}")
 
 
-@pytest.mark.parametrize("pack3", ["1", "0"])
-@pytest.mark.parametrize("fast", ["1", "0"])
-@pytest.mark.parametrize("s", [1.02, 1.3333333333333333, 1.6, 2.4, 2.7, 3.7])
-def test_reduceh_paths(gpu, oracle, rng, monkeypatch, fast, pack3, s):
-    """Horizontal reduce kernels: k_hreduce (compile-time tap pairs, RGB / RGBA,
-    default up to 16 taps) and k_hpass (MIPX_HP_FAST=0, and 1 / 2 bands, longer
-    masks): RGBA rows 16- / 4-byte aligned and unaligned (DW 16 / 4 / 0), RGB with
-    and without the 3-dword group stores (MIPX_HP_PACK3), rows that end inside a
-    4-pixel group, several column blocks, windowed plans (reduce -> extract)."""
-    monkeypatch.setenv("MIPX_HP_FAST", fast)
+@pytest.mark.parametrize("kernel,pack3", [("mfma", "0"), ("hreduce", "0"), ("hreduce", "1"), ("hpass", "0"),
+                                          ("hpass", "1")])
+@pytest.mark.parametrize("s", [1.02, 1.3333333333333333, 1.6, 2.4, 2.7, 3.7, 6.3])
+def test_reduceh_paths(gpu, oracle, rng, monkeypatch, kernel, pack3, s):
+    """Horizontal reduce kernels: k_hmfma (i8 MFMA, RGB / RGBA, an A/B variant behind
+    MIPX_HP_MFMA=1), k_hreduce (default: compile-time tap pairs, up to 16 taps) and k_hpass
+    (MIPX_HP_FAST=0 as well, and 1 / 2 bands, longer masks): RGBA rows 16- / 4-byte
+    aligned and unaligned (DW 16 / 4 / 0), RGB with and without the 3-dword group
+    stores (MIPX_HP_PACK3), rows that end inside a 4-pixel group, images narrower
+    than a group, several column blocks, windowed plans (reduce -> extract)."""
+    monkeypatch.setenv("MIPX_HP_MFMA", "1" if kernel == "mfma" else "0")
+    monkeypatch.setenv("MIPX_HP_FAST", "0" if kernel == "hpass" else "1")
     monkeypatch.setenv("MIPX_HP_PACK3", pack3)
     monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
     monkeypatch.setenv("MIPX_RSTRIP", "0")
     for h, w, b in ((19, 1100, 4), (23, 1027, 4), (21, 641, 3), (17, 2000, 3), (9, 64, 3), (5, 13, 4), (11, 301, 2),
-                    (7, 250, 1)):
+                    (7, 250, 1), (40, 333, 3), (33, 7, 3), (3, 7, 4)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
         gh = gpu.run_op("reduceh", imgs, hshrink=s)
         for i in range(3):
-            assert_same(gh[i], oracle.reduceh(imgs[i], s), f"reduceh {s} {h}x{w}x{b} fast={fast} pack3={pack3} img{i}")
+            assert_same(gh[i], oracle.reduceh(imgs[i], s), f"reduceh {s} {h}x{w}x{b} {kernel} pack3={pack3} img{i}")
     for b in (3, 4):
         opts = dict(width=333, height=120, crop=1, gravity=2)  # east: window column offset
         p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(1500, 400, b, "png"))
@@ -367,7 +369,7 @@ def test_reduceh_paths(gpu, oracle, rng, monkeypatch, fast, pack3, s):
         imgs = rng.integers(0, 256, (2, 400, 1500, b), dtype=np.uint8)
         got = gpu.execute(p, imgs)
         for i in range(2):
-            assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract b={b} fast={fast}")
+            assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract b={b} {kernel}")
 
 
 @pytest.mark.parametrize("rows", ["1", "8", "13"])
