@@ -7,7 +7,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; OUT="$R/gpurun_out"; mkdir -p "$OUT"; export TMPDIR=/tmp
 TAG=${TAG:-m}
 KERNEL=${KERNEL:-k_reduce2x2<3, 66>}
-SKIP_TESTS=0 SKIP_BENCH=0 SKIP_PROF=0 TAG=$TAG PYTEST_ARGS="--timeout 120 --timeout-method thread" bash scripts/gpu_round.sh || exit $?
+SKIP_TESTS=${SKIP_TESTS:-0} SKIP_BENCH=0 SKIP_PROF=0 TAG=$TAG PYTEST_ARGS="--timeout 120 --timeout-method thread" bash scripts/gpu_round.sh || exit $?
 TAG=$TAG PMC_LIST=$'FETCH_SIZE\nWRITE_SIZE' bash scripts/pmc.sh || exit $?
 ALG_BYTES=7962624000 timeout -k 5 60 python3 scripts/traffic_json.py "$OUT/pmc_$TAG" "$KERNEL" "$OUT/traffic_$TAG.json" \
     "256 x 3840x2160x3 -> 1920x1080x3" || exit $?
