@@ -104,11 +104,36 @@ def test_request_api_before_init():
     assert ia.lib.mipx_stats(0, C.byref(t), C.byref(t)) in (-7, -1, 0)
 
 
+def _ashr_pk_feeds(dis: str):
+    """For every v_ashr_pk_u8_i32 in a disassembly, the mnemonic of the first later
+    instruction that reads its destination (None when it is overwritten or unused)."""
+    import re
+    lines = [l.split(";")[0].strip() for l in dis.splitlines()]
+    lines = [l for l in lines if re.match(r"^[sv]_|^ds_|^buffer_|^global_", l)]
+    out = []
+    for i, l in enumerate(lines):
+        if not l.startswith("v_ashr_pk_u8_i32"):
+            continue
+        dst = l.split()[1].rstrip(",")
+        use = None
+        for m in lines[i + 1:i + 200]:
+            parts = m.replace(",", " ").split()
+            if dst in parts[2:]:
+                use = parts[0]
+                break
+            if len(parts) > 1 and parts[1] == dst:
+                break
+        out.append(use)
+    return out
+
+
 def test_code_object_avoids_known_bad_gfx950_fusion(tmp_path):
     """The gfx950 backend can fuse shift + clamp + byte packing into
-    v_ashr_pk_u8_i32 and then treat its unwritten upper half as zero (a
-    channel-2 error found by the whole-plan fuzz).  k_sep.hip guards against it;
-    this keeps any kernel from reintroducing the instruction."""
+    v_ashr_pk_u8_i32 and then OR the next channels into its unwritten upper half
+    as if it were zero (a channel-2 error found by the whole-plan fuzz).
+    fixed_round_i keeps the backend from fusing; round_pack4 uses the instruction
+    on purpose and joins the two 16-bit halves with v_perm_b32.  So every
+    v_ashr_pk_u8_i32 in the shipped code must feed a v_perm_b32, never an OR."""
     import shutil
     import imaginary_amd as ia
     objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
@@ -123,7 +148,9 @@ def test_code_object_avoids_known_bad_gfx950_fusion(tmp_path):
     for p in objs:
         dis = subprocess.run([objdump, "-d", "--mcpu=gfx950", str(p)], check=True, capture_output=True, text=True).stdout
         seen_dot2 |= "v_dot2_i32_i16" in dis or "v_dot2c_i32_i16" in dis
-        assert "v_ashr_pk_u8_i32" not in dis, f"{p.name}: v_ashr_pk_u8_i32 present"
+        feeds = _ashr_pk_feeds(dis)
+        bad = [f for f in feeds if f not in ("v_perm_b32", None)]
+        assert not bad, f"{p.name}: v_ashr_pk_u8_i32 feeding {sorted(set(bad))}"
     assert seen_dot2, "disassembly lacks the reduce passes' dot2 (extraction failed?)"
 
 
