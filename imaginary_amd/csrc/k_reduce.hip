@@ -414,6 +414,8 @@ int reduce_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     if (vs > 1.0 && hs > 1.0) {
         const int se = reduce_strip_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
         if (se != MIPX_EUNSUPPORTED) return se;
+        const int me = reduce_mfma_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
+        if (me != MIPX_EUNSUPPORTED) return me;
         const int fe = reduce_fused_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
         if (fe != MIPX_EUNSUPPORTED) return fe;
         const int f2 = reduce2d_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);

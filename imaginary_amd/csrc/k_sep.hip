@@ -1243,6 +1243,212 @@ __global__ void __launch_bounds__(256) k_hmfma(HmArgs a) {
     }
 }
 
+// ===========================================================================
+// fused reduce: vertical dot2 pass into channel-planar LDS, horizontal pass on
+// the matrix cores (k_rmfma)
+// ===========================================================================
+// A block = 128 output pixels x 16 output rows of one RGB image.  The input rows
+// the 16 rows need are DMA'd to LDS from byte 3 * org (org = the block's first tap
+// pixel floored to 16, so every 4-pixel quad is 3 aligned dwords); each wave then
+// computes 4 intermediate rows (reducev: k_vreduce's dot2 sums, rounding and
+// clamping) quad by quad, deinterleaves them to channel planes as pixel - 128
+// (the MFMA's signed i8), and after one barrier the horizontal pass runs as in
+// k_hmfma: no intermediate in HBM, and the horizontal products off the VALU.
+// Rows must be dword aligned (3 w % 4 == 0, aligned batch); taps <= 16 each way.
+constexpr int kRmRows = 16;
+constexpr int kRmXW = 128;
+
+struct RmArgs {
+    const u8 *in;
+    u8 *out;
+    int w, h, ox0, oy0, ow, oh;
+    long long in_img, out_img;
+    int x_blocks, y_blocks;
+    int lrows;    // staged input rows per block (>= 15 vs + vtaps)
+    int rs;       // LDS dwords per staged row (DMA chunks of 64)
+    int plane_w;  // bytes per channel plane row (multiple of 16)
+    int row_w;    // bytes per intermediate row (3 planes; / 16 odd)
+    int nks;      // 64-pixel K steps per horizontal group
+    const uint32_t *vpairs;  // device_reduce_pairs(vs): [129][2][tpav]
+    int tpav;
+    const signed char *tab;  // device_reduce_i8(hs)
+    const int *tsum;
+    SepTaps tv, th;
+};
+
+// RS: LDS dwords per staged row (compile time, so row offsets are immediates)
+template <int TV, int RS>
+__global__ void __launch_bounds__(256) k_rmfma(RmArgs a) {
+    constexpr int B = 3, XW = kRmXW, GPW = XW / 64;
+    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
+    int *ps = reinterpret_cast<int *>(rsm);  // [XW] horizontal: first tap pixel
+    int *pph = ps + XW;                      // [XW] phase
+    int *pbias = pph + XW;                   // [XW] 128 * tap sum + 2048
+    int *vso = pbias + XW;                   // [kRmRows] vertical: first staged row of each output row
+    uint32_t *vcp = reinterpret_cast<uint32_t *>(vso + kRmRows);  // [kRmRows][8] vertical tap pairs
+    u8 *planes = reinterpret_cast<u8 *>(vcp + kRmRows * 8);      // [kRmRows][row_w]
+    uint32_t *raw = reinterpret_cast<uint32_t *>(planes + kRmRows * a.row_w + 64);  // [lrows][RS]
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int yb = rest % a.y_blocks;
+    const int img = rest / a.y_blocks;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int x0 = xb * XW, x_last = min(x0 + XW - 1, a.ow - 1);
+    const int y0 = yb * kRmRows, nr = min(kRmRows, a.oh - y0);
+    int lo, hi, ph0, r_lo, r_last;
+    sep_position(a.th, a.ox0 + x0, &lo, &ph0);
+    sep_position(a.th, a.ox0 + x_last, &hi, &ph0);
+    hi += a.th.taps - 1;
+    sep_position(a.tv, a.oy0 + y0, &r_lo, &ph0);
+    sep_position(a.tv, a.oy0 + y0 + nr - 1, &r_last, &ph0);
+    const int org = lo & ~15;
+    const int nqv = ((hi - org) >> 2) + 1;  // quads holding horizontal taps
+    const int L = r_last + a.tv.taps - r_lo;
+    // ---- input rows [r_lo, r_lo + L) (COPY-clamped), bytes from 3 org, all in flight ----
+    {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
+        const int pitch = a.w * B;
+        const int chunks = (3 * nqv + 63) >> 6;
+        for (int l = wave; l < L; l += 4) {
+            const int r = clampi(r_lo + l, 0, a.h - 1);
+            for (int c = 0; c < chunks; ++c)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
+                                                         3 * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
+        }
+    }
+    if (tid < XW) {
+        int sp, ph;
+        sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
+        ps[tid] = sp;
+        pph[tid] = ph;
+        pbias[tid] = 128 * a.tsum[ph] + 2048;
+    } else if (tid < XW + kRmRows * 8) {
+        const int i = tid - XW, k = i >> 3, m = i & 7;
+        int sv, ph;
+        sep_position(a.tv, a.oy0 + y0 + min(k, nr - 1), &sv, &ph);
+        vcp[i] = m < a.tpav ? a.vpairs[(ph * 2) * a.tpav + m] : 0u;
+        if (m == 0) vso[k] = sv - r_lo;
+    }
+    __syncthreads();
+    // ---- vertical pass: wave w makes intermediate rows w, w + 4, ... as channel planes ----
+    for (int k = wave; k < nr; k += 4) {
+        const uint32_t *rk = raw + __builtin_amdgcn_readfirstlane(vso[k]) * RS;
+        const uint4 c0 = reinterpret_cast<const uint4 *>(vcp + k * 8)[0];
+        const uint4 c1 = reinterpret_cast<const uint4 *>(vcp + k * 8)[1];
+        const uint32_t cw[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        u8 *pl = planes + k * a.row_w;
+        for (int q = lane; q < nqv; q += 64) {
+            const uint32_t *rp = rk + 3 * q;
+            uint32_t v[2 * TV][3];  // every staged row's 3 dwords requested before the first sum
+#pragma unroll
+            for (int i = 0; i < 2 * TV; ++i)
+#pragma unroll
+                for (int d = 0; d < 3; ++d) v[i][d] = rp[i * RS + d];
+            int acc[12];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) acc[i] = 2048;
+#pragma unroll
+            for (int m = 0; m < TV; ++m)
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+#pragma unroll
+                    for (int z = 0; z < 4; ++z)
+                        acc[4 * d + z] = dot2_byte(v[2 * m][d], v[2 * m + 1][d], z, cw[m], acc[4 * d + z]);
+            uint32_t x[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) x[d] = round_pack4(acc[4 * d], acc[4 * d + 1], acc[4 * d + 2], acc[4 * d + 3]);
+            // [r0 g0 b0 r1] [g1 b1 r2 g2] [b2 r3 g3 b3] -> R, G, B planes
+            const uint32_t wr = __builtin_amdgcn_perm(x[2], __builtin_amdgcn_perm(x[1], x[0], 0x0c060300u), 0x05020100u);
+            const uint32_t wg = __builtin_amdgcn_perm(x[2], __builtin_amdgcn_perm(x[1], x[0], 0x0c070401u), 0x06020100u);
+            const uint32_t wb = __builtin_amdgcn_perm(x[2], __builtin_amdgcn_perm(x[1], x[0], 0x0c0c0502u), 0x07040100u);
+            reinterpret_cast<uint32_t *>(pl)[q] = wr ^ 0x80808080u;
+            reinterpret_cast<uint32_t *>(pl + a.plane_w)[q] = wg ^ 0x80808080u;
+            reinterpret_cast<uint32_t *>(pl + 2 * a.plane_w)[q] = wb ^ 0x80808080u;
+        }
+    }
+    __syncthreads();
+    // ---- COPY edge of the horizontal pass: pixels outside the image repeat its edge ----
+    if (lo < 0 || hi >= a.w) {
+        for (int i = tid; i < nr * (hi - org + 1); i += 256) {
+            const int k = i / (hi - org + 1), pq = i - k * (hi - org + 1);
+            const int p = org + pq;
+            if (p >= 0 && p < a.w) continue;
+            const int src = clampi(p, 0, a.w - 1) - org;
+#pragma unroll
+            for (int z = 0; z < B; ++z) planes[k * a.row_w + z * a.plane_w + pq] = planes[k * a.row_w + z * a.plane_w + src];
+        }
+        __syncthreads();
+    }
+    // ---- horizontal pass on the matrix cores (k_hmfma's group loop) ----
+    const int n = lane & 15, kg = lane >> 4;
+    u8 *ob = a.out + img * a.out_img;
+    u8 *tile = reinterpret_cast<u8 *>(raw);  // output tile [kRmRows][XW * 3 + 4] (the staged rows are dead)
+    __syncthreads();
+#pragma unroll
+    for (int gi = 0; gi < GPW; ++gi) {
+        const int g = wave * GPW + gi;
+        if (x0 + 16 * g > x_last) break;
+        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
+        const int p = min(16 * g + n, x_last - x0);
+        const int o0 = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
+        const signed char *thr = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
+        const int4 bias = *reinterpret_cast<const int4 *>(pbias + 16 * g + 4 * kg);
+        hm_v4i acc_h[B], acc_l[B];
+#pragma unroll
+        for (int z = 0; z < B; ++z) {
+            acc_h[z] = hm_v4i{0, 0, 0, 0};
+            acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
+        }
+        for (int ks = 0; ks < a.nks; ++ks) {
+            const hm_v4i ah = load_taps16(thr, o0 + 64 * ks);
+            const hm_v4i al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
+#pragma unroll
+            for (int z = 0; z < B; ++z) {
+                const hm_v4i bz =
+                    *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 64 * ks + 16 * kg);
+                acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bz, acc_h[z], 0, 0, 0);
+                acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bz, acc_l[z], 0, 0, 0);
+            }
+        }
+        uint32_t wz[3];
+#pragma unroll
+        for (int z = 0; z < B; ++z)
+            wz[z] = round_pack4((acc_h[z][0] << 6) + acc_l[z][0], (acc_h[z][1] << 6) + acc_l[z][1],
+                                (acc_h[z][2] << 6) + acc_l[z][2], (acc_h[z][3] << 6) + acc_l[z][3]);
+        const int x = x0 + 16 * g + 4 * kg;
+        if (n >= nr || x > x_last) continue;
+        uint32_t *tq = reinterpret_cast<uint32_t *>(tile + n * (XW * 3 + 4) + (x - x0) * 3);
+        tq[0] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
+        tq[1] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
+        tq[2] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
+    }
+    __syncthreads();
+    // ---- each tile row to its output row as whole dwords at the row's own alignment ----
+    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
+    const int nb = (x_last - x0 + 1) * 3;
+    for (int r = wave; r < nr; r += 4) {
+        const u8 *tr = tile + r * (XW * 3 + 4);
+        const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
+        const int qo0 = ((y0 + r) * a.ow + x0) * 3 + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+        const int d0 = qo0 >> 2, nd = ((qo0 + nb + 3) >> 2) - d0;
+        const int sh = (4 - (qo0 & 3)) & 3;
+        const int bias0 = static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+        for (int i = lane; i < nd; i += 64) {
+            const int e = 4 * (d0 + i) - qo0;
+            if (e >= 0 && e + 4 <= nb) {
+                const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
+                __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i) - bias0, 0, 0);
+            } else {
+                for (int k = 0; k < 4; ++k)
+                    if (e + k >= 0 && e + k < nb)
+                        __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
+            }
+        }
+    }
+}
+
 template <int B>
 __global__ void __launch_bounds__(256) k_hpass_gather(HPassArgs a) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1883,6 +2089,73 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
 #undef MIPX_HPW
 #undef MIPX_HP3
     return launch_check("k_hpass");
+}
+
+// Fused reduce with the horizontal pass on the matrix cores (k_rmfma): RGB with
+// dword-aligned rows, <= 16 taps each way; MIPX_EUNSUPPORTED otherwise (the caller
+// runs another path).  An A/B variant behind MIPX_RMFMA=1: bit-exact, but 1-20 %
+// slower than k_vreduce + k_hreduce (profiles/r02/rmfma_ab.jsonl) -- its VALU
+// vertical pass over the block's halo costs more than the intermediate it saves.
+int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
+                       int ow, int oh, hipStream_t st) {
+    const char *e = std::getenv("MIPX_RMFMA");
+    if (!(e && *e == '1')) return MIPX_EUNSUPPORTED;
+    const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
+    if (b != 3 || !(hs > 1.0) || !(vs > 1.0) || (w * 3) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0 ||
+        in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL)
+        return MIPX_EUNSUPPORTED;
+    SepSpec sh, sv;
+    if (!sep_spec_reduce(hs, &sh) || !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
+    if (sh.taps > 16 || sv.taps > 16) return MIPX_EUNSUPPORTED;
+    RmArgs a{};
+    a.in = in;
+    a.out = out;
+    a.w = w;
+    a.h = h;
+    a.ox0 = ox0;
+    a.oy0 = oy0;
+    a.ow = ow;
+    a.oh = oh;
+    a.in_img = in_img;
+    a.out_img = out_img;
+    a.th = make_taps(sh);
+    a.tv = make_taps(sv);
+    int nt = 0;
+    a.vpairs = device_reduce_pairs(vs, &nt, &a.tpav);
+    if (!a.vpairs || nt != sv.taps) return MIPX_EDEVICE;
+    a.tab = device_reduce_i8(hs, &nt, &a.tsum);
+    if (!a.tab || nt != sh.taps) return MIPX_EDEVICE;
+    a.x_blocks = (ow + kRmXW - 1) / kRmXW;
+    a.y_blocks = (oh + kRmRows - 1) / kRmRows;
+    a.lrows = static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps + 2;
+    const int span = static_cast<int>(std::ceil((kRmXW - 1) * hs)) + sh.taps + 16;  // >= hi - org + 1
+    a.rs = ((3 * (span / 4 + 1) + 63) / 64) * 64;
+    if (a.rs < 192) a.rs = 192;
+    if (a.rs > 256) return MIPX_EUNSUPPORTED;
+    a.plane_w = (span + 15) & ~15;
+    a.row_w = 3 * a.plane_w + ((3 * a.plane_w / 16) % 2 == 0 ? 16 : 0);
+    a.nks = (static_cast<int>(std::ceil(15 * hs)) + sh.taps + 16 + 63) / 64;
+    const size_t lds = static_cast<size_t>(3 * kRmXW + kRmRows + kRmRows * 8) * 4 +
+                       static_cast<size_t>(kRmRows) * a.row_w + 64 + static_cast<size_t>(a.lrows) * a.rs * 4;
+    if (lds > 64 * 1024 || a.nks > 4 || static_cast<size_t>(kRmRows) * (kRmXW * 3 + 4) > static_cast<size_t>(a.lrows) * a.rs * 4)
+        return MIPX_EUNSUPPORTED;
+    const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
+    if (!grid_ok(blocks)) return MIPX_EINVAL;
+    const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
+#define MIPX_RM(RS_)                                                                                    \
+    switch ((sv.taps + 1) / 2) {                                                                        \
+        case 2: hipLaunchKernelGGL((k_rmfma<2, RS_>), grid, blk, lds, st, a); break;                    \
+        case 3: hipLaunchKernelGGL((k_rmfma<3, RS_>), grid, blk, lds, st, a); break;                    \
+        case 4: hipLaunchKernelGGL((k_rmfma<4, RS_>), grid, blk, lds, st, a); break;                    \
+        case 5: hipLaunchKernelGGL((k_rmfma<5, RS_>), grid, blk, lds, st, a); break;                    \
+        case 6: hipLaunchKernelGGL((k_rmfma<6, RS_>), grid, blk, lds, st, a); break;                    \
+        case 7: hipLaunchKernelGGL((k_rmfma<7, RS_>), grid, blk, lds, st, a); break;                    \
+        default: hipLaunchKernelGGL((k_rmfma<8, RS_>), grid, blk, lds, st, a); break;                   \
+    }
+    if (a.rs == 192) { MIPX_RM(192) }
+    else { MIPX_RM(256) }
+#undef MIPX_RM
+    return launch_check("k_rmfma");
 }
 
 // Fused reducev -> reduceh of the output window [ox0, ox0 + ow) x [oy0, oy0 + oh);

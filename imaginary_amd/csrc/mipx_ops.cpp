@@ -69,6 +69,9 @@ int mipx_op_reduce(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, in
         const int es = reduce_strip_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
                                            out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
         if (es != MIPX_EUNSUPPORTED) return es;
+        const int em = reduce_mfma_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
+                                          out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
+        if (em != MIPX_EUNSUPPORTED) return em;
         const int e = reduce_fused_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
                                           out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
         if (e != MIPX_EUNSUPPORTED) return e;

@@ -372,6 +372,35 @@ def test_reduceh_paths(gpu, oracle, rng, monkeypatch, kernel, pack3, s):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract b={b} {kernel}")
 
 
+@pytest.mark.parametrize("on", ["1", "0"])
+@pytest.mark.parametrize("hs,vs", [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9),
+                                   (2.7, 1.5), (1.46484375, 1.46484375), (1.1, 1.05)])
+def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
+    """k_rmfma (vertical dot2 pass into channel-planar LDS, horizontal pass on the i8
+    matrix cores, one launch) against the oracle: RGB with dword-aligned rows, blocks
+    at both image edges, images narrower than a block and shorter than 16 rows, many
+    row and column blocks, windowed plans (reduce -> extract), and the cases it leaves
+    to other kernels (17 taps, unaligned rows).  It is an A/B variant (MIPX_RMFMA=1);
+    MIPX_RMFMA=0 runs the default kernels on the same cases."""
+    monkeypatch.setenv("MIPX_RMFMA", on)
+    monkeypatch.setenv("MIPX_RSTRIP", "0")
+    monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
+    for h, w in ((301, 1100), (97, 640), (13, 200), (40, 36), (270, 480), (37, 1026), (150, 97)):
+        imgs = np.stack([rand_img(rng, h, w, 3), smooth_img(rng, h, w, 3)])
+        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+        for i in range(2):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"rmfma={on} {h}x{w} {hs}x{vs} img{i}")
+    for g in (0, 2, 3):
+        opts = dict(width=333, height=171, crop=1, gravity=g)
+        p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(1500, 1000, 3, "png"))
+        e, rp = oracle.plan(opts, dict(w=1500, h=1000, bands=3, type=3))
+        assert e == 0
+        imgs = rng.integers(0, 256, (2, 1000, 1500, 3), dtype=np.uint8)
+        got = gpu.execute(p, imgs)
+        for i in range(2):
+            assert_same(got[i], oracle.execute(rp, imgs[i]), f"rmfma={on} window gravity {g}")
+
+
 @pytest.mark.parametrize("rows", ["1", "8", "13"])
 def test_reduce2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows):
     """Fused generic reduce (k_reduce2d, an A/B variant behind MIPX_REDUCE2D=1:
