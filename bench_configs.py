@@ -215,6 +215,26 @@ def e2e(args, dev, sp, stream):
         eng.shutdown()
 
 
+def e2e_c(args, dev, sp, stream):
+    """The same request path driven from C (tests/c/mipx_e2e.c: caller threads with
+    requests in flight over pre-faulted buffers, no Python between the callers and
+    the engine), built with gcc and run as a child process; prints its JSON line."""
+    import subprocess
+    import tempfile
+    root = os.path.dirname(os.path.abspath(__file__))
+    exe = os.path.join(tempfile.mkdtemp(), "mipx_e2e")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-D_DEFAULT_SOURCE", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "c", "mipx_e2e.c"), "-L", os.path.join(root, "imaginary_amd"),
+                    "-lmipx", "-lpthread", "-Wl,-rpath," + os.path.join(root, "imaginary_amd"), "-o", exe], check=True)
+    r = subprocess.run([exe, str(args.e2e_threads), str(max(1, args.e2e_requests * 4 // args.e2e_threads)),
+                        str(args.e2e_queues), "2", str(args.e2e_batch // 2)],
+                       capture_output=True, text=True, timeout=300)
+    sys.stdout.write(r.stdout)
+    sys.stdout.flush()
+    if r.returncode != 0:
+        raise RuntimeError(f"mipx_e2e exit {r.returncode}: {r.stderr[-500:]}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="C3,C4,C5")
@@ -236,7 +256,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = C.c_void_p(stream.cuda_stream)
     for c in args.configs.split(","):
-        {"C3": c3, "C4": c4, "C5": c5, "E2E": e2e}[c](args, dev, sp, stream)
+        {"C3": c3, "C4": c4, "C5": c5, "E2E": e2e, "E2EC": e2e_c}[c](args, dev, sp, stream)
         torch.cuda.empty_cache()
 
 

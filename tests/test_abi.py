@@ -179,6 +179,20 @@ def build_c_client(dst):
     return exe
 
 
+def build_c_e2e(dst):
+    """gcc-compile tests/c/mipx_e2e.c (the request-path throughput benchmark from C)."""
+    exe = os.path.join(str(dst), "mipx_e2e")
+    subprocess.run(["gcc", "-O2", "-Wall", "-Wextra", "-Werror", "-std=c11", "-D_DEFAULT_SOURCE",
+                    "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "c", "mipx_e2e.c"),
+                    "-L", os.path.join(ROOT, "imaginary_amd"), "-lmipx", "-lpthread",
+                    "-Wl,-rpath," + os.path.join(ROOT, "imaginary_amd"), "-o", exe], check=True)
+    return exe
+
+
+def test_c_e2e_builds_against_the_header(tmp_path):
+    assert os.path.exists(build_c_e2e(tmp_path))
+
+
 def test_c_client_builds_against_the_header(tmp_path):
     exe = build_c_client(tmp_path)
     import imaginary_amd as ia
