@@ -1257,6 +1257,7 @@ __global__ void __launch_bounds__(256) k_hmfma(HmArgs a) {
 // Rows must be dword aligned (3 w % 4 == 0, aligned batch); taps <= 16 each way.
 constexpr int kRmRows = 16;
 constexpr int kRmXW = 128;
+constexpr int kRmMaxCt = 16;  // k_rmf2: 16-byte column tiles per wave (staged span <= 1024 bytes)
 
 struct RmArgs {
     const u8 *in;
@@ -1273,6 +1274,10 @@ struct RmArgs {
     int tpav;
     const signed char *tab;  // device_reduce_i8(hs)
     const int *tsum;
+    const signed char *tabv;  // k_rmf2: device_reduce_i8(vs)
+    const int *tsumv;
+    int iw;                   // k_rmf2: bytes per row-major intermediate row (16 x column tiles)
+    int direct;               // k_rmf2: output rows and images dword aligned (12-byte stores, no tile)
     SepTaps tv, th;
 };
 
@@ -1443,6 +1448,222 @@ __global__ void __launch_bounds__(256) k_rmfma(RmArgs a) {
             } else {
                 for (int k = 0; k < 4; ++k)
                     if (e + k >= 0 && e + k < nb)
+                        __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
+            }
+        }
+    }
+}
+
+// k_rmf2: the same fused reduce with the VERTICAL products on the matrix cores too.
+// Per 16-byte column tile of the staged rows: D[byte column][output row] =
+// A[byte column][staged row] x B[staged row][output row] on v_mfma_i32_16x16x64_i8,
+// where A (the pixels, K = 64 staged rows) comes from two ds_read_b64_tr_b8 (the
+// transposing LDS read: a 16-lane group's lanes name 8 rows x 2 half-rows, each
+// lane receives one byte column of those 8 rows; scripts/probe/ds_tr8_probe.hip)
+// and B is each output row's taps from the i8 table.  The lane then holds 4
+// consecutive intermediate bytes of one output row: one dword write into a
+// row-major intermediate, deinterleaved to channel planes for the horizontal MFMA.
+// Needs 15 vs + vtaps <= 64 staged rows.
+template <int RS>
+__global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
+    constexpr int B = 3, XW = kRmXW, GPW = XW / 64;
+    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
+    int *ps = reinterpret_cast<int *>(rsm);  // [XW] horizontal: first tap pixel
+    int *pph = ps + XW;                      // [XW] phase
+    int *pbias = pph + XW;                   // [XW] 128 * tap sum + 2048
+    int *vso = pbias + XW;                   // [kRmRows] vertical: first staged row of each output row
+    int *vph = vso + kRmRows;                // [kRmRows] phase
+    int *vbias = vph + kRmRows;              // [kRmRows] 128 * tap sum + 2048
+    // one region for the staged rows, then (aliased, barrier-separated) the row-major
+    // intermediate and the channel planes, then the output tile over the intermediate:
+    // 31 KB at / 1.6, so 5 workgroups share a CU
+    uint32_t *raw = reinterpret_cast<uint32_t *>(vbias + kRmRows);  // [lrows][RS]
+    u8 *inter = reinterpret_cast<u8 *>(raw);                         // [kRmRows][iw] (pixel - 128)
+    u8 *planes = inter + kRmRows * a.iw + 64;                        // [kRmRows][row_w] channel planes
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int yb = rest % a.y_blocks;
+    const int img = rest / a.y_blocks;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int x0 = xb * XW, x_last = min(x0 + XW - 1, a.ow - 1);
+    const int y0 = yb * kRmRows, nr = min(kRmRows, a.oh - y0);
+    int lo, hi, ph0, r_lo, r_last;
+    sep_position(a.th, a.ox0 + x0, &lo, &ph0);
+    sep_position(a.th, a.ox0 + x_last, &hi, &ph0);
+    hi += a.th.taps - 1;
+    sep_position(a.tv, a.oy0 + y0, &r_lo, &ph0);
+    sep_position(a.tv, a.oy0 + y0 + nr - 1, &r_last, &ph0);
+    const int org = lo & ~15;
+    const int nqv = ((hi - org) >> 2) + 1;
+    const int L = r_last + a.tv.taps - r_lo;
+    {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
+        const int pitch = a.w * B;
+        const int chunks = (3 * nqv + 63) >> 6;
+        for (int l = wave; l < L; l += 4) {
+            const int r = clampi(r_lo + l, 0, a.h - 1);
+            for (int c = 0; c < chunks; ++c)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
+                                                         3 * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
+        }
+    }
+    if (tid < XW) {
+        int sp, ph;
+        sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
+        ps[tid] = sp;
+        pph[tid] = ph;
+        pbias[tid] = 128 * a.tsum[ph] + 2048;
+    } else if (tid < XW + kRmRows) {
+        const int k = tid - XW;
+        int sv, ph;
+        sep_position(a.tv, a.oy0 + y0 + min(k, nr - 1), &sv, &ph);
+        vso[k] = sv - r_lo;
+        vph[k] = ph;
+        vbias[k] = 128 * a.tsumv[ph] + 2048;
+    }
+    __syncthreads();
+    // ---- vertical pass on the matrix cores, 16-byte column tiles dealt to the waves ----
+    {
+        const int n = lane & 15, kg = lane >> 4;
+        const signed char *tv = a.tabv + static_cast<size_t>(vph[n]) * 2 * kHmTabW;
+        const int ov = 16 * kg - vso[n] + kHmTabPad;
+        const hm_v4i bh = load_taps16(tv, ov), bl = load_taps16(tv + kHmTabW, ov);
+        const int vb = vbias[n];
+        const int nt = (3 * (hi - org + 1) + 15) >> 4;
+        const u8 *rawb = reinterpret_cast<const u8 *>(raw);
+        const int r1 = min(16 * kg + (n >> 1), L - 1), r2 = min(16 * kg + 8 + (n >> 1), L - 1);
+        uint32_t res[kRmMaxCt];  // this wave's tiles, written after every wave has read the staged rows
+#pragma unroll
+        for (int i = 0; i < kRmMaxCt; ++i) {
+            const int ct = wave + 4 * i;
+            if (ct >= nt) break;
+            const int cb = 16 * ct + 8 * (n & 1);
+            typedef int v2i_t __attribute__((ext_vector_type(2)));
+            const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+                (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r1 * RS * 4 + cb))));
+            const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+                (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r2 * RS * 4 + cb))));
+            const hm_v4i av = hm_v4i{t1.x ^ static_cast<int>(0x80808080u), t1.y ^ static_cast<int>(0x80808080u),
+                                     t2.x ^ static_cast<int>(0x80808080u), t2.y ^ static_cast<int>(0x80808080u)};
+            hm_v4i dh = hm_v4i{0, 0, 0, 0}, dl = hm_v4i{vb, vb, vb, vb};
+            dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
+            dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
+            const uint32_t w = round_pack4((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
+                                           (dh[3] << 6) + dl[3]);
+            res[i] = w ^ 0x80808080u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kRmMaxCt; ++i) {
+            const int ct = wave + 4 * i;
+            if (ct >= nt) break;
+            *reinterpret_cast<uint32_t *>(inter + n * a.iw + 16 * ct + 4 * kg) = res[i];
+        }
+    }
+    __syncthreads();
+    // ---- row-major intermediate -> channel planes, 4 pixels per item ----
+    for (int k = wave; k < nr; k += 4) {
+        const uint32_t *ir = reinterpret_cast<const uint32_t *>(inter + k * a.iw);
+        u8 *pl = planes + k * a.row_w;
+        for (int q = lane; q < nqv; q += 64) {
+            const uint32_t x0w = ir[3 * q], x1w = ir[3 * q + 1], x2w = ir[3 * q + 2];
+            reinterpret_cast<uint32_t *>(pl)[q] =
+                __builtin_amdgcn_perm(x2w, __builtin_amdgcn_perm(x1w, x0w, 0x0c060300u), 0x05020100u);
+            reinterpret_cast<uint32_t *>(pl + a.plane_w)[q] =
+                __builtin_amdgcn_perm(x2w, __builtin_amdgcn_perm(x1w, x0w, 0x0c070401u), 0x06020100u);
+            reinterpret_cast<uint32_t *>(pl + 2 * a.plane_w)[q] =
+                __builtin_amdgcn_perm(x2w, __builtin_amdgcn_perm(x1w, x0w, 0x0c0c0502u), 0x07040100u);
+        }
+    }
+    __syncthreads();
+    // ---- COPY edge of the horizontal pass: pixels outside the image repeat its edge ----
+    if (lo < 0 || hi >= a.w) {
+        for (int i = tid; i < nr * (hi - org + 1); i += 256) {
+            const int k = i / (hi - org + 1), pq = i - k * (hi - org + 1);
+            const int p = org + pq;
+            if (p >= 0 && p < a.w) continue;
+            const int src = clampi(p, 0, a.w - 1) - org;
+#pragma unroll
+            for (int z = 0; z < B; ++z) planes[k * a.row_w + z * a.plane_w + pq] = planes[k * a.row_w + z * a.plane_w + src];
+        }
+        __syncthreads();
+    }
+    // ---- horizontal pass on the matrix cores (k_hmfma's group loop) ----
+    const int n = lane & 15, kg = lane >> 4;
+    u8 *ob = a.out + img * a.out_img;
+    u8 *tile = inter;  // output tile [kRmRows][XW * 3 + 4] over the intermediate (dead after the deinterleave)
+    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
+    __syncthreads();
+#pragma unroll
+    for (int gi = 0; gi < GPW; ++gi) {
+        const int g = wave * GPW + gi;
+        if (x0 + 16 * g > x_last) break;
+        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
+        const int p = min(16 * g + n, x_last - x0);
+        const int o0 = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
+        const signed char *thr = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
+        const int4 bias = *reinterpret_cast<const int4 *>(pbias + 16 * g + 4 * kg);
+        hm_v4i acc_h[B], acc_l[B];
+#pragma unroll
+        for (int z = 0; z < B; ++z) {
+            acc_h[z] = hm_v4i{0, 0, 0, 0};
+            acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
+        }
+        for (int ks = 0; ks < a.nks; ++ks) {
+            const hm_v4i ah = load_taps16(thr, o0 + 64 * ks);
+            const hm_v4i al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
+#pragma unroll
+            for (int z = 0; z < B; ++z) {
+                const hm_v4i bz =
+                    *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 64 * ks + 16 * kg);
+                acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bz, acc_h[z], 0, 0, 0);
+                acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bz, acc_l[z], 0, 0, 0);
+            }
+        }
+        uint32_t wz[3];
+#pragma unroll
+        for (int z = 0; z < B; ++z)
+            wz[z] = round_pack4((acc_h[z][0] << 6) + acc_l[z][0], (acc_h[z][1] << 6) + acc_l[z][1],
+                                (acc_h[z][2] << 6) + acc_l[z][2], (acc_h[z][3] << 6) + acc_l[z][3]);
+        const int x = x0 + 16 * g + 4 * kg;
+        if (n >= nr || x > x_last) continue;
+        const uint32_t w0 = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
+        const uint32_t w1 = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
+        const uint32_t w2 = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
+        if (a.direct && x + 3 <= x_last) {  // dword-aligned output rows: the lane's 12 bytes in one store
+            typedef int v3i_t __attribute__((ext_vector_type(3)));
+            __builtin_amdgcn_raw_buffer_store_b96(v3i_t{static_cast<int>(w0), static_cast<int>(w1), static_cast<int>(w2)},
+                                                  os, ((y0 + n) * a.ow + x) * 3, 0, 0);
+            continue;
+        }
+        uint32_t *tq = reinterpret_cast<uint32_t *>(tile + n * (XW * 3 + 4) + (x - x0) * 3);
+        tq[0] = w0;
+        tq[1] = w1;
+        tq[2] = w2;
+    }
+    __syncthreads();
+    // ---- each tile row to its output row as whole dwords at the row's own alignment ----
+    // (direct mode: only the partial last group of the row's last block went through the tile)
+    const int nb = (x_last - x0 + 1) * 3;
+    const int tb = a.direct ? ((x_last - x0 + 1) & ~3) * 3 : 0;  // tile bytes already stored
+    for (int r = wave; r < nr && tb < nb; r += 4) {
+        const u8 *tr = tile + r * (XW * 3 + 4);
+        const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
+        const int qo0 = ((y0 + r) * a.ow + x0) * 3 + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+        const int d0 = qo0 >> 2, nd = ((qo0 + nb + 3) >> 2) - d0;
+        const int sh = (4 - (qo0 & 3)) & 3;
+        const int bias0 = static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+        for (int i = lane; i < nd; i += 64) {
+            const int e = 4 * (d0 + i) - qo0;
+            if (e + 4 <= tb) continue;
+            if (e >= tb && e + 4 <= nb) {
+                const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
+                __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i) - bias0, 0, 0);
+            } else {
+                for (int k = 0; k < 4; ++k)
+                    if (e + k >= tb && e + k < nb)
                         __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
             }
         }
@@ -2098,8 +2319,9 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
 // vertical pass over the block's halo costs more than the intermediate it saves.
 int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
                        int ow, int oh, hipStream_t st) {
-    const char *e = std::getenv("MIPX_RMFMA");
-    if (!(e && *e == '1')) return MIPX_EUNSUPPORTED;
+    const char *e = std::getenv("MIPX_RMFMA");  // 1: k_rmfma (VALU vertical), 2: k_rmf2 (MFMA vertical)
+    if (!(e && (*e == '1' || *e == '2'))) return MIPX_EUNSUPPORTED;
+    const bool v2 = *e == '2';
     const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
     if (b != 3 || !(hs > 1.0) || !(vs > 1.0) || (w * 3) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0 ||
         in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL)
@@ -2125,6 +2347,10 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
     if (!a.vpairs || nt != sv.taps) return MIPX_EDEVICE;
     a.tab = device_reduce_i8(hs, &nt, &a.tsum);
     if (!a.tab || nt != sh.taps) return MIPX_EDEVICE;
+    if (v2) {
+        a.tabv = device_reduce_i8(vs, &nt, &a.tsumv);
+        if (!a.tabv || nt != sv.taps) return MIPX_EDEVICE;
+    }
     a.x_blocks = (ow + kRmXW - 1) / kRmXW;
     a.y_blocks = (oh + kRmRows - 1) / kRmRows;
     a.lrows = static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps + 2;
@@ -2135,9 +2361,13 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
     a.plane_w = (span + 15) & ~15;
     a.row_w = 3 * a.plane_w + ((3 * a.plane_w / 16) % 2 == 0 ? 16 : 0);
     a.nks = (static_cast<int>(std::ceil(15 * hs)) + sh.taps + 16 + 63) / 64;
+    a.iw = ((3 * span + 15) & ~15) + 16;
+    if (v2 && (static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps > 64 || 4 * a.rs < a.iw))
+        return MIPX_EUNSUPPORTED;
     const size_t lds = static_cast<size_t>(3 * kRmXW + kRmRows + kRmRows * 8) * 4 +
                        static_cast<size_t>(kRmRows) * a.row_w + 64 + static_cast<size_t>(a.lrows) * a.rs * 4;
-    if (lds > 64 * 1024 || a.nks > 4 || static_cast<size_t>(kRmRows) * (kRmXW * 3 + 4) > static_cast<size_t>(a.lrows) * a.rs * 4)
+    if (a.nks > 4 || (!v2 && (lds > 64 * 1024 || static_cast<size_t>(kRmRows) * (kRmXW * 3 + 4) >
+                                                      static_cast<size_t>(a.lrows) * a.rs * 4)))
         return MIPX_EUNSUPPORTED;
     const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
@@ -2151,6 +2381,19 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         case 6: hipLaunchKernelGGL((k_rmfma<6, RS_>), grid, blk, lds, st, a); break;                    \
         case 7: hipLaunchKernelGGL((k_rmfma<7, RS_>), grid, blk, lds, st, a); break;                    \
         default: hipLaunchKernelGGL((k_rmfma<8, RS_>), grid, blk, lds, st, a); break;                   \
+    }
+    if (v2) {  // row stride = 4 (mod 64) dwords: a transposed read's 8 rows x 2 halves hit 16 distinct bank pairs
+        const int rs2 = a.rs + 4;
+        a.direct = (ow * 3) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
+        const size_t l2 = static_cast<size_t>(3 * kRmXW + 3 * kRmRows) * 4 +
+                          std::max(static_cast<size_t>(a.lrows) * rs2 * 4,
+                                   static_cast<size_t>(kRmRows) * (a.iw + a.row_w) + 64 + 16);
+        if (l2 > 64 * 1024 || 3 * span > 16 * 4 * kRmMaxCt || static_cast<size_t>(kRmRows) * (kRmXW * 3 + 4) >
+                                                                  static_cast<size_t>(kRmRows) * a.iw)
+            return MIPX_EUNSUPPORTED;
+        if (a.rs == 192) hipLaunchKernelGGL(k_rmf2<196>, grid, blk, l2, st, a);
+        else hipLaunchKernelGGL(k_rmf2<260>, grid, blk, l2, st, a);
+        return launch_check("k_rmf2");
     }
     if (a.rs == 192) { MIPX_RM(192) }
     else { MIPX_RM(256) }

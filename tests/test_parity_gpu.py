@@ -372,7 +372,7 @@ def test_reduceh_paths(gpu, oracle, rng, monkeypatch, kernel, pack3, s):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract b={b} {kernel}")
 
 
-@pytest.mark.parametrize("on", ["1", "0"])
+@pytest.mark.parametrize("on", ["2", "1", "0"])
 @pytest.mark.parametrize("hs,vs", [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9),
                                    (2.7, 1.5), (1.46484375, 1.46484375), (1.1, 1.05)])
 def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
