@@ -2312,16 +2312,20 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     return launch_check("k_hpass");
 }
 
-// Fused reduce with the horizontal pass on the matrix cores (k_rmfma): RGB with
+// Fused reduce on the matrix cores (k_rmf2, and the A/B variant k_rmfma with a VALU
+// vertical pass: bit-exact, but 1-20 % slower than the two passes -- its vertical
+// pass over the block's halo costs more than the intermediate it saves): RGB with
 // dword-aligned rows, <= 16 taps each way; MIPX_EUNSUPPORTED otherwise (the caller
-// runs another path).  An A/B variant behind MIPX_RMFMA=1: bit-exact, but 1-20 %
-// slower than k_vreduce + k_hreduce (profiles/r02/rmfma_ab.jsonl) -- its VALU
-// vertical pass over the block's halo costs more than the intermediate it saves.
+// runs another path).
 int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
                        int ow, int oh, hipStream_t st) {
-    const char *e = std::getenv("MIPX_RMFMA");  // 1: k_rmfma (VALU vertical), 2: k_rmf2 (MFMA vertical)
-    if (!(e && (*e == '1' || *e == '2'))) return MIPX_EUNSUPPORTED;
-    const bool v2 = *e == '2';
+    // default: k_rmf2 where its LDS leaves >= 4 workgroups per CU (rmfma_ab.jsonl: -10 to
+    // -35 % against the two passes there, slower at 2 workgroups); MIPX_RMFMA=0 off,
+    // 1 forces k_rmfma (VALU vertical pass, an A/B variant), 2 forces k_rmf2
+    const char *e = std::getenv("MIPX_RMFMA");
+    if (e && *e == '0') return MIPX_EUNSUPPORTED;
+    const bool forced = e && (*e == '1' || *e == '2');
+    const bool v2 = !forced || *e == '2';
     const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
     if (b != 3 || !(hs > 1.0) || !(vs > 1.0) || (w * 3) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0 ||
         in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL)
@@ -2388,8 +2392,8 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         const size_t l2 = static_cast<size_t>(3 * kRmXW + 3 * kRmRows) * 4 +
                           std::max(static_cast<size_t>(a.lrows) * rs2 * 4,
                                    static_cast<size_t>(kRmRows) * (a.iw + a.row_w) + 64 + 16);
-        if (l2 > 64 * 1024 || 3 * span > 16 * 4 * kRmMaxCt || static_cast<size_t>(kRmRows) * (kRmXW * 3 + 4) >
-                                                                  static_cast<size_t>(kRmRows) * a.iw)
+        if (l2 > (forced ? 64 : 40) * 1024 || 3 * span > 16 * 4 * kRmMaxCt ||
+            static_cast<size_t>(kRmRows) * (kRmXW * 3 + 4) > static_cast<size_t>(kRmRows) * a.iw)
             return MIPX_EUNSUPPORTED;
         if (a.rs == 192) hipLaunchKernelGGL(k_rmf2<196>, grid, blk, l2, st, a);
         else hipLaunchKernelGGL(k_rmf2<260>, grid, blk, l2, st, a);

@@ -91,6 +91,7 @@ def test_reduce_fused_and_two_pass_paths(gpu, oracle, rng, fused, monkeypatch):
     the small-image fused kernel off (k_reduce2d is off unless asked for)."""
     monkeypatch.setenv("MIPX_FUSED_REDUCE", fused)
     monkeypatch.setenv("MIPX_REDUCE2D", "0")
+    monkeypatch.setenv("MIPX_RMFMA", "0")  # k_rmf2 has its own test
     for h, w, b, hs, vs in ((240, 427, 3, 1.4233, 1.4233), (273, 364, 3, 1.421875, 1.06640625),
                             (97, 130, 4, 1.3333333333333333, 1.3333333333333333), (45, 61, 1, 2.9, 1.7),
                             (60, 90, 2, 1.05, 3.3), (300, 200, 3, 2.4666666666666666, 2.4666666666666666)):
@@ -372,7 +373,7 @@ def test_reduceh_paths(gpu, oracle, rng, monkeypatch, kernel, pack3, s):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract b={b} {kernel}")
 
 
-@pytest.mark.parametrize("on", ["2", "1", "0"])
+@pytest.mark.parametrize("on", ["", "2", "1", "0"])
 @pytest.mark.parametrize("hs,vs", [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9),
                                    (2.7, 1.5), (1.46484375, 1.46484375), (1.1, 1.05)])
 def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
@@ -409,6 +410,7 @@ def test_reduce2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows):
     taps; the small-image fused kernel is switched off so this path runs."""
     monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
     monkeypatch.setenv("MIPX_REDUCE2D", "1")  # A/B variant, off by default
+    monkeypatch.setenv("MIPX_RMFMA", "0")
     monkeypatch.setenv("MIPX_REDUCE2D_ROWS", rows)
     for h, w, b, hs, vs in ((41, 57, 1, 1.1, 1.1), (37, 43, 2, 1.3333333333333333, 1.6), (64, 90, 3, 1.6, 1.6),
                             (50, 128, 4, 2.5, 1.3333333333333333), (31, 17, 3, 1.3, 2.9), (40, 1100, 3, 1.3333333333333333, 1.4),
