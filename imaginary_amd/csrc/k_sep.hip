@@ -1464,9 +1464,9 @@ __global__ void __launch_bounds__(256) k_rmfma(RmArgs a) {
 // consecutive intermediate bytes of one output row: one dword write into a
 // row-major intermediate, deinterleaved to channel planes for the horizontal MFMA.
 // Needs 15 vs + vtaps <= 64 staged rows.
-template <int RS>
+template <int B, int RS>
 __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
-    constexpr int B = 3, XW = kRmXW, GPW = XW / 64;
+    constexpr int XW = kRmXW, GPW = XW / 64;
     extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
     int *ps = reinterpret_cast<int *>(rsm);  // [XW] horizontal: first tap pixel
     int *pph = ps + XW;                      // [XW] phase
@@ -1501,12 +1501,12 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     {
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
         const int pitch = a.w * B;
-        const int chunks = (3 * nqv + 63) >> 6;
+        const int chunks = (B * nqv + 63) >> 6;
         for (int l = wave; l < L; l += 4) {
             const int r = clampi(r_lo + l, 0, a.h - 1);
             for (int c = 0; c < chunks; ++c)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
-                                                         3 * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
+                                                         B * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
         }
     }
     if (tid < XW) {
@@ -1531,7 +1531,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
         const int ov = 16 * kg - vso[n] + kHmTabPad;
         const hm_v4i bh = load_taps16(tv, ov), bl = load_taps16(tv + kHmTabW, ov);
         const int vb = vbias[n];
-        const int nt = (3 * (hi - org + 1) + 15) >> 4;
+        const int nt = (B * (hi - org + 1) + 15) >> 4;
         const u8 *rawb = reinterpret_cast<const u8 *>(raw);
         const int r1 = min(16 * kg + (n >> 1), L - 1), r2 = min(16 * kg + 8 + (n >> 1), L - 1);
         uint32_t res[kRmMaxCt];  // this wave's tiles, written after every wave has read the staged rows
@@ -1568,13 +1568,18 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
         const uint32_t *ir = reinterpret_cast<const uint32_t *>(inter + k * a.iw);
         u8 *pl = planes + k * a.row_w;
         for (int q = lane; q < nqv; q += 64) {
-            const uint32_t x0w = ir[3 * q], x1w = ir[3 * q + 1], x2w = ir[3 * q + 2];
-            reinterpret_cast<uint32_t *>(pl)[q] =
-                __builtin_amdgcn_perm(x2w, __builtin_amdgcn_perm(x1w, x0w, 0x0c060300u), 0x05020100u);
-            reinterpret_cast<uint32_t *>(pl + a.plane_w)[q] =
-                __builtin_amdgcn_perm(x2w, __builtin_amdgcn_perm(x1w, x0w, 0x0c070401u), 0x06020100u);
-            reinterpret_cast<uint32_t *>(pl + 2 * a.plane_w)[q] =
-                __builtin_amdgcn_perm(x2w, __builtin_amdgcn_perm(x1w, x0w, 0x0c0c0502u), 0x07040100u);
+            uint32_t xw[4], pw[4];
+#pragma unroll
+            for (int d = 0; d < B; ++d) xw[d] = ir[B * q + d];
+            if (B == 3) {
+                pw[0] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c060300u), 0x05020100u);
+                pw[1] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c070401u), 0x06020100u);
+                pw[2] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c0c0502u), 0x07040100u);
+            } else {
+                transpose4x4(xw[0], xw[1], xw[2], xw[3], pw);
+            }
+#pragma unroll
+            for (int z = 0; z < B; ++z) reinterpret_cast<uint32_t *>(pl + z * a.plane_w)[q] = pw[z];
         }
     }
     __syncthreads();
@@ -1622,36 +1627,47 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
                 acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bz, acc_l[z], 0, 0, 0);
             }
         }
-        uint32_t wz[3];
+        uint32_t wz[4];
 #pragma unroll
         for (int z = 0; z < B; ++z)
             wz[z] = round_pack4((acc_h[z][0] << 6) + acc_l[z][0], (acc_h[z][1] << 6) + acc_l[z][1],
                                 (acc_h[z][2] << 6) + acc_l[z][2], (acc_h[z][3] << 6) + acc_l[z][3]);
         const int x = x0 + 16 * g + 4 * kg;
         if (n >= nr || x > x_last) continue;
-        const uint32_t w0 = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
-        const uint32_t w1 = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
-        const uint32_t w2 = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
-        if (a.direct && x + 3 <= x_last) {  // dword-aligned output rows: the lane's 12 bytes in one store
-            typedef int v3i_t __attribute__((ext_vector_type(3)));
-            __builtin_amdgcn_raw_buffer_store_b96(v3i_t{static_cast<int>(w0), static_cast<int>(w1), static_cast<int>(w2)},
-                                                  os, ((y0 + n) * a.ow + x) * 3, 0, 0);
+        uint32_t wo[4];  // the 4 pixels interleaved: B dwords
+        if (B == 3) {
+            wo[0] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
+            wo[1] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
+            wo[2] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
+        } else {
+            transpose4x4(wz[0], wz[1], wz[2], wz[3], wo);
+        }
+        if (a.direct && x + 3 <= x_last) {  // dword-aligned output rows: the lane's 4 pixels in one store
+            const int qo = ((y0 + n) * a.ow + x) * B;
+            if (B == 3) {
+                typedef int v3i_t __attribute__((ext_vector_type(3)));
+                __builtin_amdgcn_raw_buffer_store_b96(
+                    v3i_t{static_cast<int>(wo[0]), static_cast<int>(wo[1]), static_cast<int>(wo[2])}, os, qo, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b128(hm_v4i{static_cast<int>(wo[0]), static_cast<int>(wo[1]),
+                                                              static_cast<int>(wo[2]), static_cast<int>(wo[3])},
+                                                       os, qo, 0, 0);
+            }
             continue;
         }
-        uint32_t *tq = reinterpret_cast<uint32_t *>(tile + n * (XW * 3 + 4) + (x - x0) * 3);
-        tq[0] = w0;
-        tq[1] = w1;
-        tq[2] = w2;
+        uint32_t *tq = reinterpret_cast<uint32_t *>(tile + n * (XW * B + 4) + (x - x0) * B);
+#pragma unroll
+        for (int d = 0; d < B; ++d) tq[d] = wo[d];
     }
     __syncthreads();
     // ---- each tile row to its output row as whole dwords at the row's own alignment ----
     // (direct mode: only the partial last group of the row's last block went through the tile)
-    const int nb = (x_last - x0 + 1) * 3;
-    const int tb = a.direct ? ((x_last - x0 + 1) & ~3) * 3 : 0;  // tile bytes already stored
+    const int nb = (x_last - x0 + 1) * B;
+    const int tb = a.direct ? ((x_last - x0 + 1) & ~3) * B : 0;  // tile bytes already stored
     for (int r = wave; r < nr && tb < nb; r += 4) {
-        const u8 *tr = tile + r * (XW * 3 + 4);
+        const u8 *tr = tile + r * (XW * B + 4);
         const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
-        const int qo0 = ((y0 + r) * a.ow + x0) * 3 + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+        const int qo0 = ((y0 + r) * a.ow + x0) * B + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
         const int d0 = qo0 >> 2, nd = ((qo0 + nb + 3) >> 2) - d0;
         const int sh = (4 - (qo0 & 3)) & 3;
         const int bias0 = static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
@@ -2327,7 +2343,7 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
     const bool forced = e && (*e == '1' || *e == '2');
     const bool v2 = !forced || *e == '2';
     const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
-    if (b != 3 || !(hs > 1.0) || !(vs > 1.0) || (w * 3) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0 ||
+    if ((b != 3 && b != 4) || !(hs > 1.0) || !(vs > 1.0) || (w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0 ||
         in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL)
         return MIPX_EUNSUPPORTED;
     SepSpec sh, sv;
@@ -2359,13 +2375,14 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
     a.y_blocks = (oh + kRmRows - 1) / kRmRows;
     a.lrows = static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps + 2;
     const int span = static_cast<int>(std::ceil((kRmXW - 1) * hs)) + sh.taps + 16;  // >= hi - org + 1
-    a.rs = ((3 * (span / 4 + 1) + 63) / 64) * 64;
+    if (!v2 && b != 3) return MIPX_EUNSUPPORTED;  // k_rmfma is RGB only
+    a.rs = ((b * (span / 4 + 1) + 63) / 64) * 64;
     if (a.rs < 192) a.rs = 192;
     if (a.rs > 256) return MIPX_EUNSUPPORTED;
     a.plane_w = (span + 15) & ~15;
-    a.row_w = 3 * a.plane_w + ((3 * a.plane_w / 16) % 2 == 0 ? 16 : 0);
+    a.row_w = b * a.plane_w + ((b * a.plane_w / 16) % 2 == 0 ? 16 : 0);
     a.nks = (static_cast<int>(std::ceil(15 * hs)) + sh.taps + 16 + 63) / 64;
-    a.iw = ((3 * span + 15) & ~15) + 16;
+    a.iw = ((b * span + 15) & ~15) + 16;
     if (v2 && (static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps > 64 || 4 * a.rs < a.iw))
         return MIPX_EUNSUPPORTED;
     const size_t lds = static_cast<size_t>(3 * kRmXW + kRmRows + kRmRows * 8) * 4 +
@@ -2388,15 +2405,20 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
     }
     if (v2) {  // row stride = 4 (mod 64) dwords: a transposed read's 8 rows x 2 halves hit 16 distinct bank pairs
         const int rs2 = a.rs + 4;
-        a.direct = (ow * 3) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
+        a.direct = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
         const size_t l2 = static_cast<size_t>(3 * kRmXW + 3 * kRmRows) * 4 +
                           std::max(static_cast<size_t>(a.lrows) * rs2 * 4,
                                    static_cast<size_t>(kRmRows) * (a.iw + a.row_w) + 64 + 16);
-        if (l2 > (forced ? 64 : 40) * 1024 || 3 * span > 16 * 4 * kRmMaxCt ||
-            static_cast<size_t>(kRmRows) * (kRmXW * 3 + 4) > static_cast<size_t>(kRmRows) * a.iw)
+        if (l2 > (forced ? 64 : 40) * 1024 || b * span > 16 * 4 * kRmMaxCt ||
+            static_cast<size_t>(kRmRows) * (kRmXW * b + 4) > static_cast<size_t>(kRmRows) * a.iw)
             return MIPX_EUNSUPPORTED;
-        if (a.rs == 192) hipLaunchKernelGGL(k_rmf2<196>, grid, blk, l2, st, a);
-        else hipLaunchKernelGGL(k_rmf2<260>, grid, blk, l2, st, a);
+        if (b == 3) {
+            if (a.rs == 192) hipLaunchKernelGGL((k_rmf2<3, 196>), grid, blk, l2, st, a);
+            else hipLaunchKernelGGL((k_rmf2<3, 260>), grid, blk, l2, st, a);
+        } else {
+            if (a.rs == 192) hipLaunchKernelGGL((k_rmf2<4, 196>), grid, blk, l2, st, a);
+            else hipLaunchKernelGGL((k_rmf2<4, 260>), grid, blk, l2, st, a);
+        }
         return launch_check("k_rmf2");
     }
     if (a.rs == 192) { MIPX_RM(192) }

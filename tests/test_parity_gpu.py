@@ -386,20 +386,21 @@ def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
     monkeypatch.setenv("MIPX_RMFMA", on)
     monkeypatch.setenv("MIPX_RSTRIP", "0")
     monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
-    for h, w in ((301, 1100), (97, 640), (13, 200), (40, 36), (270, 480), (37, 1026), (150, 97)):
-        imgs = np.stack([rand_img(rng, h, w, 3), smooth_img(rng, h, w, 3)])
+    for h, w, b in ((301, 1100, 3), (97, 640, 3), (13, 200, 3), (40, 36, 3), (270, 480, 3), (37, 1026, 3),
+                    (150, 97, 3), (201, 700, 4), (19, 333, 4), (64, 1024, 4)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
         got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
         for i in range(2):
-            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"rmfma={on} {h}x{w} {hs}x{vs} img{i}")
-    for g in (0, 2, 3):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"rmfma={on} {h}x{w}x{b} {hs}x{vs} img{i}")
+    for g, b in ((0, 3), (2, 3), (3, 3), (0, 4), (3, 4)):
         opts = dict(width=333, height=171, crop=1, gravity=g)
-        p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(1500, 1000, 3, "png"))
-        e, rp = oracle.plan(opts, dict(w=1500, h=1000, bands=3, type=3))
+        p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(1500, 1000, b, "png"))
+        e, rp = oracle.plan(opts, dict(w=1500, h=1000, bands=b, type=3))
         assert e == 0
-        imgs = rng.integers(0, 256, (2, 1000, 1500, 3), dtype=np.uint8)
+        imgs = rng.integers(0, 256, (2, 1000, 1500, b), dtype=np.uint8)
         got = gpu.execute(p, imgs)
         for i in range(2):
-            assert_same(got[i], oracle.execute(rp, imgs[i]), f"rmfma={on} window gravity {g}")
+            assert_same(got[i], oracle.execute(rp, imgs[i]), f"rmfma={on} window gravity {g} bands {b}")
 
 
 @pytest.mark.parametrize("rows", ["1", "8", "13"])
