@@ -1535,12 +1535,12 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
         const u8 *rawb = reinterpret_cast<const u8 *>(raw);
         const int r1 = min(16 * kg + (n >> 1), L - 1), r2 = min(16 * kg + 8 + (n >> 1), L - 1);
         uint32_t res[kRmMaxCt];  // this wave's tiles, written after every wave has read the staged rows
+        typedef int v2i_t __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int i = 0; i < kRmMaxCt; ++i) {
             const int ct = wave + 4 * i;
-            if (ct >= nt) break;
-            const int cb = 16 * ct + 8 * (n & 1);
-            typedef int v2i_t __attribute__((ext_vector_type(2)));
+            if (ct >= nt) continue;  // uniform; no break: results of skipped tiles stay undefined, no copies
+            const int cb = 16 * ct + 8 * (n & 1);  // the tile's 16 staged rows of this lane's byte column
             const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
                 (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r1 * RS * 4 + cb))));
             const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
@@ -1558,7 +1558,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
 #pragma unroll
         for (int i = 0; i < kRmMaxCt; ++i) {
             const int ct = wave + 4 * i;
-            if (ct >= nt) break;
+            if (ct >= nt) continue;
             *reinterpret_cast<uint32_t *>(inter + n * a.iw + 16 * ct + 4 * kg) = res[i];
         }
     }
