@@ -2409,7 +2409,9 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         const size_t l2 = static_cast<size_t>(3 * kRmXW + 3 * kRmRows) * 4 +
                           std::max(static_cast<size_t>(a.lrows) * rs2 * 4,
                                    static_cast<size_t>(kRmRows) * (a.iw + a.row_w) + 64 + 16);
-        if (l2 > (forced ? 64 : 40) * 1024 || b * span > 16 * 4 * kRmMaxCt ||
+        // RGBA by default stays on the two passes: C3's 1024^2 / 1.333 window reduce
+        // measured 1.22 ms fused vs 1.11 ms (profiles/r02/C3_kernel_stats.csv runs)
+        if (l2 > (forced ? 64 : 40) * 1024 || (!forced && b != 3) || b * span > 16 * 4 * kRmMaxCt ||
             static_cast<size_t>(kRmRows) * (kRmXW * b + 4) > static_cast<size_t>(kRmRows) * a.iw)
             return MIPX_EUNSUPPORTED;
         if (b == 3) {
