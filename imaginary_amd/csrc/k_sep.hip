@@ -1278,6 +1278,7 @@ struct RmArgs {
     const int *tsumv;
     int iw;                   // k_rmf2: bytes per row-major intermediate row (16 x column tiles)
     int direct;               // k_rmf2: output rows and images dword aligned (12-byte stores, no tile)
+    int tiles;                // k_rmf3: 16-row x 128-pixel tiles of the batch (column-major)
     SepTaps tv, th;
 };
 
@@ -1682,6 +1683,305 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
                     if (e + k >= tb && e + k < nb)
                         __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
             }
+        }
+    }
+}
+
+// LDS-only workgroup barrier: orders LDS accesses without draining outstanding
+// global loads (the next tile's rows stay in flight across it)
+__device__ __forceinline__ void lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// k_rmf3: k_rmf2 as a persistent kernel.  The batch's 16-row x 128-pixel tiles,
+// column-major (a column's tiles top to bottom, then the next column), are split into
+// one equal run per resident workgroup; the input rows of the run's next tile are
+// loaded into registers (kRmPf dwords per lane) while the current one computes, then
+// written to LDS, so a tile's HBM latency hides behind the previous tile's work
+// instead of stalling the workgroup, and a column's horizontal taps load once.
+constexpr int kRmPf = 27;  // prefetch dwords per lane: staged rows (<= 36) / 4 waves x 3 chunks
+template <int B, int RS>
+__global__ void __launch_bounds__(256) k_rmf3(RmArgs a) {
+    constexpr int XW = kRmXW, GPW = XW / 64;
+    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
+    int *ps = reinterpret_cast<int *>(rsm);
+    int *pph = ps + XW;
+    int *pbias = pph + XW;
+    uint32_t *junk = reinterpret_cast<uint32_t *>(pbias + XW);  // [64] sink of the unused prefetch slots
+    uint32_t *raw = junk + 64;                                  // [lrows][RS]
+    u8 *inter = reinterpret_cast<u8 *>(raw);
+    u8 *planes = inter + kRmRows * a.iw + 64;
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring runs on one XCD's L2
+    const int tt0 = static_cast<int>(static_cast<long long>(t) * a.tiles / gridDim.x);
+    const int tt1 = static_cast<int>(static_cast<long long>(t + 1) * a.tiles / gridDim.x);
+    if (tt0 >= tt1) return;  // uniform, before any barrier
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int ph0;
+    // tile tt: column (image, 128-pixel block) and 16-row block
+    auto column_of = [&](int tt, int *img, int *x0, int *x_last, int *lo, int *hi) {
+        const int col = tt / a.y_blocks;
+        *img = col / a.x_blocks;
+        *x0 = (col - *img * a.x_blocks) * XW;
+        *x_last = min(*x0 + XW - 1, a.ow - 1);
+        int ph;
+        sep_position(a.th, a.ox0 + *x0, lo, &ph);
+        sep_position(a.th, a.ox0 + *x_last, hi, &ph);
+        *hi += a.th.taps - 1;
+    };
+    auto rows_of = [&](int tt, int *y0, int *nr, int *r_lo, int *L) {
+        *y0 = (tt % a.y_blocks) * kRmRows;
+        *nr = min(kRmRows, a.oh - *y0);
+        int r_last, ph;
+        sep_position(a.tv, a.oy0 + *y0, r_lo, &ph);
+        sep_position(a.tv, a.oy0 + *y0 + *nr - 1, &r_last, &ph);
+        *L = r_last + a.tv.taps - *r_lo;
+    };
+    // rows of tile tt into registers: wave w takes staged rows w, w + 4, ..., lane one dword
+    // per 256-byte chunk.  Every slot issues a load (rows past the tile repeat its last row,
+    // an L2 hit; past the run, the run's last tile again), so the load count is static and
+    // later waits count past them; the row offset is uniform (soffset).
+    uint32_t pf[kRmPf];
+    auto fetch = [&](int tt) {
+        const int tc = min(tt, tt1 - 1);
+        int img, x0, x_last, lo, hi, y0, nr, rl, Lf;
+        column_of(tc, &img, &x0, &x_last, &lo, &hi);
+        rows_of(tc, &y0, &nr, &rl, &Lf);
+        const __amdgpu_buffer_rsrc_t rsi = image_rsrc(a.in + img * a.in_img, a.in_img);
+        const int vo = B * (lo & ~15) + 4 * lane;
+#pragma unroll
+        for (int i = 0; i < kRmPf; ++i) {
+            const int l = wave + 4 * (i / 3), c = i % 3;
+            const int r = __builtin_amdgcn_readfirstlane(clampi(rl + min(l, Lf - 1), 0, a.h - 1));
+            pf[i] = __builtin_amdgcn_raw_buffer_load_b32(rsi, vo + 256 * c, r * a.w * B, 0);
+        }
+    };
+    hm_v4i hah[GPW], hal[GPW];  // the column's horizontal taps (first 64-pixel step), per lane
+    int reg_col = -1, lds_col = -1;
+    // iteration tt0 - 1 only issues the first fetch: one fetch site, one set of registers
+    for (int tt = tt0 - 1; tt < tt1; ++tt) {
+        // lane-derived LDS addresses recomputed per tile (an opaque copy of the lane id) rather
+        // than hoisted out of the loop into registers the prefetch needs
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const bool live = tt >= tt0;
+        const int tc = max(tt, tt0), col = tc / a.y_blocks;
+        int img, x0, x_last, lo, hi, y0, nr, r_lo, L;
+        column_of(tc, &img, &x0, &x_last, &lo, &hi);
+        rows_of(tc, &y0, &nr, &r_lo, &L);
+        const int org = lo & ~15;
+        const int nqv = ((hi - org) >> 2) + 1;
+        const int n = ln & 15, kg = ln >> 4;
+        // this tile's global reads (vertical taps, a new column's horizontal taps) go before the
+        // next fetch, so their waits do not cover it
+        int sv, vph;
+        sep_position(a.tv, a.oy0 + y0 + min(n, nr - 1), &sv, &vph);
+        const signed char *tv = a.tabv + static_cast<size_t>(vph) * 2 * kHmTabW;
+        const int ov = 16 * kg - (sv - r_lo) + kHmTabPad;
+        const hm_v4i bh = load_taps16(tv, ov), bl = load_taps16(tv + kHmTabW, ov);
+        const int vb = 128 * a.tsumv[vph] + 2048;
+        if (col != reg_col) {
+            reg_col = col;
+#pragma unroll
+            for (int gi = 0; gi < GPW; ++gi) {
+                const int g = wave * GPW + gi, p = min(16 * g + n, x_last - x0);
+                int s16, sp, ph;
+                sep_position(a.th, a.ox0 + min(x0 + 16 * g, x_last), &s16, &ph);
+                sep_position(a.th, a.ox0 + x0 + p, &sp, &ph);
+                const int o0 = (s16 & ~15) + 16 * kg - sp + kHmTabPad;
+                const signed char *thr = a.tab + static_cast<size_t>(ph) * 2 * kHmTabW;
+                hah[gi] = load_taps16(thr, o0);
+                hal[gi] = load_taps16(thr + kHmTabW, o0);
+            }
+        }
+        int hps = 0, hph = 0, hbias = 0;
+        const bool new_lds_col = live && col != lds_col;  // uniform
+        if (new_lds_col && tid < XW) {
+            sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &hps, &hph);
+            hbias = 128 * a.tsum[hph] + 2048;
+        }
+        lds_sync();  // the previous tile is done with every LDS region
+        if (live) {
+#pragma unroll
+            for (int i = 0; i < kRmPf; ++i) {
+                const int l = wave + 4 * (i / 3), c = i % 3;
+                *(l < L ? raw + l * RS + c * 64 + ln : junk + ln) = pf[i];
+            }
+            if (new_lds_col) {
+                lds_col = col;
+                if (tid < XW) {
+                    ps[tid] = hps;
+                    pph[tid] = hph;
+                    pbias[tid] = hbias;
+                }
+            }
+        }
+        fetch(tt + 1);  // in flight across this tile's LDS-only barriers
+        if (!live) continue;
+        lds_sync();
+        {
+            // ---- vertical pass on the matrix cores, 16-byte column tiles dealt to the waves ----
+            {
+                const int nt = (B * (hi - org + 1) + 15) >> 4;
+                const u8 *rawb = reinterpret_cast<const u8 *>(raw);
+                const int r1 = min(16 * kg + (n >> 1), L - 1), r2 = min(16 * kg + 8 + (n >> 1), L - 1);
+                uint32_t res[kRmMaxCt];  // this wave's tiles, written after every wave has read the staged rows
+                typedef int v2i_t __attribute__((ext_vector_type(2)));
+        #pragma unroll
+                for (int i = 0; i < kRmMaxCt; ++i) {
+                    const int ct = wave + 4 * i;
+                    if (ct >= nt) continue;  // uniform; no break: results of skipped tiles stay undefined, no copies
+                    const int cb = 16 * ct + 8 * (n & 1);  // the tile's 16 staged rows of this ln's byte column
+                    const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+                        (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r1 * RS * 4 + cb))));
+                    const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+                        (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r2 * RS * 4 + cb))));
+                    const hm_v4i av = hm_v4i{t1.x ^ static_cast<int>(0x80808080u), t1.y ^ static_cast<int>(0x80808080u),
+                                             t2.x ^ static_cast<int>(0x80808080u), t2.y ^ static_cast<int>(0x80808080u)};
+                    hm_v4i dh = hm_v4i{0, 0, 0, 0}, dl = hm_v4i{vb, vb, vb, vb};
+                    dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
+                    dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
+                    const uint32_t w = round_pack4((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
+                                                   (dh[3] << 6) + dl[3]);
+                    res[i] = w ^ 0x80808080u;
+                    __builtin_amdgcn_sched_barrier(0);  // one column tile at a time: registers for the prefetch
+                }
+                lds_sync();
+        #pragma unroll
+                for (int i = 0; i < kRmMaxCt; ++i) {
+                    const int ct = wave + 4 * i;
+                    if (ct >= nt) continue;
+                    *reinterpret_cast<uint32_t *>(inter + n * a.iw + 16 * ct + 4 * kg) = res[i];
+                }
+            }
+            lds_sync();
+            // ---- row-major intermediate -> channel planes, 4 pixels per item ----
+            for (int k = wave; k < nr; k += 4) {
+                const uint32_t *ir = reinterpret_cast<const uint32_t *>(inter + k * a.iw);
+                u8 *pl = planes + k * a.row_w;
+                for (int q = ln; q < nqv; q += 64) {
+                    uint32_t xw[4], pw[4];
+        #pragma unroll
+                    for (int d = 0; d < B; ++d) xw[d] = ir[B * q + d];
+                    if (B == 3) {
+                        pw[0] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c060300u), 0x05020100u);
+                        pw[1] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c070401u), 0x06020100u);
+                        pw[2] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c0c0502u), 0x07040100u);
+                    } else {
+                        transpose4x4(xw[0], xw[1], xw[2], xw[3], pw);
+                    }
+        #pragma unroll
+                    for (int z = 0; z < B; ++z) reinterpret_cast<uint32_t *>(pl + z * a.plane_w)[q] = pw[z];
+                }
+            }
+            lds_sync();
+            // ---- COPY edge of the horizontal pass: pixels outside the image repeat its edge ----
+            if (lo < 0 || hi >= a.w) {
+                for (int i = tid; i < nr * (hi - org + 1); i += 256) {
+                    const int k = i / (hi - org + 1), pq = i - k * (hi - org + 1);
+                    const int p = org + pq;
+                    if (p >= 0 && p < a.w) continue;
+                    const int src = clampi(p, 0, a.w - 1) - org;
+        #pragma unroll
+                    for (int z = 0; z < B; ++z) planes[k * a.row_w + z * a.plane_w + pq] = planes[k * a.row_w + z * a.plane_w + src];
+                }
+                lds_sync();
+            }
+            // ---- horizontal pass on the matrix cores (k_hmfma's group loop) ----
+            const int n = ln & 15, kg = ln >> 4;
+            u8 *ob = a.out + img * a.out_img;
+            u8 *tile = inter;  // output tile [kRmRows][XW * 3 + 4] over the intermediate (dead after the deinterleave)
+            const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
+            lds_sync();
+        #pragma unroll
+            for (int gi = 0; gi < GPW; ++gi) {
+                const int g = wave * GPW + gi;
+                if (x0 + 16 * g > x_last) break;
+                const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
+                const int p = min(16 * g + n, x_last - x0);
+                const int o0 = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
+                const signed char *thr = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
+                const int4 bias = *reinterpret_cast<const int4 *>(pbias + 16 * g + 4 * kg);
+                hm_v4i acc_h[B], acc_l[B];
+        #pragma unroll
+                for (int z = 0; z < B; ++z) {
+                    acc_h[z] = hm_v4i{0, 0, 0, 0};
+                    acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
+                }
+                for (int ks = 0; ks < a.nks; ++ks) {
+                    hm_v4i ah = hah[gi], al = hal[gi];
+                    if (ks) {
+                        ah = load_taps16(thr, o0 + 64 * ks);
+                        al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
+                    }
+        #pragma unroll
+                    for (int z = 0; z < B; ++z) {
+                        const hm_v4i bz =
+                            *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 64 * ks + 16 * kg);
+                        acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bz, acc_h[z], 0, 0, 0);
+                        acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bz, acc_l[z], 0, 0, 0);
+                    }
+                }
+                uint32_t wz[4];
+        #pragma unroll
+                for (int z = 0; z < B; ++z)
+                    wz[z] = round_pack4((acc_h[z][0] << 6) + acc_l[z][0], (acc_h[z][1] << 6) + acc_l[z][1],
+                                        (acc_h[z][2] << 6) + acc_l[z][2], (acc_h[z][3] << 6) + acc_l[z][3]);
+                const int x = x0 + 16 * g + 4 * kg;
+                if (n >= nr || x > x_last) continue;
+                uint32_t wo[4];  // the 4 pixels interleaved: B dwords
+                if (B == 3) {
+                    wo[0] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
+                    wo[1] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
+                    wo[2] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
+                } else {
+                    transpose4x4(wz[0], wz[1], wz[2], wz[3], wo);
+                }
+                if (a.direct && x + 3 <= x_last) {  // dword-aligned output rows: the ln's 4 pixels in one store
+                    const int qo = ((y0 + n) * a.ow + x) * B;
+                    if (B == 3) {
+                        typedef int v3i_t __attribute__((ext_vector_type(3)));
+                        __builtin_amdgcn_raw_buffer_store_b96(
+                            v3i_t{static_cast<int>(wo[0]), static_cast<int>(wo[1]), static_cast<int>(wo[2])}, os, qo, 0, 0);
+                    } else {
+                        __builtin_amdgcn_raw_buffer_store_b128(hm_v4i{static_cast<int>(wo[0]), static_cast<int>(wo[1]),
+                                                                      static_cast<int>(wo[2]), static_cast<int>(wo[3])},
+                                                               os, qo, 0, 0);
+                    }
+                    continue;
+                }
+                uint32_t *tq = reinterpret_cast<uint32_t *>(tile + n * (XW * B + 4) + (x - x0) * B);
+        #pragma unroll
+                for (int d = 0; d < B; ++d) tq[d] = wo[d];
+            }
+            lds_sync();
+            // ---- each tile row to its output row as whole dwords at the row's own alignment ----
+            // (direct mode: only the partial last group of the row's last block went through the tile)
+            const int nb = (x_last - x0 + 1) * B;
+            const int tb = a.direct ? ((x_last - x0 + 1) & ~3) * B : 0;  // tile bytes already stored
+            for (int r = wave; r < nr && tb < nb; r += 4) {
+                const u8 *tr = tile + r * (XW * B + 4);
+                const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
+                const int qo0 = ((y0 + r) * a.ow + x0) * B + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+                const int d0 = qo0 >> 2, nd = ((qo0 + nb + 3) >> 2) - d0;
+                const int sh = (4 - (qo0 & 3)) & 3;
+                const int bias0 = static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+                for (int i = ln; i < nd; i += 64) {
+                    const int e = 4 * (d0 + i) - qo0;
+                    if (e + 4 <= tb) continue;
+                    if (e >= tb && e + 4 <= nb) {
+                        const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
+                        __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i) - bias0, 0, 0);
+                    } else {
+                        for (int k = 0; k < 4; ++k)
+                            if (e + k >= tb && e + k < nb)
+                                __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
+                    }
+                }
+            }
+
         }
     }
 }
@@ -2340,8 +2640,9 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
     // 1 forces k_rmfma (VALU vertical pass, an A/B variant), 2 forces k_rmf2
     const char *e = std::getenv("MIPX_RMFMA");
     if (e && *e == '0') return MIPX_EUNSUPPORTED;
-    const bool forced = e && (*e == '1' || *e == '2');
-    const bool v2 = !forced || *e == '2';
+    const bool forced = e && (*e == '1' || *e == '2' || *e == '3');
+    const bool v2 = !forced || *e == '2' || *e == '3';
+    const bool v3 = forced && *e == '3';
     const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
     if ((b != 3 && b != 4) || !(hs > 1.0) || !(vs > 1.0) || (w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0 ||
         in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL)
@@ -2414,6 +2715,33 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         if (l2 > (forced ? 64 : 40) * 1024 || (!forced && b != 3) || b * span > 16 * 4 * kRmMaxCt ||
             static_cast<size_t>(kRmRows) * (kRmXW * b + 4) > static_cast<size_t>(kRmRows) * a.iw)
             return MIPX_EUNSUPPORTED;
+        if (v3) {  // persistent, register prefetch of the next tile's rows
+            const int lmax = static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps;
+            if (lmax > 36 || (b * (span / 4 + 1) + 63) / 64 > 3) return MIPX_EUNSUPPORTED;
+            const long long tiles = blocks;
+            a.tiles = static_cast<int>(tiles);
+            const size_t l3 = l2 + 64 * 4;  // the prefetch sink
+            const void *fn = b == 3 ? (a.rs == 192 ? reinterpret_cast<const void *>(&k_rmf3<3, 196>)
+                                                  : reinterpret_cast<const void *>(&k_rmf3<3, 260>))
+                                    : (a.rs == 192 ? reinterpret_cast<const void *>(&k_rmf3<4, 196>)
+                                                  : reinterpret_cast<const void *>(&k_rmf3<4, 260>));
+            // one run per resident workgroup (occupancy x CUs), so every CU finishes together
+            int per_cu = 0, dev = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, l3) != hipSuccess || per_cu < 1) per_cu = 1;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+                cus = 256;
+            long long g = static_cast<long long>(per_cu) * cus;
+            if (const char *ge = std::getenv("MIPX_RM3_G"); ge && std::atoll(ge) > 0) g = std::atoll(ge);  // A/B
+            const dim3 g3(static_cast<unsigned>(std::min(g, tiles)));
+            if (b == 3) {
+                if (a.rs == 192) hipLaunchKernelGGL((k_rmf3<3, 196>), g3, blk, l3, st, a);
+                else hipLaunchKernelGGL((k_rmf3<3, 260>), g3, blk, l3, st, a);
+            } else {
+                if (a.rs == 192) hipLaunchKernelGGL((k_rmf3<4, 196>), g3, blk, l3, st, a);
+                else hipLaunchKernelGGL((k_rmf3<4, 260>), g3, blk, l3, st, a);
+            }
+            return launch_check("k_rmf3");
+        }
         if (b == 3) {
             if (a.rs == 192) hipLaunchKernelGGL((k_rmf2<3, 196>), grid, blk, l2, st, a);
             else hipLaunchKernelGGL((k_rmf2<3, 260>), grid, blk, l2, st, a);

@@ -5,5 +5,5 @@ SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_IN
 GRBM_GUI_ACTIVE GRBM_COUNT
 FETCH_SIZE
 WRITE_SIZE"
-TAG=vf bash scripts/pmc_op.sh > gpurun_out/pmc_vf.txt 2>&1 || { tail gpurun_out/pmc_vf.txt; exit 1; }
-cat gpurun_out/pmc_vf.txt
+TAG=${TAG:-vf} bash scripts/pmc_op.sh > gpurun_out/pmc_${TAG:-vf}.txt 2>&1 || { tail gpurun_out/pmc_${TAG:-vf}.txt; exit 1; }
+cat gpurun_out/pmc_${TAG:-vf}.txt
