@@ -1279,6 +1279,7 @@ struct RmArgs {
     int iw;                   // k_rmf2: bytes per row-major intermediate row (16 x column tiles)
     int direct;               // k_rmf2: output rows and images dword aligned (12-byte stores, no tile)
     int tiles;                // k_rmf3: 16-row x 128-pixel tiles of the batch (column-major)
+    int rsd;                  // k_rmf2: staged row stride in dwords, (rsd mod 64) / 4 odd
     SepTaps tv, th;
 };
 
@@ -1465,9 +1466,10 @@ __global__ void __launch_bounds__(256) k_rmfma(RmArgs a) {
 // consecutive intermediate bytes of one output row: one dword write into a
 // row-major intermediate, deinterleaved to channel planes for the horizontal MFMA.
 // Needs 15 vs + vtaps <= 64 staged rows.
-template <int B, int RS>
+template <int B, int XW>
 __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
-    constexpr int XW = kRmXW, GPW = XW / 64;
+    constexpr int GPW = XW / 64;
+    const int RS = a.rsd;
     extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
     int *ps = reinterpret_cast<int *>(rsm);  // [XW] horizontal: first tap pixel
     int *pph = ps + XW;                      // [XW] phase
@@ -1506,8 +1508,9 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
         for (int l = wave; l < L; l += 4) {
             const int r = clampi(r_lo + l, 0, a.h - 1);
             for (int c = 0; c < chunks; ++c)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
-                                                         B * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
+                if (c * 64 + lane < RS)  // the last chunk stops at the row stride
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
+                                                             B * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
         }
     }
     if (tid < XW) {
@@ -1719,7 +1722,6 @@ __global__ void __launch_bounds__(256) k_rmf3(RmArgs a) {
     if (tt0 >= tt1) return;  // uniform, before any barrier
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int ph0;
     // tile tt: column (image, 128-pixel block) and 16-row block
     auto column_of = [&](int tt, int *img, int *x0, int *x_last, int *lo, int *hi) {
         const int col = tt / a.y_blocks;
@@ -2635,9 +2637,10 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
 // runs another path).
 int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
                        int ow, int oh, hipStream_t st) {
-    // default: k_rmf2 where its LDS leaves >= 4 workgroups per CU (rmfma_ab.jsonl: -10 to
-    // -35 % against the two passes there, slower at 2 workgroups); MIPX_RMFMA=0 off,
-    // 1 forces k_rmfma (VALU vertical pass, an A/B variant), 2 forces k_rmf2
+    // default: k_rmf2 where its LDS leaves >= 4 workgroups per CU (rmfma_ab.jsonl,
+    // rmf2_xw_ab.jsonl: -6 to -35 % against the two passes there); MIPX_RMFMA=0 off,
+    // 1 forces k_rmfma (VALU vertical pass, an A/B variant), 2 forces k_rmf2 (<= 64 KB),
+    // 3 the persistent k_rmf3 (A/B)
     const char *e = std::getenv("MIPX_RMFMA");
     if (e && *e == '0') return MIPX_EUNSUPPORTED;
     const bool forced = e && (*e == '1' || *e == '2' || *e == '3');
@@ -2704,18 +2707,16 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         case 7: hipLaunchKernelGGL((k_rmfma<7, RS_>), grid, blk, lds, st, a); break;                    \
         default: hipLaunchKernelGGL((k_rmfma<8, RS_>), grid, blk, lds, st, a); break;                   \
     }
-    if (v2) {  // row stride = 4 (mod 64) dwords: a transposed read's 8 rows x 2 halves hit 16 distinct bank pairs
-        const int rs2 = a.rs + 4;
+    if (v2) {
         a.direct = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
-        const size_t l2 = static_cast<size_t>(3 * kRmXW + 3 * kRmRows) * 4 +
-                          std::max(static_cast<size_t>(a.lrows) * rs2 * 4,
-                                   static_cast<size_t>(kRmRows) * (a.iw + a.row_w) + 64 + 16);
-        // RGBA by default stays on the two passes: C3's 1024^2 / 1.333 window reduce
-        // measured 1.22 ms fused vs 1.11 ms (profiles/r02/C3_kernel_stats.csv runs)
-        if (l2 > (forced ? 64 : 40) * 1024 || (!forced && b != 3) || b * span > 16 * 4 * kRmMaxCt ||
-            static_cast<size_t>(kRmRows) * (kRmXW * b + 4) > static_cast<size_t>(kRmRows) * a.iw)
-            return MIPX_EUNSUPPORTED;
-        if (v3) {  // persistent, register prefetch of the next tile's rows
+        if (v3) {  // persistent, register prefetch of the next tile's rows (128-pixel columns, stride rs + 4)
+            const int rs2 = a.rs + 4;
+            const size_t l2 = static_cast<size_t>(3 * kRmXW + 3 * kRmRows) * 4 +
+                              std::max(static_cast<size_t>(a.lrows) * rs2 * 4,
+                                       static_cast<size_t>(kRmRows) * (a.iw + a.row_w) + 64 + 16);
+            if (l2 > 64 * 1024 || b * span > 16 * 4 * kRmMaxCt ||
+                static_cast<size_t>(kRmRows) * (kRmXW * b + 4) > static_cast<size_t>(kRmRows) * a.iw)
+                return MIPX_EUNSUPPORTED;
             const int lmax = static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps;
             if (lmax > 36 || (b * (span / 4 + 1) + 63) / 64 > 3) return MIPX_EUNSUPPORTED;
             const long long tiles = blocks;
@@ -2742,12 +2743,44 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
             }
             return launch_check("k_rmf3");
         }
+        // k_rmf2: 128- or 64-pixel columns; staged rows at the narrowest stride whose
+        // (dwords mod 64) / 4 is odd, so a transposed read's 8 rows x 2 halves hit 16 distinct
+        // bank pairs.  The smaller the LDS, the more workgroups share a CU (<= 32 KB: 5).
+        const char *xe = std::getenv("MIPX_RMF2_XW");  // A/B: 128 or 64 forces the column width
+        const int xw_only = xe ? std::atoi(xe) : 0;
+        const char *re = std::getenv("MIPX_RMF2_RS");
+        const bool rs_wide = re && *re == '1';
+        size_t l2 = 0;
+        int xw = 0;
+        for (const int x : {128, 64}) {
+            if (xw_only && x != xw_only) continue;
+            const int sp = static_cast<int>(std::ceil((x - 1) * hs)) + sh.taps + 16;  // >= hi - org + 1
+            int rsd = (b * (sp / 4 + 1) + 3) & ~3;
+            while (((rsd & 63) >> 2) % 2 == 0) rsd += 4;
+            if (rs_wide) rsd = std::max(192, (b * (sp / 4 + 1) + 63) / 64 * 64) + 4;  // A/B: the r02 stride
+            const int pw = (sp + 15) & ~15;
+            const int rw = b * pw + ((b * pw / 16) % 2 == 0 ? 16 : 0);
+            const int iw = ((b * sp + 15) & ~15) + 16;
+            const size_t lx = static_cast<size_t>(3 * x + 3 * kRmRows) * 4 +
+                              std::max(static_cast<size_t>(a.lrows) * rsd * 4, static_cast<size_t>(kRmRows) * (iw + rw) + 64 + 16);
+            if (b * sp > 16 * 4 * kRmMaxCt || x * b + 4 > iw) continue;
+            if (xw == 0 || (l2 > 32 * 1024 && lx < l2)) {
+                xw = x, l2 = lx, a.rsd = rsd, a.plane_w = pw, a.row_w = rw, a.iw = iw;
+                a.x_blocks = (ow + x - 1) / x;
+            }
+        }
+        // RGB and RGBA by default (cfg_rmf2_ab.jsonl: C3 / C4 / C5 +2.7 / +1.7 / +0.2 % over the
+        // RGB-only default once the narrow stride took 1024^2 RGBA / 1.333 to 6 workgroups)
+        if (xw == 0 || l2 > (forced ? 64 : 40) * 1024) return MIPX_EUNSUPPORTED;
+        const long long blocks2 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
+        if (!grid_ok(blocks2)) return MIPX_EINVAL;
+        const dim3 grid2(static_cast<unsigned>(blocks2));
         if (b == 3) {
-            if (a.rs == 192) hipLaunchKernelGGL((k_rmf2<3, 196>), grid, blk, l2, st, a);
-            else hipLaunchKernelGGL((k_rmf2<3, 260>), grid, blk, l2, st, a);
+            if (xw == 128) hipLaunchKernelGGL((k_rmf2<3, 128>), grid2, blk, l2, st, a);
+            else hipLaunchKernelGGL((k_rmf2<3, 64>), grid2, blk, l2, st, a);
         } else {
-            if (a.rs == 192) hipLaunchKernelGGL((k_rmf2<4, 196>), grid, blk, l2, st, a);
-            else hipLaunchKernelGGL((k_rmf2<4, 260>), grid, blk, l2, st, a);
+            if (xw == 128) hipLaunchKernelGGL((k_rmf2<4, 128>), grid2, blk, l2, st, a);
+            else hipLaunchKernelGGL((k_rmf2<4, 64>), grid2, blk, l2, st, a);
         }
         return launch_check("k_rmf2");
     }
