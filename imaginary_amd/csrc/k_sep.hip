@@ -1906,18 +1906,18 @@ __global__ void __launch_bounds__(256) k_rmf3(RmArgs a) {
                 const int o0 = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
                 const signed char *thr = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
                 const int4 bias = *reinterpret_cast<const int4 *>(pbias + 16 * g + 4 * kg);
+                // step 0 from the column's registers; later steps (wide shrinks) load their taps,
+                // and only there do waits (which also cover the prefetch) appear
                 hm_v4i acc_h[B], acc_l[B];
         #pragma unroll
                 for (int z = 0; z < B; ++z) {
-                    acc_h[z] = hm_v4i{0, 0, 0, 0};
-                    acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
+                    const hm_v4i bz = *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 16 * kg);
+                    acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(hah[gi], bz, hm_v4i{0, 0, 0, 0}, 0, 0, 0);
+                    acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(hal[gi], bz, hm_v4i{bias.x, bias.y, bias.z, bias.w}, 0, 0, 0);
                 }
-                for (int ks = 0; ks < a.nks; ++ks) {
-                    hm_v4i ah = hah[gi], al = hal[gi];
-                    if (ks) {
-                        ah = load_taps16(thr, o0 + 64 * ks);
-                        al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
-                    }
+                for (int ks = 1; ks < a.nks; ++ks) {
+                    const hm_v4i ah = load_taps16(thr, o0 + 64 * ks);
+                    const hm_v4i al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
         #pragma unroll
                     for (int z = 0; z < B; ++z) {
                         const hm_v4i bz =
