@@ -397,6 +397,31 @@ int reduceh_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hsh
     return hpass_launch(in, out, n, spec, win, st);
 }
 
+// Both shrinks > 1 in one launch, output window [ox0, ox0 + ow) x [oy0, oy0 + oh):
+// k_rmf2 (matrix cores) first, then the small-image strip walker (rows k_rmf2 does
+// not take: unaligned, > 16 taps), then the A/B fused kernels; MIPX_EUNSUPPORTED
+// leaves it to the two separable passes.  small_ab.jsonl: k_rmf2 2x faster than the
+// strip walker on small images (C1's 480x270 / 1.6 0.161 -> 0.075 ms);
+// MIPX_RSTRIP=1 puts the strip walker first again.
+int reduce_one_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
+                      int ow, int oh, hipStream_t st) {
+    const char *ef = std::getenv("MIPX_RSTRIP");
+    const bool strip_first = ef && *ef == '1';
+    if (strip_first) {
+        const int se = reduce_strip_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
+        if (se != MIPX_EUNSUPPORTED) return se;
+    }
+    const int me = reduce_mfma_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
+    if (me != MIPX_EUNSUPPORTED) return me;
+    if (!strip_first) {
+        const int se = reduce_strip_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
+        if (se != MIPX_EUNSUPPORTED) return se;
+    }
+    const int fe = reduce_fused_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
+    if (fe != MIPX_EUNSUPPORTED) return fe;
+    return reduce2d_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
+}
+
 // vips_reduce followed by vips_extract_area(left, top, ow, oh): only the
 // window's output rows (vertical pass) and columns (horizontal pass) are
 // computed.  Every output is the same sum over the same input pixels, so the
@@ -412,14 +437,8 @@ int reduce_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     if (vs > 1.0 && !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
     if (hs > 1.0 && !sep_spec_reduce(hs, &sh)) return MIPX_EDEVICE;
     if (vs > 1.0 && hs > 1.0) {
-        const int se = reduce_strip_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
-        if (se != MIPX_EUNSUPPORTED) return se;
-        const int me = reduce_mfma_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
-        if (me != MIPX_EUNSUPPORTED) return me;
-        const int fe = reduce_fused_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
+        const int fe = reduce_one_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
         if (fe != MIPX_EUNSUPPORTED) return fe;
-        const int f2 = reduce2d_launch(in, out, n, w, h, b, hs, vs, left, top, ow, oh, st);
-        if (f2 != MIPX_EUNSUPPORTED) return f2;
         const size_t need = align_up(static_cast<size_t>(n) * w * oh * b);
         if (!ws || ws_bytes < need) return MIPX_EINVAL;
         u8 *tmp = static_cast<u8 *>(ws);

@@ -1280,6 +1280,8 @@ struct RmArgs {
     int direct;               // k_rmf2: output rows and images dword aligned (12-byte stores, no tile)
     int tiles;                // k_rmf3: 16-row x 128-pixel tiles of the batch (column-major)
     int rsd;                  // k_rmf2: staged row stride in dwords, (rsd mod 64) / 4 odd
+    int dbg;                  // k_rmf2 timing experiments (MIPX_RMF2_DBG, wrong pixels): 1 no staging
+                              // loads, 2 no products, 4 no position set-up (rmf2_parts.jsonl)
     SepTaps tv, th;
 };
 
@@ -1505,7 +1507,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
         const int pitch = a.w * B;
         const int chunks = (B * nqv + 63) >> 6;
-        for (int l = wave; l < L; l += 4) {
+        for (int l = (a.dbg & 1) ? L : wave; l < L; l += 4) {  // dbg 1: no staging loads (timing only)
             const int r = clampi(r_lo + l, 0, a.h - 1);
             for (int c = 0; c < chunks; ++c)
                 if (c * 64 + lane < RS)  // the last chunk stops at the row stride
@@ -1513,7 +1515,8 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
                                                              B * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
         }
     }
-    if (tid < XW) {
+    if (a.dbg & 4) {  // dbg 4: no position set-up (timing only)
+    } else if (tid < XW) {
         int sp, ph;
         sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
         ps[tid] = sp;
@@ -1529,7 +1532,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     }
     __syncthreads();
     // ---- vertical pass on the matrix cores, 16-byte column tiles dealt to the waves ----
-    {
+    if (!(a.dbg & 2)) {  // dbg 2: no vertical pass, deinterleave or horizontal products (timing only)
         const int n = lane & 15, kg = lane >> 4;
         const signed char *tv = a.tabv + static_cast<size_t>(vph[n]) * 2 * kHmTabW;
         const int ov = 16 * kg - vso[n] + kHmTabPad;
@@ -1568,7 +1571,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     }
     __syncthreads();
     // ---- row-major intermediate -> channel planes, 4 pixels per item ----
-    for (int k = wave; k < nr; k += 4) {
+    for (int k = (a.dbg & 2) ? nr : wave; k < nr; k += 4) {
         const uint32_t *ir = reinterpret_cast<const uint32_t *>(inter + k * a.iw);
         u8 *pl = planes + k * a.row_w;
         for (int q = lane; q < nqv; q += 64) {
@@ -1620,7 +1623,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
             acc_h[z] = hm_v4i{0, 0, 0, 0};
             acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
         }
-        for (int ks = 0; ks < a.nks; ++ks) {
+        for (int ks = 0; ks < ((a.dbg & 2) ? 0 : a.nks); ++ks) {
             const hm_v4i ah = load_taps16(thr, o0 + 64 * ks);
             const hm_v4i al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
 #pragma unroll
@@ -2772,6 +2775,8 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         // RGB and RGBA by default (cfg_rmf2_ab.jsonl: C3 / C4 / C5 +2.7 / +1.7 / +0.2 % over the
         // RGB-only default once the narrow stride took 1024^2 RGBA / 1.333 to 6 workgroups)
         if (xw == 0 || l2 > (forced ? 64 : 40) * 1024) return MIPX_EUNSUPPORTED;
+        if (const char *de = std::getenv("MIPX_RMF2_DBG")) a.dbg = std::atoi(de);  // timing only: wrong pixels
+        if (const char *ds = std::getenv("MIPX_RMF2_DIRECT"); ds && *ds == '0') a.direct = 0;  // A/B: tile stores
         const long long blocks2 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
         if (!grid_ok(blocks2)) return MIPX_EINVAL;
         const dim3 grid2(static_cast<unsigned>(blocks2));

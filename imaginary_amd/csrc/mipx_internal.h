@@ -92,6 +92,10 @@ int reduce2d_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b,
 int reduce_fused_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                         int oy0, int ow, int oh, hipStream_t st);
 // k_rstrip.hip: streaming fused reduce (LDS row ring + LDS intermediate), any shrink pair
+// both shrinks > 1 in one launch (k_rmf2, else the strip walker, else the A/B fused
+// kernels); MIPX_EUNSUPPORTED = run the two separable passes
+int reduce_one_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
+                      int oy0, int ow, int oh, hipStream_t st);
 int reduce_mfma_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                        int oy0, int ow, int oh, hipStream_t st);
 int reduce_strip_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,

@@ -66,18 +66,9 @@ int mipx_op_reduce(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, in
     if (vshrink == 1.0) return mipx_op_reduceh(d_in, d_out, n, w, h, bands, hshrink, stream);
     if (hshrink == 1.0) return mipx_op_reducev(d_in, d_out, n, w, h, bands, vshrink, stream);
     {  // both axes: one fused launch, intermediate in LDS
-        const int es = reduce_strip_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
-                                           out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
-        if (es != MIPX_EUNSUPPORTED) return es;
-        const int em = reduce_mfma_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
-                                          out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
-        if (em != MIPX_EUNSUPPORTED) return em;
-        const int e = reduce_fused_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
-                                          out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
+        const int e = reduce_one_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
+                                        out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
         if (e != MIPX_EUNSUPPORTED) return e;
-        const int e2 = reduce2d_launch(d_in, d_out, n, w, h, bands, hshrink, vshrink, 0, 0,
-                                       out_size_reduce(w, hshrink), out_size_reduce(h, vshrink), st);
-        if (e2 != MIPX_EUNSUPPORTED) return e2;
     }
     const size_t need = op_workspace_bytes(MIPX_OP_REDUCE, n, w, h, bands, hshrink, vshrink);
     if (!d_ws || ws_bytes < need) return MIPX_EINVAL;
