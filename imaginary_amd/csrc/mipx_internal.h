@@ -59,6 +59,9 @@ const uint32_t *device_reduce_pairs(double shrink, int *n_taps, int *tpa);
 constexpr int kHmTabW = 64;     // k_hmfma i8 tap rows: bytes per (phase, hi / lo) row (16.5 KB: L1-resident)
 constexpr int kHmTabPad = 16;   // zero bytes in front of tap 0 (taps <= 16; windows clamped to [-16, 16])
 const signed char *device_reduce_i8(double shrink, int *n_taps, const int **sums);
+// k_bmf's i8 MFMA operands for a blur mask (cached per device): [nks][64][16]
+// horizontal taps at byte stride `bands` shifted by delta, then [64][16] vertical taps
+const signed char *device_blur_ops(const std::vector<int> &mask, int bands, int delta, int nks);
 const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt | 257 y2v]
 const int *device_bicubic_table();     // 129 x 4
 // float copy of the integer gaussmat mask; *scale = mask sum

@@ -244,7 +244,8 @@ def test_gaussblur_dot4_and_float_paths(gpu, oracle, rng, monkeypatch, dot, sigm
     (MIPX_SEP_DOT=0) on every band count, odd widths and unaligned batches
     (3 images of an odd byte size: the DMA=0 vertical staging)."""
     monkeypatch.setenv("MIPX_SEP_DOT", dot)
-    monkeypatch.setenv("MIPX_BLUR2D", "0")  # the two separable passes, not the fused kernel
+    monkeypatch.setenv("MIPX_BLUR2D", "0")  # the two separable passes, not the fused kernels
+    monkeypatch.setenv("MIPX_BMF", "0")
     for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
         got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
@@ -263,12 +264,42 @@ def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma,
     mul-hi (default) and fp32 rounding (MIPX_BLUR2D_FROUND=1)."""
     monkeypatch.setenv("MIPX_BLUR2D_ROWS", rows)
     monkeypatch.setenv("MIPX_BLUR2D_FROUND", fround)
+    monkeypatch.setenv("MIPX_BMF", "0")  # k_blur2d, not the matrix-core kernel
     for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3), (9, 600, 4), (130, 513, 3),
                     (3, 5, 4), (70, 257, 2)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
         got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
         for i in range(3):
             assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur2d {sigma} {h}x{w}x{b} rows={rows} fr={fround} img{i}")
+
+
+@pytest.mark.parametrize("on", ["1", "0"])
+@pytest.mark.parametrize("sigma", [0.3, 1.0, 2.2, 5.0, 7.5, 9.0, 12.5])
+def test_blur_mfma_matches_oracle(gpu, oracle, rng, monkeypatch, on, sigma):
+    """k_bmf (both convsep passes on the i8 matrix cores: horizontal on the
+    interleaved bytes with the taps at byte stride B, vertical through transposed
+    LDS reads) against the oracle: RGB / RGBA, images narrower than a block and
+    shorter than the mask, several column and row blocks, both edges of every
+    window, windowed plans (resize -> crop -> blur) at every gravity, and the
+    cases it leaves to k_blur2d (unaligned rows, 1-2 bands, > 33 taps).  "0" runs
+    k_blur2d on the same cases."""
+    monkeypatch.setenv("MIPX_BMF", on)
+    for h, w, b in ((64, 76, 3), (130, 516, 3), (9, 600, 4), (50, 260, 4), (3, 8, 4), (33, 20, 3), (17, 132, 3),
+                    (200, 388, 4), (33, 19, 3), (29, 41, 2), (41, 57, 1)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
+        for i in range(2):
+            assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"bmf={on} {sigma} {h}x{w}x{b} img{i}")
+    if sigma in (1.0, 5.0):
+        for g, b in ((0, 3), (2, 3), (3, 4), (1, 4)):
+            opts = dict(width=300, height=200, crop=1, gravity=g, sigma=sigma)
+            p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(1200, 700, b, "png"))
+            e, rp = oracle.plan(opts, dict(w=1200, h=700, bands=b, type=3))
+            assert e == 0
+            imgs = rng.integers(0, 256, (2, 700, 1200, b), dtype=np.uint8)
+            got = gpu.execute(p, imgs)
+            for i in range(2):
+                assert_same(got[i], oracle.execute(rp, imgs[i]), f"bmf={on} window gravity {g} bands {b}")
 
 
 @pytest.mark.parametrize("hdma", ["16", "4"])
@@ -279,6 +310,7 @@ def test_hpass_dma_widths(gpu, oracle, rng, monkeypatch, hdma):
     16-byte grid), each against the oracle, with both image edges inside a block."""
     monkeypatch.setenv("MIPX_HP_DMA", hdma)
     monkeypatch.setenv("MIPX_BLUR2D", "0")
+    monkeypatch.setenv("MIPX_BMF", "0")
     for h, w, s in ((23, 256, 1.3333333333333333), (19, 300, 2.5), (11, 1028, 1.1), (9, 64, 3.0)):
         imgs = np.stack([rand_img(rng, h, w, 4), smooth_img(rng, h, w, 4)])
         got = gpu.run_op("reduceh", imgs, hshrink=s)
