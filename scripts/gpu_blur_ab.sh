@@ -8,7 +8,7 @@ fi
 : > gpurun_out/blur_ab.jsonl
 for sh in "768 512 4 512 5" "1920 1080 3 32 1" "1920 1080 3 32 3" "1920 1080 3 32 5" "3840 2160 3 8 3" "1024 1024 4 64 2"; do
   set -- $sh
-  for v in 1 0; do
+  for v in ${BMF_VARIANTS:-1 0}; do
     MIPX_BMF=$v timeout -k 10 60 python3 scripts/op_bench.py blur --w $1 --h $2 --b $3 --n $4 --s $5 --iters 20 > gpurun_out/ob.txt 2>&1 || { cat gpurun_out/ob.txt; exit 1; }
     echo "{\"bmf\": $v, \"shape\": \"$sh\", \"out\": $(grep '^{' gpurun_out/ob.txt | tail -1)}" >> gpurun_out/blur_ab.jsonl
   done
