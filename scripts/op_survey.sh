@@ -15,6 +15,7 @@ reduce --w 1024 --h 1024 --b 4 --n 512 --s 1.3333333333333333
 reduce --w 1920 --h 1080 --b 3 --n 64 --s 1.6
 reduce --w 1920 --h 1080 --b 3 --n 64 --s 2.4
 reduce --w 500 --h 375 --b 3 --n 128 --s 1.46484375
+reduce --w 480 --h 270 --b 3 --n 256 --s 1.6 --s2 1.5976331360946747
 reducev --w 1024 --h 1024 --b 4 --n 512 --s 1.3333333333333333
 reduceh --w 1024 --h 768 --b 4 --n 512 --s 1.3333333333333333
 shrink --w 4000 --h 3000 --b 3 --n 64 --s 8
