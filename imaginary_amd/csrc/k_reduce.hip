@@ -76,6 +76,10 @@ struct Reduce2Args {
     u8 *out;
     int w, h, ow, oh;
     int n_strips, n_bands, band_rows;  // band_rows multiple of kR
+    // computed output region (demand-driven execution, mipx_runtime.cpp plan_demand):
+    // strips from s_base, bands from row y_base (a multiple of kR), clipped at x_end /
+    // y_end; the full image is s_base = y_base = 0, x_end = ow, y_end = oh
+    int s_base, y_base, x_end, y_end;
     long long in_img, out_img;
     // taps pre-scaled by 1/4096 (exact: powers of two); the bias 2^-13 turns the
     // exact chain into RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5) at the cvt
@@ -128,7 +132,7 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
     constexpr int kThreads = G::kThreads, kPitch = G::kPitch;
     constexpr int TW = G::TW, K = G::K;
     const int tid = threadIdx.x;
-    const int x0 = strip * TW;
+    const int x0 = (a.s_base + strip) * TW;
     const int row_bytes = a.w * B;
     const int px0 = 2 * x0 - 5;          // first intermediate pixel of the strip
     const int base = (B * px0) & ~3;     // floor to a dword (two's complement)
@@ -139,13 +143,13 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<u8 *>(a.in + img * a.in_img), 0, static_cast<int>(a.in_img), 0x00020000);
     const uint32_t voff = vlane ? static_cast<uint32_t>(byte0) : 0x80000000u;
-    const int y0 = band * a.band_rows;
-    const int y1 = min(y0 + a.band_rows, a.oh);
+    const int y0 = a.y_base + band * a.band_rows;
+    const int y1 = min(y0 + a.band_rows, a.y_end);
     const float c0 = a.c0, c1 = a.c1, c3 = a.c3, c5 = a.c5, bias = a.bias;
     // strip pixels outside the image (COPY edge): LDS pixels [0, nl) copy pixel 0,
     // [fr, fr_end] copy pixel w-1; filled after each vertical pass
     const int nl = px0 < 0 ? -px0 : 0;
-    const int x_last = min(x0 + TW, a.ow) - 1;
+    const int x_last = min(x0 + TW, a.x_end) - 1;
     const int fr = a.w - px0;                                   // LDS index of pixel w
     const int fr_end = min(2 * x_last + 5 - px0, G::NPX - 1);   // last LDS pixel read
     const int nr = fr_end >= fr ? fr_end - fr + 1 : 0;
@@ -240,7 +244,7 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
             const int j = it - u * items_per_row;
             const int x = x0 + K * j;
             const int y = yc + u;
-            if (y >= a.oh || x >= a.ow) continue;
+            if (y >= a.y_end || x >= a.x_end) continue;
             const uint32_t *row = L + u * kPitch;
             constexpr int W0 = (B * 2 * K) / 4;  // window start (dwords) per item
             uint32_t win[13];
@@ -503,6 +507,14 @@ int reduce2_variant() {
 }
 
 int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_t st) {
+    return reduce2_window_launch(in, out, n, w, h, b, 0, 0, out_size_reduce(w, 2.0), out_size_reduce(h, 2.0), st);
+}
+
+// Only the output region [x0, x1) x [y0, y1) is computed (rounded out to whole
+// strips and 12-row chunks); the rest of the full-size output is left as it was.
+// Every computed pixel is the same sum as in the full launch.
+int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x0, int y0, int x1, int y1,
+                          hipStream_t st) {
     float c[4];
     if (!reduce2_taps(c)) return MIPX_EINVAL;
     Reduce2Args a{};
@@ -512,18 +524,23 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
     a.h = h;
     a.ow = out_size_reduce(w, 2.0);
     a.oh = out_size_reduce(h, 2.0);
+    if (x0 < 0 || y0 < 0 || x1 > a.ow || y1 > a.oh || x0 >= x1 || y0 >= y1) return MIPX_EINVAL;
     const int var = reduce2_variant();
     const int wl = (var & 128) ? 2 : (var & 64) ? 1 : 0;
     const int tw = b == 3 ? (wl == 2 ? R2<3, 2>::TW : wl == 1 ? R2<3, 1>::TW : R2<3>::TW)
                           : (wl == 2 ? R2<4, 2>::TW : wl == 1 ? R2<4, 1>::TW : R2<4>::TW);
-    a.n_strips = (a.ow + tw - 1) / tw;
-    const int chunks = (a.oh + kR - 1) / kR;
+    a.s_base = x0 / tw;
+    a.x_end = x1;
+    a.y_base = y0 / kR * kR;
+    a.y_end = y1;
+    a.n_strips = (x1 + tw - 1) / tw - a.s_base;
+    const int chunks = (y1 - a.y_base + kR - 1) / kR;
     // rows per workgroup: 2 chunks of 12 (measured best, profiles/r01/geom_ab.log; MIPX_R2_BAND overrides)
     const char *eb = std::getenv("MIPX_R2_BAND");
     const int cpb = (eb && *eb) ? std::max(1, std::atoi(eb)) : 2;
     const int chunks_per_band = std::max(1, std::min(chunks, cpb));
     a.band_rows = chunks_per_band * kR;
-    a.n_bands = (a.oh + a.band_rows - 1) / a.band_rows;
+    a.n_bands = (y1 - a.y_base + a.band_rows - 1) / a.band_rows;
     a.in_img = img_bytes(w, h, b);
     a.out_img = img_bytes(a.ow, a.oh, b);
     a.c0 = c[0] / 4096.0f;

@@ -25,6 +25,9 @@ struct ShrinkArgs {
     u8 *out;
     int w, h, ow, oh, hs, vs, tws, x_blocks;
     int ry, y_blocks, lstride;  // k_shrink_x4: output rows per block, row blocks, LDS dwords per row
+    // computed output region (demand-driven execution): column blocks from xb0, rows
+    // from y_base, clipped at x_end / y_end (full image: 0, 0, ow, oh)
+    int xb0, y_base, x_end, y_end;
     float inv_hs, inv_vs;
     long long in_img, out_img;
 };
@@ -36,10 +39,10 @@ __global__ void __launch_bounds__(256) k_shrink_lds(ShrinkArgs a) {
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int xb = t % a.x_blocks;
     const int rest = t / a.x_blocks;
-    const int y = rest % a.oh;
-    const int img = rest / a.oh;
-    const int x0 = xb * a.tws;
-    const int nx = min(a.tws, a.ow - x0);
+    const int y = a.y_base + rest % (a.y_end - a.y_base);
+    const int img = rest / (a.y_end - a.y_base);
+    const int x0 = (a.xb0 + xb) * a.tws;
+    const int nx = min(a.tws, a.x_end - x0);
     const int row_bytes = a.w * B;
     const int span = nx * a.hs * B;           // bytes of the input span, COPY-extended
     const int sb = x0 * a.hs * B;             // first byte (may extend past the row)
@@ -126,16 +129,16 @@ __global__ void __launch_bounds__(256) k_shrink_x4(ShrinkArgs a) {
     const int rest = t / a.x_blocks;
     const int yb = rest % a.y_blocks;
     const int img = rest / a.y_blocks;
-    const int x0 = xb * a.tws;
-    const int nx = min(a.tws, a.ow - x0);
+    const int x0 = (a.xb0 + xb) * a.tws;
+    const int nx = min(a.tws, a.x_end - x0);
     const int row_bytes = a.w * B;
     const int span = nx * a.hs * B;
     const int sb = x0 * a.hs * B;  // multiple of 4: x0 is a multiple of tws >= 4
     const u8 *src = a.in + img * a.in_img;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
     const uint32_t half = a.vs / 2;
-    const int y0 = ROWS ? yb * a.ry : yb;
-    const int ny = ROWS ? min(a.ry, a.oh - y0) : 1;
+    const int y0 = a.y_base + (ROWS ? yb * a.ry : yb);
+    const int ny = ROWS ? min(a.ry, a.y_end - y0) : 1;
     // phase 1: 16 bytes x vs rows -> 16 rounded column means in LDS
     auto chunk = [&](int yy, int d) {
         const int g = sb + d;
@@ -226,6 +229,13 @@ __global__ void __launch_bounds__(256) k_shrink_x4(ShrinkArgs a) {
 }  // namespace
 
 int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int vs, hipStream_t st) {
+    return shrink_window_launch(in, out, n, w, h, b, hs, vs, 0, 0, out_size_shrink(w, hs), out_size_shrink(h, vs), st);
+}
+
+// Only the output region [x0, x1) x [y0, y1) of the full-size output is computed
+// (columns rounded out to whole blocks); each computed pixel is the same box mean.
+int shrink_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int vs, int x0, int y0, int x1,
+                         int y1, hipStream_t st) {
     ShrinkArgs a{};
     a.in = in;
     a.out = out;
@@ -233,6 +243,7 @@ int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int
     a.h = h;
     a.ow = out_size_shrink(w, hs);
     a.oh = out_size_shrink(h, vs);
+    if (x0 < 0 || y0 < 0 || x1 > a.ow || y1 > a.oh || x0 >= x1 || y0 >= y1) return MIPX_EINVAL;
     a.hs = hs;
     a.vs = vs;
     a.inv_hs = 1.0f / hs;
@@ -245,11 +256,15 @@ int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int
         return MIPX_EUNSUPPORTED;
     }
     a.tws = tws;
-    a.x_blocks = (a.ow + tws - 1) / tws;
+    a.xb0 = x0 / tws;
+    a.x_end = x1;
+    a.y_base = y0;
+    a.y_end = y1;
+    a.x_blocks = (x1 + tws - 1) / tws - a.xb0;
     a.in_img = img_bytes(w, h, b);
     a.out_img = img_bytes(a.ow, a.oh, b);
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
-    const long long blocks = static_cast<long long>(a.x_blocks) * a.oh * n;
+    const long long blocks = static_cast<long long>(a.x_blocks) * (y1 - y0) * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const char *ex = std::getenv("MIPX_SHRINK_X4");  // A/B: 0 selects the dword kernel
     const bool x4 = (w * b) % 4 == 0 && a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0 &&
@@ -262,8 +277,8 @@ int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int
         // measured (profiles/r01/v14/ab_shrink_rows.log): only vs <= 3 gains from several rows per block
         int ry = (ery && *ery) ? std::max(1, std::atoi(ery)) : vs <= 3 ? (8 + vs - 1) / vs : 1;
         while (ry > 1 && static_cast<size_t>(ry) * a.lstride * 4 > 32768) --ry;
-        a.ry = std::min(ry, a.oh);
-        a.y_blocks = (a.oh + a.ry - 1) / a.ry;
+        a.ry = std::min(ry, y1 - y0);
+        a.y_blocks = (y1 - y0 + a.ry - 1) / a.ry;
         const long long blocks4 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
         if (!grid_ok(blocks4)) return MIPX_EINVAL;
         const size_t lds16 = static_cast<size_t>(a.ry) * a.lstride * 4;

@@ -112,8 +112,12 @@ int reduce_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, i
                          int top, int ow, int oh, void *ws, size_t ws_bytes, hipStream_t st);
 bool reduce2_eligible(const uint8_t *in, int w, int h, int b, double hs, double vs);
 int reduce2_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, hipStream_t st);
+int reduce2_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int x0, int y0, int x1,
+                          int y1, hipStream_t st);
 // k_shrink.hip
 int shrink_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int hs, int vs, hipStream_t st);
+int shrink_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int hs, int vs, int x0, int y0,
+                         int x1, int y1, hipStream_t st);
 // k_geometry.hip
 int embed_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int x, int y, int ow, int oh,
                  int extend, const int *bg, const int *d_origins, hipStream_t st);
