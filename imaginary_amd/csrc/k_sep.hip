@@ -1468,7 +1468,7 @@ __global__ void __launch_bounds__(256) k_rmfma(RmArgs a) {
 // consecutive intermediate bytes of one output row: one dword write into a
 // row-major intermediate, deinterleaved to channel planes for the horizontal MFMA.
 // Needs 15 vs + vtaps <= 64 staged rows.
-template <int B, int XW>
+template <int B, int XW, int HT>
 __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     constexpr int GPW = XW / 64;
     const int RS = a.rsd;
@@ -1515,6 +1515,33 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
                                                              B * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
         }
     }
+    // HT: the lane's tap fragments (vertical: its output row; horizontal: its pixel of
+    // each group, first K step) are loaded here, while the staged rows are in flight,
+    // instead of after the barriers that precede the two products
+    hm_v4i hbh = hm_v4i{0, 0, 0, 0}, hbl = hbh, hah[GPW], hal[GPW];
+    if constexpr (HT != 0) {
+        const int n = lane & 15, kg = lane >> 4;
+        int sv, ph;
+        sep_position(a.tv, a.oy0 + y0 + min(n, nr - 1), &sv, &ph);
+        const signed char *tv = a.tabv + static_cast<size_t>(ph) * 2 * kHmTabW;
+        const int ov = 16 * kg - (sv - r_lo) + kHmTabPad;
+        hbh = load_taps16(tv, ov);
+        hbl = load_taps16(tv + kHmTabW, ov);
+#pragma unroll
+        for (int gi = 0; gi < GPW; ++gi) {
+            const int g = wave * GPW + gi;
+            hah[gi] = hal[gi] = hm_v4i{0, 0, 0, 0};
+            if (x0 + 16 * g > x_last) continue;
+            int s0, sp, pp;
+            sep_position(a.th, a.ox0 + x0 + 16 * g, &s0, &pp);
+            const int p = min(16 * g + n, x_last - x0);
+            sep_position(a.th, a.ox0 + x0 + p, &sp, &pp);
+            const int o0 = (s0 & ~15) - org + 16 * kg - (sp - org) + kHmTabPad;
+            const signed char *thr = a.tab + static_cast<size_t>(pp) * 2 * kHmTabW;
+            hah[gi] = load_taps16(thr, o0);
+            hal[gi] = load_taps16(thr + kHmTabW, o0);
+        }
+    }
     if (a.dbg & 4) {  // dbg 4: no position set-up (timing only)
     } else if (tid < XW) {
         int sp, ph;
@@ -1534,9 +1561,13 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     // ---- vertical pass on the matrix cores, 16-byte column tiles dealt to the waves ----
     if (!(a.dbg & 2)) {  // dbg 2: no vertical pass, deinterleave or horizontal products (timing only)
         const int n = lane & 15, kg = lane >> 4;
-        const signed char *tv = a.tabv + static_cast<size_t>(vph[n]) * 2 * kHmTabW;
-        const int ov = 16 * kg - vso[n] + kHmTabPad;
-        const hm_v4i bh = load_taps16(tv, ov), bl = load_taps16(tv + kHmTabW, ov);
+        hm_v4i bh = hbh, bl = hbl;
+        if constexpr (HT == 0) {
+            const signed char *tv = a.tabv + static_cast<size_t>(vph[n]) * 2 * kHmTabW;
+            const int ov = 16 * kg - vso[n] + kHmTabPad;
+            bh = load_taps16(tv, ov);
+            bl = load_taps16(tv + kHmTabW, ov);
+        }
         const int vb = vbias[n];
         const int nt = (B * (hi - org + 1) + 15) >> 4;
         const u8 *rawb = reinterpret_cast<const u8 *>(raw);
@@ -1624,8 +1655,14 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
             acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
         }
         for (int ks = 0; ks < ((a.dbg & 2) ? 0 : a.nks); ++ks) {
-            const hm_v4i ah = load_taps16(thr, o0 + 64 * ks);
-            const hm_v4i al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
+            hm_v4i ah, al;
+            if (HT != 0 && ks == 0) {
+                ah = hah[gi];
+                al = hal[gi];
+            } else {
+                ah = load_taps16(thr, o0 + 64 * ks);
+                al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
+            }
 #pragma unroll
             for (int z = 0; z < B; ++z) {
                 const hm_v4i bz =
@@ -2780,13 +2817,25 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         const long long blocks2 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
         if (!grid_ok(blocks2)) return MIPX_EINVAL;
         const dim3 grid2(static_cast<unsigned>(blocks2));
-        if (b == 3) {
-            if (xw == 128) hipLaunchKernelGGL((k_rmf2<3, 128>), grid2, blk, l2, st, a);
-            else hipLaunchKernelGGL((k_rmf2<3, 64>), grid2, blk, l2, st, a);
+        // HT: tap fragments loaded while the staged rows are in flight.  ht_ab.jsonl: RGBA
+        // -5 % (1024^2 / 1.333 1.308 -> 1.246 ms, 1080p / 1.6 0.288 -> 0.275), RGB flat (+-2 %,
+        // the extra registers cost what the hidden latency saves); MIPX_RMF2_HT=0/1 forces
+        const char *he = std::getenv("MIPX_RMF2_HT");
+        const bool ht = (he && *he) ? *he != '0' : b == 4;
+#define MIPX_RMF2_GO(HT_)                                                                 \
+    if (b == 3) {                                                                         \
+        if (xw == 128) hipLaunchKernelGGL((k_rmf2<3, 128, HT_>), grid2, blk, l2, st, a);  \
+        else hipLaunchKernelGGL((k_rmf2<3, 64, HT_>), grid2, blk, l2, st, a);             \
+    } else {                                                                              \
+        if (xw == 128) hipLaunchKernelGGL((k_rmf2<4, 128, HT_>), grid2, blk, l2, st, a);  \
+        else hipLaunchKernelGGL((k_rmf2<4, 64, HT_>), grid2, blk, l2, st, a);             \
+    }
+        if (ht) {
+            MIPX_RMF2_GO(1)
         } else {
-            if (xw == 128) hipLaunchKernelGGL((k_rmf2<4, 128>), grid2, blk, l2, st, a);
-            else hipLaunchKernelGGL((k_rmf2<4, 64>), grid2, blk, l2, st, a);
+            MIPX_RMF2_GO(0)
         }
+#undef MIPX_RMF2_GO
         return launch_check("k_rmf2");
     }
     if (a.rs == 192) { MIPX_RM(192) }
