@@ -1280,6 +1280,7 @@ struct RmArgs {
     int direct;               // k_rmf2: output rows and images dword aligned (12-byte stores, no tile)
     int tiles;                // k_rmf3: 16-row x 128-pixel tiles of the batch (column-major)
     int rsd;                  // k_rmf2: staged row stride in dwords, (rsd mod 64) / 4 odd
+    const signed char *tabs;  // k_rmf4: device_reduce_i8s(hs, B), taps at a byte stride of B
     int dbg;                  // k_rmf2 timing experiments (MIPX_RMF2_DBG, wrong pixels): 1 no staging
                               // loads, 2 no products, 4 no position set-up (rmf2_parts.jsonl)
     SepTaps tv, th;
@@ -1724,6 +1725,249 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
             } else {
                 for (int k = 0; k < 4; ++k)
                     if (e + k >= tb && e + k < nb)
+                        __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
+            }
+        }
+    }
+}
+
+// The 16 bytes of a tap row from byte offset o (any alignment; the row's padding
+// keeps o within it)
+__device__ __forceinline__ hm_v4i load_frag16(const signed char *row, int o) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (o & ~3));
+    const int sh = o & 3;
+    const uint4 d = *reinterpret_cast<const uint4 *>(p);
+    const uint32_t e = p[4];
+    hm_v4i r;
+    r[0] = static_cast<int>(__builtin_amdgcn_alignbyte(d.y, d.x, sh));
+    r[1] = static_cast<int>(__builtin_amdgcn_alignbyte(d.z, d.y, sh));
+    r[2] = static_cast<int>(__builtin_amdgcn_alignbyte(d.w, d.z, sh));
+    r[3] = static_cast<int>(__builtin_amdgcn_alignbyte(e, d.w, sh));
+    return r;
+}
+
+// k_rmf4: k_rmf2 with the horizontal products on the INTERLEAVED intermediate bytes,
+// so the channel planes, their deinterleave pass and its barrier, and the output
+// re-interleave are gone.  A horizontal unit is 16 consecutive output bytes of one
+// row x 16 rows: output byte o = B x + c needs intermediate bytes B (s(x) + k) + c,
+// k = 0 .. taps - 1, so its operand row (M = o) holds tap k at K = B (s(x) - org) + c
+// + B k - kb, where kb is the unit's first tap byte rounded down to 8.  The rows come
+// from the stride-B tap table (device_reduce_i8s) at a per-lane byte offset; B (the
+// pixels) is two ds_read_b64 per lane from the row-major intermediate; the result
+// D[4 consecutive output bytes][row] is one output dword per lane.
+template <int B, int HT>
+__global__ void __launch_bounds__(256) k_rmf4(RmArgs a) {
+    constexpr int XW = kRmXW;
+    constexpr int NU = XW * B / 16;  // 16-byte output units per block row set
+    constexpr int UPW = NU / 4;      // units per wave
+    const int RS = a.rsd;
+    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
+    int *ps = reinterpret_cast<int *>(rsm);  // [XW] first tap pixel
+    int *pph = ps + XW;                      // [XW] phase
+    int *hbb = pph + XW;                     // [XW * B] per output byte: 128 * tap sum + 2048
+    int *vso = hbb + XW * B;                 // [kRmRows] vertical: first staged row of each output row
+    int *vph = vso + kRmRows;                // [kRmRows] phase
+    int *vbias = vph + kRmRows;              // [kRmRows] 128 * tap sum + 2048
+    uint32_t *raw = reinterpret_cast<uint32_t *>(vbias + kRmRows);  // [lrows][RS] staged rows
+    u8 *inter = reinterpret_cast<u8 *>(raw);                         // [kRmRows][iw] (pixel - 128), after the vertical pass
+    u8 *tile = inter + kRmRows * a.iw;                               // [kRmRows][XW * B + 4] unaligned output rows
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int xb = t % a.x_blocks;
+    const int rest = t / a.x_blocks;
+    const int yb = rest % a.y_blocks;
+    const int img = rest / a.y_blocks;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int x0 = xb * XW, x_last = min(x0 + XW - 1, a.ow - 1);
+    const int y0 = yb * kRmRows, nr = min(kRmRows, a.oh - y0);
+    int lo, hi, ph0, r_lo, r_last;
+    sep_position(a.th, a.ox0 + x0, &lo, &ph0);
+    sep_position(a.th, a.ox0 + x_last, &hi, &ph0);
+    hi += a.th.taps - 1;
+    sep_position(a.tv, a.oy0 + y0, &r_lo, &ph0);
+    sep_position(a.tv, a.oy0 + y0 + nr - 1, &r_last, &ph0);
+    const int org = lo & ~15;
+    const int nqv = ((hi - org) >> 2) + 1;
+    const int L = r_last + a.tv.taps - r_lo;
+    {
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
+        const int pitch = a.w * B;
+        const int chunks = (B * nqv + 63) >> 6;
+        for (int l = wave; l < L; l += 4) {
+            const int r = clampi(r_lo + l, 0, a.h - 1);
+            for (int c = 0; c < chunks; ++c)
+                if (c * 64 + lane < RS)  // the last chunk stops at the row stride
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
+                                                             B * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
+        }
+    }
+    const int n = lane & 15, kg = lane >> 4;
+    hm_v4i hbh = hm_v4i{0, 0, 0, 0}, hbl = hbh;
+    if constexpr (HT & 1) {  // the lane's vertical tap fragments, while the rows are in flight
+        int sv, ph;
+        sep_position(a.tv, a.oy0 + y0 + min(n, nr - 1), &sv, &ph);
+        const signed char *tv = a.tabv + static_cast<size_t>(ph) * 2 * kHmTabW;
+        const int ov = 16 * kg - (sv - r_lo) + kHmTabPad;
+        hbh = load_taps16(tv, ov);
+        hbl = load_taps16(tv + kHmTabW, ov);
+    }
+    // HT 2: also every unit's first-K-step tap fragments (UPW x 8 registers)
+    const int nbytes = (x_last - x0 + 1) * B;  // output bytes of this block's rows
+    hm_v4i fh[HT >= 2 ? UPW : 1], fl[HT >= 2 ? UPW : 1];
+    if constexpr (HT >= 2) {
+#pragma unroll
+        for (int ui = 0; ui < UPW; ++ui) {
+            const int u = wave * UPW + ui;
+            fh[ui] = fl[ui] = hm_v4i{0, 0, 0, 0};
+            if (16 * u >= nbytes) continue;
+            const int xf = (16 * u) / B, cf = 16 * u - xf * B;
+            int sf, sp, pp;
+            sep_position(a.th, a.ox0 + x0 + xf, &sf, &pp);
+            const int kb = (B * (sf - org) + cf) & ~7;
+            const int m = min(16 * u + n, nbytes - 1);
+            const int xm = m / B, cm = m - xm * B;
+            sep_position(a.th, a.ox0 + x0 + xm, &sp, &pp);
+            const int off = kRsTabPad + 16 * kg + kb - (B * (sp - org) + cm);
+            const signed char *tr = a.tabs + static_cast<size_t>(pp) * 2 * kRsTabW;
+            fh[ui] = load_frag16(tr, off);
+            fl[ui] = load_frag16(tr + kRsTabW, off);
+        }
+    }
+    if (tid < XW) {
+        int sp, ph;
+        sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
+        ps[tid] = sp;
+        pph[tid] = ph;
+        const int bias = 128 * a.tsum[ph] + 2048;
+#pragma unroll
+        for (int z = 0; z < B; ++z) hbb[B * tid + z] = bias;
+    } else if (tid < XW + kRmRows) {
+        const int k = tid - XW;
+        int sv, ph;
+        sep_position(a.tv, a.oy0 + y0 + min(k, nr - 1), &sv, &ph);
+        vso[k] = sv - r_lo;
+        vph[k] = ph;
+        vbias[k] = 128 * a.tsumv[ph] + 2048;
+    }
+    __syncthreads();
+    // ---- vertical pass on the matrix cores (k_rmf2's), 16-byte column tiles dealt to the waves ----
+    {
+        hm_v4i bh = hbh, bl = hbl;
+        if constexpr ((HT & 1) == 0) {
+            const signed char *tv = a.tabv + static_cast<size_t>(vph[n]) * 2 * kHmTabW;
+            const int ov = 16 * kg - vso[n] + kHmTabPad;
+            bh = load_taps16(tv, ov);
+            bl = load_taps16(tv + kHmTabW, ov);
+        }
+        const int vb = vbias[n];
+        const int nt = (B * (hi - org + 1) + 15) >> 4;
+        const u8 *rawb = reinterpret_cast<const u8 *>(raw);
+        const int r1 = min(16 * kg + (n >> 1), L - 1), r2 = min(16 * kg + 8 + (n >> 1), L - 1);
+        uint32_t res[kRmMaxCt];
+        typedef int v2i_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int i = 0; i < kRmMaxCt; ++i) {
+            const int ct = wave + 4 * i;
+            if (ct >= nt) continue;
+            const int cb = 16 * ct + 8 * (n & 1);
+            const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+                (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r1 * RS * 4 + cb))));
+            const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+                (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r2 * RS * 4 + cb))));
+            const hm_v4i av = hm_v4i{t1.x ^ static_cast<int>(0x80808080u), t1.y ^ static_cast<int>(0x80808080u),
+                                     t2.x ^ static_cast<int>(0x80808080u), t2.y ^ static_cast<int>(0x80808080u)};
+            hm_v4i dh = hm_v4i{0, 0, 0, 0}, dl = hm_v4i{vb, vb, vb, vb};
+            dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
+            dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
+            const uint32_t w = round_pack4((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
+                                           (dh[3] << 6) + dl[3]);
+            res[i] = w ^ 0x80808080u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kRmMaxCt; ++i) {
+            const int ct = wave + 4 * i;
+            if (ct >= nt) continue;
+            *reinterpret_cast<uint32_t *>(inter + n * a.iw + 16 * ct + 4 * kg) = res[i];
+        }
+    }
+    __syncthreads();
+    // ---- COPY edge of the horizontal pass: pixels outside the image repeat its edge ----
+    if (lo < 0 || hi >= a.w) {
+        const int np = hi - org + 1;
+        for (int i = tid; i < nr * np; i += 256) {
+            const int k = i / np, pq = i - k * np;
+            const int p = org + pq;
+            if (p >= 0 && p < a.w) continue;
+            const int src = clampi(p, 0, a.w - 1) - org;
+#pragma unroll
+            for (int z = 0; z < B; ++z) inter[k * a.iw + B * pq + z] = inter[k * a.iw + B * src + z];
+        }
+        __syncthreads();
+    }
+    // ---- horizontal pass: 16-byte output units on the interleaved intermediate ----
+    u8 *ob = a.out + img * a.out_img;
+    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
+    typedef int v2i_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int ui = 0; ui < UPW; ++ui) {
+        const int u = wave * UPW + ui;
+        if (16 * u >= nbytes) break;  // uniform
+        // the unit's first tap byte (output byte 16 u: pixel (16 u) / B, channel (16 u) % B), down to 8
+        const int xf = (16 * u) / B, cf = 16 * u - xf * B;
+        const int kb = (B * (__builtin_amdgcn_readfirstlane(ps[xf]) - org) + cf) & ~7;
+        // this lane's operand row: output byte m = 16 u + n
+        const int m = min(16 * u + n, nbytes - 1);
+        const int xm = m / B, cm = m - xm * B;
+        const int off = kRsTabPad + 16 * kg + kb - (B * (ps[xm] - org) + cm);
+        const signed char *tr = a.tabs + static_cast<size_t>(pph[xm]) * 2 * kRsTabW;
+        const int4 bias = *reinterpret_cast<const int4 *>(hbb + 16 * u + 4 * kg);
+        hm_v4i acc_h = hm_v4i{0, 0, 0, 0}, acc_l = hm_v4i{bias.x, bias.y, bias.z, bias.w};
+        for (int ks = 0; ks < a.nks; ++ks) {
+            hm_v4i ah, al;
+            if (HT >= 2 && ks == 0) {
+                ah = fh[HT >= 2 ? ui : 0];
+                al = fl[HT >= 2 ? ui : 0];
+            } else {
+                ah = load_frag16(tr, off + 64 * ks);
+                al = load_frag16(tr + kRsTabW, off + 64 * ks);
+            }
+            const u8 *src = inter + n * a.iw + kb + 64 * ks + 16 * kg;
+            const v2i_t b0 = *reinterpret_cast<const v2i_t *>(src);
+            const v2i_t b1 = *reinterpret_cast<const v2i_t *>(src + 8);
+            const hm_v4i bv = hm_v4i{b0.x, b0.y, b1.x, b1.y};
+            acc_h = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bv, acc_h, 0, 0, 0);
+            acc_l = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bv, acc_l, 0, 0, 0);
+        }
+        const uint32_t wv = round_pack4((acc_h[0] << 6) + acc_l[0], (acc_h[1] << 6) + acc_l[1],
+                                        (acc_h[2] << 6) + acc_l[2], (acc_h[3] << 6) + acc_l[3]);
+        const int e = 16 * u + 4 * kg;  // first output byte of this lane in the block's row
+        if (n >= nr || e >= nbytes) continue;
+        if (a.direct && e + 4 <= nbytes) {
+            __builtin_amdgcn_raw_buffer_store_b32(wv, os, ((y0 + n) * a.ow + x0) * B + e, 0, 0);
+        } else {
+            *reinterpret_cast<uint32_t *>(tile + n * (XW * B + 4) + e) = wv;
+        }
+    }
+    __syncthreads();
+    // ---- rows through the tile: unaligned output rows, and the partial dword at a row end ----
+    const int tb = a.direct ? (nbytes & ~3) : 0;  // bytes already stored
+    for (int r = wave; r < nr && tb < nbytes; r += 4) {
+        const u8 *tr = tile + r * (XW * B + 4);
+        const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
+        const int qo0 = ((y0 + r) * a.ow + x0) * B + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+        const int d0 = qo0 >> 2, nd = ((qo0 + nbytes + 3) >> 2) - d0;
+        const int sh = (4 - (qo0 & 3)) & 3;
+        const int bias0 = static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
+        for (int i = lane; i < nd; i += 64) {
+            const int e = 4 * (d0 + i) - qo0;
+            if (e + 4 <= tb) continue;
+            if (e >= tb && e + 4 <= nbytes) {
+                const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
+                __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i) - bias0, 0, 0);
+            } else {
+                for (int k = 0; k < 4; ++k)
+                    if (e + k >= tb && e + k < nbytes)
                         __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
             }
         }
@@ -2782,6 +3026,49 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
                 else hipLaunchKernelGGL((k_rmf3<4, 260>), g3, blk, l3, st, a);
             }
             return launch_check("k_rmf3");
+        }
+        // k_rmf4 (horizontal products on the interleaved bytes; an A/B variant, MIPX_RMF4=1,
+        // or 2 with the horizontal fragments hoisted): bit-exact but 1.2-1.5x slower than
+        // k_rmf2 except at / 2.4 (rmf4_ab.jsonl): per output BYTE tap fragments gathered from
+        // a 70 KB table cost more than the channel planes' deinterleave they replace
+        const char *e4 = std::getenv("MIPX_RMF4");
+        if (e4 && (*e4 == '1' || *e4 == '2') && !forced) {
+            const int sp = static_cast<int>(std::ceil((kRmXW - 1) * hs)) + sh.taps + 16;  // >= hi - org + 1
+            int rsd = (b * (sp / 4 + 1) + 3) & ~3;
+            while (((rsd & 63) >> 2) % 2 == 0) rsd += 4;
+            const int iw = ((b * sp + 15) & ~15) + 16;
+            const int dx = (15 + b - 1) / b;  // pixels a 16-byte unit spans beyond its first
+            const int span = b * (static_cast<int>(std::ceil(dx * hs)) + sh.taps - 1) + b - 1 + 8;
+            const int nks = (span + 63) / 64;
+            const size_t l4 = static_cast<size_t>(2 * kRmXW + kRmXW * b + 3 * kRmRows) * 4 +
+                              std::max(static_cast<size_t>(a.lrows) * rsd * 4,
+                                       static_cast<size_t>(kRmRows) * (iw + kRmXW * b + 4));
+            const char *he = std::getenv("MIPX_RMF2_HT");
+            const bool ht = (he && *he) ? *he != '0' : b == 4;
+            int nt4 = 0;
+            a.tabs = device_reduce_i8s(hs, b, &nt4);
+            if (a.tabs && nt4 == sh.taps && nks <= 2 && b * sp <= 16 * 4 * kRmMaxCt && l4 <= 40 * 1024) {
+                a.rsd = rsd;
+                a.iw = iw;
+                a.nks = nks;
+                a.x_blocks = (ow + kRmXW - 1) / kRmXW;
+                a.direct = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0 &&
+                           !(std::getenv("MIPX_RMF2_DIRECT") && *std::getenv("MIPX_RMF2_DIRECT") == '0');
+                const long long blocks4 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
+                if (!grid_ok(blocks4)) return MIPX_EINVAL;
+                const dim3 grid4(static_cast<unsigned>(blocks4));
+                const bool hf = e4 && *e4 == '2';  // MIPX_RMF4=2: horizontal fragments hoisted too
+                if (b == 3) {
+                    if (hf) hipLaunchKernelGGL((k_rmf4<3, 3>), grid4, blk, l4, st, a);
+                    else if (ht) hipLaunchKernelGGL((k_rmf4<3, 1>), grid4, blk, l4, st, a);
+                    else hipLaunchKernelGGL((k_rmf4<3, 0>), grid4, blk, l4, st, a);
+                } else {
+                    if (hf) hipLaunchKernelGGL((k_rmf4<4, 3>), grid4, blk, l4, st, a);
+                    else if (ht) hipLaunchKernelGGL((k_rmf4<4, 1>), grid4, blk, l4, st, a);
+                    else hipLaunchKernelGGL((k_rmf4<4, 0>), grid4, blk, l4, st, a);
+                }
+                return launch_check("k_rmf4");
+            }
         }
         // k_rmf2: 128- or 64-pixel columns; staged rows at the narrowest stride whose
         // (dwords mod 64) / 4 is odd, so a transposed read's 8 rows x 2 halves hit 16 distinct

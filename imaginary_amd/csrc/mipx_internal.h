@@ -58,7 +58,10 @@ const float *device_reduce_table(double shrink, int *n_taps);
 const uint32_t *device_reduce_pairs(double shrink, int *n_taps, int *tpa);
 constexpr int kHmTabW = 64;     // k_hmfma i8 tap rows: bytes per (phase, hi / lo) row (16.5 KB: L1-resident)
 constexpr int kHmTabPad = 16;   // zero bytes in front of tap 0 (taps <= 16; windows clamped to [-16, 16])
+constexpr int kRsTabPad = 128;  // k_rmf4 stride-B tap rows: zero bytes in front of tap 0
+constexpr int kRsTabW = 272;    // bytes per (phase, hi / lo) row: pad + 2 K steps + a fragment (70 KB per table)
 const signed char *device_reduce_i8(double shrink, int *n_taps, const int **sums);
+const signed char *device_reduce_i8s(double shrink, int bands, int *n_taps);  // taps at a byte stride of bands
 // k_bmf's i8 MFMA operands for a blur mask (cached per device): [nks][64][16]
 // horizontal taps at byte stride `bands` shifted by delta, then [64][16] vertical taps
 const signed char *device_blur_ops(const std::vector<int> &mask, int bands, int delta, int nks);

@@ -405,7 +405,7 @@ def test_reduceh_paths(gpu, oracle, rng, monkeypatch, kernel, pack3, s):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract b={b} {kernel}")
 
 
-@pytest.mark.parametrize("on", ["", "3", "3g", "2", "2n", "2t", "1", "0"])
+@pytest.mark.parametrize("on", ["", "4", "4t", "4h", "3", "3g", "2", "2n", "2t", "1", "0"])
 @pytest.mark.parametrize("hs,vs", [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9),
                                    (2.7, 1.5), (1.46484375, 1.46484375), (1.1, 1.05)])
 def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
@@ -416,9 +416,13 @@ def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
     to other kernels (17 taps, unaligned rows).  It is an A/B variant (MIPX_RMFMA=1);
     MIPX_RMFMA=0 runs the default kernels on the same cases; "3g" runs the persistent
     k_rmf3 on 5 workgroups, so each one's run of tiles crosses columns and images; "2n"
-    forces k_rmf2's 64-pixel columns, "2t" k_rmf2 with its tap loads after the barriers."""
-    monkeypatch.setenv("MIPX_RMFMA", on[:1])
-    monkeypatch.setenv("MIPX_RMF2_HT", "0" if on == "2t" else "1")  # "2t": taps after the barriers
+    forces k_rmf2's 64-pixel columns, "2t" k_rmf2 with its tap loads after the barriers.
+    "4" runs the A/B variant k_rmf4 (horizontal products on the interleaved bytes), "4t"
+    the same with its vertical taps loaded after the barrier, "4h" with every tap
+    fragment loaded while the rows are in flight."""
+    monkeypatch.setenv("MIPX_RMFMA", "" if on[:1] == "4" else on[:1])
+    monkeypatch.setenv("MIPX_RMF2_HT", "0" if on in ("2t", "4t") else "1")
+    monkeypatch.setenv("MIPX_RMF4", {"4": "1", "4t": "1", "4h": "2"}.get(on, "0"))
     monkeypatch.setenv("MIPX_RM3_G", "5" if on == "3g" else "0")
     monkeypatch.setenv("MIPX_RMF2_XW", "64" if on == "2n" else "0")
     monkeypatch.setenv("MIPX_RSTRIP", "0")
