@@ -226,6 +226,138 @@ __global__ void __launch_bounds__(256) k_shrink_x4(ShrinkArgs a) {
     for (; y2 < ny; y2 += py, x2 += px, y2 += x2 >= nx ? 1 : 0, x2 -= x2 >= nx ? nx : 0) pixel(y2, x2);
 }
 
+// Small factors (S <= 4, both axes) without LDS: a lane makes 4 output pixels of one
+// row from the S x 4 S input pixels under them, held in registers (S rows of S B
+// dwords, loaded as 16/8/4-byte buffer loads), vertical means first (shrinkv), then
+// horizontal (shrinkh), each (sum + S/2) / S like shrink.c.  Consecutive lanes take
+// consecutive quads of a row, so a wave streams 64 * 4 S B contiguous bytes per input
+// row.  The k_shrink_x4 path stages every row through LDS and reads it back a byte at a
+// time; at S = 2 / 3 that ran at 37 % of HBM (C5 r02).
+template <int B, int S>
+__device__ __forceinline__ void load_row_words(const __amdgpu_buffer_rsrc_t &rs, int off, int roff, uint32_t *w) {
+    constexpr int N = S * B;  // dwords per lane and row
+    int i = 0;
+#pragma unroll
+    for (; i + 4 <= N; i += 4) {
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        const u4v v = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 4 * i, roff, 0));
+        w[i] = v[0], w[i + 1] = v[1], w[i + 2] = v[2], w[i + 3] = v[3];
+    }
+    if constexpr (N % 4 >= 2) {
+        typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+        const u2v v = __builtin_bit_cast(u2v, __builtin_amdgcn_raw_buffer_load_b64(rs, off + 4 * i, roff, 0));
+        w[i] = v[0], w[i + 1] = v[1];
+        i += 2;
+    }
+    if constexpr (N % 2 == 1) w[i] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * i, roff, 0));
+}
+
+template <int B, int S>
+__global__ void __launch_bounds__(256) k_shrink_q(ShrinkArgs a) {
+    constexpr int N = S * B;  // input dwords per lane and row: 4 S pixels
+    const int nq = (a.x_end - 4 * a.xb0 + 3) >> 2;  // quads per computed output row (xb0 in quads here)
+    const long long gq = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
+    const int rows = a.y_end - a.y_base;
+    const long long per_img = static_cast<long long>(nq) * rows;
+    if (gq >= per_img * a.ry) return;  // a.ry = images
+    const int img = static_cast<int>(gq / per_img);
+    const int rem = static_cast<int>(gq - img * per_img);
+    const int y = a.y_base + rem / nq;
+    const int xq = a.xb0 + rem - (rem / nq) * nq;
+    const int x = 4 * xq;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
+    const int row_bytes = a.w * B;
+    uint8_t o[4 * B];
+    if (x + 4 <= a.ow && S * (x + 4) <= a.w) {
+        // ---- vertical means of the S rows, packed u16 pairs (sums <= 4 * 255) ----
+        uint32_t lo[N], hi[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) lo[i] = hi[i] = 0u;
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            uint32_t w[N];
+            load_row_words<B, S>(rs, S * x * B, min(S * y + k, a.h - 1) * row_bytes, w);
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                lo[i] += w[i] & 0x00ff00ffu;
+                hi[i] += (w[i] >> 8) & 0x00ff00ffu;
+            }
+        }
+        uint8_t v[4 * N];  // the vertical means: 4 S pixels of the row
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            v[4 * i + 0] = static_cast<uint8_t>(((lo[i] & 0xffffu) + S / 2) / S);
+            v[4 * i + 1] = static_cast<uint8_t>(((hi[i] & 0xffffu) + S / 2) / S);
+            v[4 * i + 2] = static_cast<uint8_t>(((lo[i] >> 16) + S / 2) / S);
+            v[4 * i + 3] = static_cast<uint8_t>(((hi[i] >> 16) + S / 2) / S);
+        }
+        // ---- horizontal means ----
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                uint32_t sum = 0;
+#pragma unroll
+                for (int k = 0; k < S; ++k) sum += v[(S * p + k) * B + c];
+                o[p * B + c] = static_cast<uint8_t>((sum + S / 2) / S);
+            }
+    } else {  // the row's last quad: pixels past the image repeat its edge (COPY)
+        const u8 *src = a.in + img * a.in_img;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int xo = min(x + p, a.ow - 1);
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                uint32_t sum = 0;
+                for (int k = 0; k < S; ++k) {
+                    const int xi = min(S * xo + k, a.w - 1);
+                    uint32_t vs = 0;
+                    for (int r = 0; r < S; ++r) vs += src[static_cast<size_t>(min(S * y + r, a.h - 1)) * row_bytes + xi * B + c];
+                    sum += (vs + S / 2) / S;
+                }
+                o[p * B + c] = static_cast<uint8_t>((sum + S / 2) / S);
+            }
+        }
+    }
+    // ---- 4 B bytes out: one store when the row position is dword aligned; otherwise
+    // a 1-3 byte head, B - 1 realigned dwords and a 1-3 byte tail ----
+    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
+    const int np = min(4, a.ow - x);
+    const int r = static_cast<int>(reinterpret_cast<uintptr_t>(q) & 3u);
+    uint32_t d[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i)
+        d[i] = o[4 * i] | (static_cast<uint32_t>(o[4 * i + 1]) << 8) | (static_cast<uint32_t>(o[4 * i + 2]) << 16) |
+               (static_cast<uint32_t>(o[4 * i + 3]) << 24);
+    const __amdgpu_buffer_rsrc_t os = image_rsrc(a.out + img * a.out_img, a.out_img);
+    const int qo = (y * a.ow + x) * B;
+    if (np == 4 && r != 0) {
+        const int hb = 4 - r;  // head bytes
+        if (hb & 1) __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(d[0]), os, qo, 0, 0);
+        if (hb & 2)
+            __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(d[0] >> (8 * (hb & 1))), os, qo + (hb & 1), 0, 0);
+#pragma unroll
+        for (int j = 0; j + 1 < B; ++j)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_alignbyte(d[j + 1], d[j], hb), os, qo + hb + 4 * j, 0, 0);
+        const uint32_t tl = d[B - 1] >> (8 * hb);  // the last r bytes
+        const int to = qo + 4 * B - r;
+        if (r & 2) __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(tl), os, to, 0, 0);
+        if (r & 1) __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(tl >> (8 * (r & 2))), os, to + (r & 2), 0, 0);
+    } else if (np == 4) {
+        if constexpr (B == 3) {
+            typedef int v3i_t __attribute__((ext_vector_type(3)));
+            __builtin_amdgcn_raw_buffer_store_b96(v3i_t{static_cast<int>(d[0]), static_cast<int>(d[1]),
+                                                        static_cast<int>(d[2])}, os, qo, 0, 0);
+        } else {
+            typedef int v4i_t __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(v4i_t{static_cast<int>(d[0]), static_cast<int>(d[1]),
+                                                         static_cast<int>(d[2]), static_cast<int>(d[3])}, os, qo, 0, 0);
+        }
+    } else {
+        for (int i = 0; i < np * B; ++i) q[i] = o[i];
+    }
+}
+
 }  // namespace
 
 int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int vs, hipStream_t st) {
@@ -266,6 +398,24 @@ int shrink_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int 
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     const long long blocks = static_cast<long long>(a.x_blocks) * (y1 - y0) * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
+    // S <= 4 on both axes, dword-aligned rows: the register-only quad kernel (MIPX_SHRINK_Q=0: off)
+    const char *eq = std::getenv("MIPX_SHRINK_Q");
+    if (!(eq && *eq == '0') && hs == vs && hs >= 2 && hs <= 4 && (b == 3 || b == 4) && (w * b) % 4 == 0 &&
+        a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0) {
+        ShrinkArgs q = a;
+        q.xb0 = x0 / 4;  // in quads
+        q.ry = n;        // images
+        const long long quads = static_cast<long long>((x1 - 4 * q.xb0 + 3) / 4) * (y1 - y0) * n;
+        const long long qblocks = (quads + 255) / 256;
+        if (!grid_ok(qblocks)) return MIPX_EINVAL;
+        const dim3 g(static_cast<unsigned>(qblocks));
+#define MIPX_SQ(S_)                                                                                   \
+    if (b == 3) hipLaunchKernelGGL((k_shrink_q<3, S_>), g, dim3(256), 0, st, q);                      \
+    else hipLaunchKernelGGL((k_shrink_q<4, S_>), g, dim3(256), 0, st, q);
+        if (hs == 2) { MIPX_SQ(2) } else if (hs == 3) { MIPX_SQ(3) } else { MIPX_SQ(4) }
+#undef MIPX_SQ
+        return launch_check("k_shrink_q");
+    }
     const char *ex = std::getenv("MIPX_SHRINK_X4");  // A/B: 0 selects the dword kernel
     const bool x4 = (w * b) % 4 == 0 && a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0 &&
                     vs <= 257 && tws >= 4 && !(ex && *ex == '0');

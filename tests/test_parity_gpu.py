@@ -228,6 +228,24 @@ def test_shrink_x4_and_dword_kernels(gpu, oracle, rng, monkeypatch, x4):
             assert_same(got[i], oracle.shrink(imgs[i], hs, vs), f"shrink {h}x{w}x{b} {hs}x{vs} x4={x4}")
 
 
+@pytest.mark.parametrize("q", ["1", "0"])
+@pytest.mark.parametrize("s", [2, 3, 4])
+def test_shrink_quad_kernel(gpu, oracle, rng, monkeypatch, q, s):
+    """Small equal factors (k_shrink_q: registers only, 4 output pixels per lane)
+    against the oracle and against the LDS kernels (MIPX_SHRINK_Q=0): widths that end
+    inside a quad and past the last whole box (COPY border), odd heights, output rows
+    that are not dword aligned (byte stores), RGB and RGBA, batches of 2."""
+    monkeypatch.setenv("MIPX_SHRINK_Q", q)
+    for h, w, b in ((64, 400, 3), (37, 1000, 3), (9, 4000 // 3 * 3 // 4 * 4, 3), (33, 84, 3), (5, 12, 3), (70, 333 * 4, 4),
+                    (41, 52, 4), (3, 4, 4), (17, 1276, 3)):
+        if (w * b) % 4:
+            continue
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("shrink", imgs, hshrink=s, vshrink=s)
+        for i in range(2):
+            assert_same(got[i], oracle.shrink(imgs[i], s, s), f"shrink q={q} {h}x{w}x{b} /{s}")
+
+
 # ---------------------------------------------------------------- gaussian blur
 @pytest.mark.parametrize("sigma", [0.8, 1.0, 3.0, 5.0, 12.5])
 @pytest.mark.parametrize("b", [1, 3, 4])
