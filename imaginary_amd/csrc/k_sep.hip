@@ -1505,7 +1505,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     const int nqv = ((hi - org) >> 2) + 1;
     const int L = r_last + a.tv.taps - r_lo;
     {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img + 3);  // rows of any alignment: a dword may start at any of the last bytes
         const int pitch = a.w * B;
         const int chunks = (B * nqv + 63) >> 6;
         for (int l = (a.dbg & 1) ? L : wave; l < L; l += 4) {  // dbg 1: no staging loads (timing only)
@@ -1790,7 +1790,7 @@ __global__ void __launch_bounds__(256) k_rmf4(RmArgs a) {
     const int nqv = ((hi - org) >> 2) + 1;
     const int L = r_last + a.tv.taps - r_lo;
     {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img + 3);  // rows of any alignment: a dword may start at any of the last bytes
         const int pitch = a.w * B;
         const int chunks = (B * nqv + 63) >> 6;
         for (int l = wave; l < L; l += 4) {
@@ -2931,9 +2931,16 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
     const bool v2 = !forced || *e == '2' || *e == '3';
     const bool v3 = forced && *e == '3';
     const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
-    if ((b != 3 && b != 4) || !(hs > 1.0) || !(vs > 1.0) || (w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0 ||
-        in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL)
+    if ((b != 3 && b != 4) || !(hs > 1.0) || !(vs > 1.0) || in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL)
         return MIPX_EUNSUPPORTED;
+    // k_rmf2 stages rows of any alignment: a direct-to-LDS dword load honours a byte
+    // offset that is not a multiple of 4 (scripts/probe/lds_dma_unaligned.hip,
+    // profiles/r02/lds_dma_unaligned.jsonl), so 1333 x 1000 RGB rows (3999 bytes) take
+    // it too; the A/B kernels k_rmfma / k_rmf3 keep the dword-aligned rows they were
+    // built for (MIPX_RMF2_UNALIGNED=0 restores that limit for k_rmf2 as well)
+    const bool rows_aligned = (w * b) % 4 == 0 && reinterpret_cast<uintptr_t>(in) % 4 == 0;
+    const char *eu = std::getenv("MIPX_RMF2_UNALIGNED");
+    if (!rows_aligned && ((e && (*e == '1' || *e == '3')) || (eu && *eu == '0'))) return MIPX_EUNSUPPORTED;
     SepSpec sh, sv;
     if (!sep_spec_reduce(hs, &sh) || !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
     if (sh.taps > 16 || sv.taps > 16) return MIPX_EUNSUPPORTED;

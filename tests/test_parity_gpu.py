@@ -446,7 +446,7 @@ def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
     monkeypatch.setenv("MIPX_RSTRIP", "0")
     monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
     for h, w, b in ((301, 1100, 3), (97, 640, 3), (13, 200, 3), (40, 36, 3), (270, 480, 3), (37, 1026, 3),
-                    (150, 97, 3), (201, 700, 4), (19, 333, 4), (64, 1024, 4)):
+                    (150, 97, 3), (201, 700, 4), (19, 333, 4), (64, 1024, 4), (101, 1333, 3), (99, 1331, 3)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
         got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
         for i in range(2):
