@@ -1281,6 +1281,7 @@ struct RmArgs {
     int tiles;                // k_rmf3: 16-row x 128-pixel tiles of the batch (column-major)
     int rsd;                  // k_rmf2: staged row stride in dwords, (rsd mod 64) / 4 odd
     const signed char *tabs;  // k_rmf4: device_reduce_i8s(hs, B), taps at a byte stride of B
+    int orgmask;              // k_rmf2: first staged pixel = lo & orgmask (~3; ~15 is the r02 A/B)
     int dbg;                  // k_rmf2 timing experiments (MIPX_RMF2_DBG, wrong pixels): 1 no staging
                               // loads, 2 no products, 4 no position set-up (rmf2_parts.jsonl)
     SepTaps tv, th;
@@ -1501,7 +1502,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     hi += a.th.taps - 1;
     sep_position(a.tv, a.oy0 + y0, &r_lo, &ph0);
     sep_position(a.tv, a.oy0 + y0 + nr - 1, &r_last, &ph0);
-    const int org = lo & ~15;
+    const int org = lo & a.orgmask;  // first staged pixel: floor to 4 (r02; 16 before, MIPX_RMF2_ORG=16)
     const int nqv = ((hi - org) >> 2) + 1;
     const int L = r_last + a.tv.taps - r_lo;
     {
@@ -1537,7 +1538,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
             sep_position(a.th, a.ox0 + x0 + 16 * g, &s0, &pp);
             const int p = min(16 * g + n, x_last - x0);
             sep_position(a.th, a.ox0 + x0 + p, &sp, &pp);
-            const int o0 = (s0 & ~15) - org + 16 * kg - (sp - org) + kHmTabPad;
+            const int o0 = ((s0 - org) & ~15) + 16 * kg - (sp - org) + kHmTabPad;
             const signed char *thr = a.tab + static_cast<size_t>(pp) * 2 * kHmTabW;
             hah[gi] = load_taps16(thr, o0);
             hal[gi] = load_taps16(thr + kHmTabW, o0);
@@ -1644,7 +1645,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     for (int gi = 0; gi < GPW; ++gi) {
         const int g = wave * GPW + gi;
         if (x0 + 16 * g > x_last) break;
-        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
+        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) - org) & ~15;  // plane offset of the group's window
         const int p = min(16 * g + n, x_last - x0);
         const int o0 = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
         const signed char *thr = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
@@ -3086,9 +3087,16 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         const bool rs_wide = re && *re == '1';
         size_t l2 = 0;
         int xw = 0;
+        // staged pixels start at lo floored to 4 (the planes are indexed from there, so the
+        // horizontal windows need no 16-pixel origin): 12 fewer pixels per row, and staged
+        // rows for ceil(15 vs) + taps + 1 output-row windows; MIPX_RMF2_ORG=16 is the r02 layout
+        const char *eo = std::getenv("MIPX_RMF2_ORG");
+        const bool org16 = eo && std::atoi(eo) == 16;
+        a.orgmask = org16 ? ~15 : ~3;
+        const int lrows2 = org16 ? a.lrows : static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps + 1;
         for (const int x : {128, 64}) {
             if (xw_only && x != xw_only) continue;
-            const int sp = static_cast<int>(std::ceil((x - 1) * hs)) + sh.taps + 16;  // >= hi - org + 1
+            const int sp = static_cast<int>(std::ceil((x - 1) * hs)) + sh.taps + (org16 ? 16 : 4);  // >= hi - org + 1
             int rsd = (b * (sp / 4 + 1) + 3) & ~3;
             while (((rsd & 63) >> 2) % 2 == 0) rsd += 4;
             if (rs_wide) rsd = std::max(192, (b * (sp / 4 + 1) + 63) / 64 * 64) + 4;  // A/B: the r02 stride
@@ -3096,7 +3104,7 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
             const int rw = b * pw + ((b * pw / 16) % 2 == 0 ? 16 : 0);
             const int iw = ((b * sp + 15) & ~15) + 16;
             const size_t lx = static_cast<size_t>(3 * x + 3 * kRmRows) * 4 +
-                              std::max(static_cast<size_t>(a.lrows) * rsd * 4, static_cast<size_t>(kRmRows) * (iw + rw) + 64 + 16);
+                              std::max(static_cast<size_t>(lrows2) * rsd * 4, static_cast<size_t>(kRmRows) * (iw + rw) + 64 + 16);
             if (b * sp > 16 * 4 * kRmMaxCt || x * b + 4 > iw) continue;
             if (xw == 0 || (l2 > 32 * 1024 && lx < l2)) {
                 xw = x, l2 = lx, a.rsd = rsd, a.plane_w = pw, a.row_w = rw, a.iw = iw;

@@ -423,7 +423,7 @@ def test_reduceh_paths(gpu, oracle, rng, monkeypatch, kernel, pack3, s):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract b={b} {kernel}")
 
 
-@pytest.mark.parametrize("on", ["", "4", "4t", "4h", "3", "3g", "2", "2n", "2t", "1", "0"])
+@pytest.mark.parametrize("on", ["", "2o", "4", "4t", "4h", "3", "3g", "2", "2n", "2t", "1", "0"])
 @pytest.mark.parametrize("hs,vs", [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9),
                                    (2.7, 1.5), (1.46484375, 1.46484375), (1.1, 1.05)])
 def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
@@ -441,6 +441,7 @@ def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
     monkeypatch.setenv("MIPX_RMFMA", "" if on[:1] == "4" else on[:1])
     monkeypatch.setenv("MIPX_RMF2_HT", "0" if on in ("2t", "4t") else "1")
     monkeypatch.setenv("MIPX_RMF4", {"4": "1", "4t": "1", "4h": "2"}.get(on, "0"))
+    monkeypatch.setenv("MIPX_RMF2_ORG", "16" if on == "2o" else "4")  # "2o": the r02 16-pixel staging origin
     monkeypatch.setenv("MIPX_RM3_G", "5" if on == "3g" else "0")
     monkeypatch.setenv("MIPX_RMF2_XW", "64" if on == "2n" else "0")
     monkeypatch.setenv("MIPX_RSTRIP", "0")
