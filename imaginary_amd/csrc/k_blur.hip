@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(256) k_blur2d(Blur2DArgs a) {
 typedef int bm_v4i __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void bm_lds_void;
 __device__ __forceinline__ bm_lds_void *bm_lds(void *p) { return (bm_lds_void *)p; }
-constexpr int kBmRows = 16, kBmXW = 128, kBmMaxKs = 3, kBmMaxRg = 3, kBmMaxCt = 8;
+constexpr int kBmXW = 128, kBmMaxKs = 3, kBmMaxCt = 8;
 
 struct BmArgs {
     const u8 *in;
@@ -338,8 +338,12 @@ __device__ __forceinline__ uint32_t bm_pack(const bm_v4i &d, uint32_t mag) {
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
-template <int B>
+// RG: 16-row output groups per block (2: 32 output rows from 31 + taps staged rows, so
+// the horizontal products and the row loads per output row drop from (16 + taps - 1) / 16
+// to (32 + taps - 1) / 32)
+template <int B, int RG>
 __global__ void __launch_bounds__(256) k_bmf(BmArgs a) {
+    constexpr int ROWS = 16 * RG, MAXRG = RG + 2;
     extern __shared__ __attribute__((aligned(16))) uint32_t bsm[];
     uint32_t *raw = bsm;                   // [L][rsd] staged rows
     u8 *rawb = reinterpret_cast<u8 *>(bsm);
@@ -352,7 +356,7 @@ __global__ void __launch_bounds__(256) k_bmf(BmArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int x0 = xb * kBmXW, xw = min(kBmXW, a.w - x0);
-    const int y0 = yb * kBmRows, nr = min(kBmRows, a.h - y0);
+    const int y0 = yb * ROWS, nr = min(ROWS, a.h - y0);
     const int L = nr + a.taps - 1;
     const int sx = x0 - a.sx0;                       // first staged window pixel
     const int spx = xw + a.taps - 1 + (a.sx0 - a.half);  // staged pixels per row
@@ -390,9 +394,9 @@ __global__ void __launch_bounds__(256) k_bmf(BmArgs a) {
         const int ngr = (xw * B + 15) >> 4, nrg = (L + 15) >> 4;
         const int kb0 = a.e & ~3;
         // unit (row group rg, 16-byte group g = wave + 4 j): no divisions, static register slots
-        uint32_t res[kBmMaxRg][kBmMaxCt];
+        uint32_t res[MAXRG][kBmMaxCt];
 #pragma unroll
-        for (int rg = 0; rg < kBmMaxRg; ++rg) {
+        for (int rg = 0; rg < MAXRG; ++rg) {
             if (rg >= nrg) break;  // uniform
             const int row = min(16 * rg + n, L - 1);
             const u8 *rrow = rawb + row * a.rsd * 4 + kb0 + 16 * kg;
@@ -414,7 +418,7 @@ __global__ void __launch_bounds__(256) k_bmf(BmArgs a) {
         }
         __syncthreads();
 #pragma unroll
-        for (int rg = 0; rg < kBmMaxRg; ++rg) {
+        for (int rg = 0; rg < MAXRG; ++rg) {
             if (rg >= nrg) break;
             if (16 * rg + n >= L) continue;
             u8 *trow = tm + (16 * rg + n) * a.tw + 4 * kg;
@@ -431,29 +435,35 @@ __global__ void __launch_bounds__(256) k_bmf(BmArgs a) {
     {
         const bm_v4i tb = *reinterpret_cast<const bm_v4i *>(a.ops + (a.nks * 64 + lane) * 16);
         const int nct = (xw * B + 15) >> 4;
-        const int r1 = min(16 * kg + (n >> 1), L - 1), r2 = min(16 * kg + 8 + (n >> 1), L - 1);
         typedef int v2i_t __attribute__((ext_vector_type(2)));
-        uint32_t res[kBmMaxCt];
+        uint32_t res[RG][kBmMaxCt];
 #pragma unroll
-        for (int i = 0; i < kBmMaxCt; ++i) {
-            const int ct = wave + 4 * i;
-            if (ct >= nct) continue;
-            const int cb = 16 * ct + 8 * (n & 1);
-            const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                (__attribute__((address_space(3))) v2i_t *)(bm_lds(tm + r1 * a.tw + cb)));
-            const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                (__attribute__((address_space(3))) v2i_t *)(bm_lds(tm + r2 * a.tw + cb)));
-            const bm_v4i av = bm_v4i{t1.x, t1.y, t2.x, t2.y};
-            const bm_v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, tb, bm_v4i{a.seed, a.seed, a.seed, a.seed}, 0, 0, 0);
-            res[i] = bm_pack(d, a.mag);
+        for (int g = 0; g < RG; ++g) {  // output rows 16 g .. 16 g + 15 from intermediate rows 16 g ..
+            const int r1 = min(16 * g + 16 * kg + (n >> 1), L - 1), r2 = min(16 * g + 16 * kg + 8 + (n >> 1), L - 1);
+#pragma unroll
+            for (int i = 0; i < kBmMaxCt; ++i) {
+                const int ct = wave + 4 * i;
+                if (ct >= nct) continue;
+                const int cb = 16 * ct + 8 * (n & 1);
+                const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+                    (__attribute__((address_space(3))) v2i_t *)(bm_lds(tm + r1 * a.tw + cb)));
+                const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+                    (__attribute__((address_space(3))) v2i_t *)(bm_lds(tm + r2 * a.tw + cb)));
+                const bm_v4i av = bm_v4i{t1.x, t1.y, t2.x, t2.y};
+                const bm_v4i d =
+                    __builtin_amdgcn_mfma_i32_16x16x64_i8(av, tb, bm_v4i{a.seed, a.seed, a.seed, a.seed}, 0, 0, 0);
+                res[g][i] = bm_pack(d, a.mag);
+            }
         }
         __syncthreads();  // every wave is done with the intermediate: the output tile goes over it
 #pragma unroll
-        for (int i = 0; i < kBmMaxCt; ++i) {
-            const int ct = wave + 4 * i;
-            if (ct >= nct) continue;
-            *reinterpret_cast<uint32_t *>(tm + n * a.tw + 16 * ct + 4 * kg) = res[i];
-        }
+        for (int g = 0; g < RG; ++g)
+#pragma unroll
+            for (int i = 0; i < kBmMaxCt; ++i) {
+                const int ct = wave + 4 * i;
+                if (ct >= nct) continue;
+                *reinterpret_cast<uint32_t *>(tm + (16 * g + n) * a.tw + 16 * ct + 4 * kg) = res[g][i];
+            }
     }
     __syncthreads();
     {
@@ -515,8 +525,17 @@ int blur_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left
     if (a.in_img >= 0x7fffffffLL - 1024 || a.out_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     a.w = ow;
     a.h = oh;
+    // output rows per block: 32 where the image has them, 48 for short masks (the staged
+    // halo is taps - 1 rows per block, so taller blocks redo less of the horizontal pass
+    // and reload fewer rows; bmf_rg_ab.jsonl / bmf_rg3_ab.jsonl: 32 rows -17 to -21 % on
+    // RGB at sigma 1-5, 48 rows a further -7 % at sigma 1 and +1-5 % at sigma 3-5);
+    // MIPX_BMF_RG=1/2/3 forces 16 / 32 / 48
+    const char *eg = std::getenv("MIPX_BMF_RG");
+    const int rg = (eg && *eg) ? std::min(3, std::max(1, std::atoi(eg)))
+                               : (oh >= 48 && taps <= 7) ? 3 : (oh >= 32 ? 2 : 1);
+    const int rows = 16 * rg;
     a.x_blocks = (ow + kBmXW - 1) / kBmXW;
-    a.y_blocks = (oh + kBmRows - 1) / kBmRows;
+    a.y_blocks = (oh + rows - 1) / rows;
     a.taps = taps;
     a.half = taps / 2;
     a.sx0 = b == 3 ? (a.half + 3) & ~3 : a.half;  // RGB: staged rows start on a 4-pixel (3-dword) boundary
@@ -533,8 +552,8 @@ int blur_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left
     twd = (twd + 3) & ~3;
     while (((twd & 63) >> 2) % 2 == 0) twd += 4;
     a.tw = 4 * twd;
-    const int lmax = kBmRows + taps - 1;
-    if ((lmax + 15) / 16 > kBmMaxRg || (kBmXW * b + 15) / 16 > 4 * kBmMaxCt)
+    const int lmax = rows + taps - 1;
+    if ((lmax + 15) / 16 > rg + 2 || (kBmXW * b + 15) / 16 > 4 * kBmMaxCt)
         return MIPX_EUNSUPPORTED;
     // horizontal B reads run up to 64 nks bytes past a group's start: slack after the last row
     const size_t lds = std::max(static_cast<size_t>(lmax) * rsd * 4, static_cast<size_t>(lmax) * a.tw) + 64 * a.nks + 64;
@@ -547,8 +566,16 @@ int blur_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left
     const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
-    if (b == 3) hipLaunchKernelGGL((k_bmf<3>), grid, blk, lds, st, a);
-    else hipLaunchKernelGGL((k_bmf<4>), grid, blk, lds, st, a);
+    if (rg == 3) {
+        if (b == 3) hipLaunchKernelGGL((k_bmf<3, 3>), grid, blk, lds, st, a);
+        else hipLaunchKernelGGL((k_bmf<4, 3>), grid, blk, lds, st, a);
+    } else if (rg == 2) {
+        if (b == 3) hipLaunchKernelGGL((k_bmf<3, 2>), grid, blk, lds, st, a);
+        else hipLaunchKernelGGL((k_bmf<4, 2>), grid, blk, lds, st, a);
+    } else {
+        if (b == 3) hipLaunchKernelGGL((k_bmf<3, 1>), grid, blk, lds, st, a);
+        else hipLaunchKernelGGL((k_bmf<4, 1>), grid, blk, lds, st, a);
+    }
     return launch_check("k_bmf");
 }
 

@@ -291,7 +291,7 @@ def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma,
             assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur2d {sigma} {h}x{w}x{b} rows={rows} fr={fround} img{i}")
 
 
-@pytest.mark.parametrize("on", ["1", "0"])
+@pytest.mark.parametrize("on", ["1", "1r", "1t", "0"])
 @pytest.mark.parametrize("sigma", [0.3, 1.0, 2.2, 5.0, 7.5, 9.0, 12.5])
 def test_blur_mfma_matches_oracle(gpu, oracle, rng, monkeypatch, on, sigma):
     """k_bmf (both convsep passes on the i8 matrix cores: horizontal on the
@@ -300,10 +300,12 @@ def test_blur_mfma_matches_oracle(gpu, oracle, rng, monkeypatch, on, sigma):
     shorter than the mask, several column and row blocks, both edges of every
     window, windowed plans (resize -> crop -> blur) at every gravity, and the
     cases it leaves to k_blur2d (unaligned rows, 1-2 bands, > 33 taps).  "0" runs
-    k_blur2d on the same cases."""
-    monkeypatch.setenv("MIPX_BMF", on)
+    k_blur2d on the same cases; "1" uses 32-row blocks where the image has 32 rows,
+    "1r" the 16-row blocks, "1t" 48-row blocks."""
+    monkeypatch.setenv("MIPX_BMF", on[:1])
+    monkeypatch.setenv("MIPX_BMF_RG", {"1r": "1", "1t": "3"}.get(on, ""))
     for h, w, b in ((64, 76, 3), (130, 516, 3), (9, 600, 4), (50, 260, 4), (3, 8, 4), (33, 20, 3), (17, 132, 3),
-                    (200, 388, 4), (33, 19, 3), (29, 41, 2), (41, 57, 1)):
+                    (200, 388, 4), (33, 19, 3), (29, 41, 2), (41, 57, 1), (47, 140, 3), (95, 300, 4)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
         got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
         for i in range(2):
