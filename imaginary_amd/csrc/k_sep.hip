@@ -1506,15 +1506,21 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     const int nqv = ((hi - org) >> 2) + 1;
     const int L = r_last + a.tv.taps - r_lo;
     {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img + 3);  // rows of any alignment: a dword may start at any of the last bytes
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
         const int pitch = a.w * B;
         const int chunks = (B * nqv + 63) >> 6;
         for (int l = (a.dbg & 1) ? L : wave; l < L; l += 4) {  // dbg 1: no staging loads (timing only)
             const int r = clampi(r_lo + l, 0, a.h - 1);
             for (int c = 0; c < chunks; ++c)
-                if (c * 64 + lane < RS)  // the last chunk stops at the row stride
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
-                                                             B * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
+                if (c * 64 + lane < RS) {  // the last chunk stops at the row stride
+                    // rows of any alignment: a dword that starts in the image's last 3 bytes
+                    // would be dropped whole by the range check, so it is loaded ending at
+                    // the image's last byte and shifted into place below (tail fix-up)
+                    int vo = B * org + 4 * (c * 64 + lane);
+                    const int over = r * pitch + vo + 4 - static_cast<int>(a.in_img);
+                    if (over > 0 && over < 4) vo -= over;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4, vo, r * pitch, 0, 0);
+                }
         }
     }
     // HT: the lane's tap fragments (vertical: its output row; horizontal: its pixel of
@@ -1560,6 +1566,22 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
         vbias[k] = 128 * a.tsumv[ph] + 2048;
     }
     __syncthreads();
+    // ---- tail fix-up: blocks that stage the image's last row with a row end off the dword grid ----
+    if ((a.w * B) % 4 != 0 && r_lo + L > a.h - 1 && !(a.dbg & 1)) {  // uniform
+        const int pitch = a.w * B;
+        const int chunks = (B * nqv + 63) >> 6;
+        for (int l = wave; l < L; l += 4) {
+            if (clampi(r_lo + l, 0, a.h - 1) != a.h - 1) continue;
+            for (int c = 0; c < chunks; ++c) {
+                const int over = (a.h - 1) * pitch + B * org + 4 * (c * 64 + lane) + 4 - static_cast<int>(a.in_img);
+                if (c * 64 + lane < RS && over > 0 && over < 4) {
+                    uint32_t *q = raw + l * RS + c * 64 + lane;
+                    *q = *q >> (8 * over);
+                }
+            }
+        }
+        __syncthreads();
+    }
     // ---- vertical pass on the matrix cores, 16-byte column tiles dealt to the waves ----
     if (!(a.dbg & 2)) {  // dbg 2: no vertical pass, deinterleave or horizontal products (timing only)
         const int n = lane & 15, kg = lane >> 4;
@@ -1791,7 +1813,7 @@ __global__ void __launch_bounds__(256) k_rmf4(RmArgs a) {
     const int nqv = ((hi - org) >> 2) + 1;
     const int L = r_last + a.tv.taps - r_lo;
     {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img + 3);  // rows of any alignment: a dword may start at any of the last bytes
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
         const int pitch = a.w * B;
         const int chunks = (B * nqv + 63) >> 6;
         for (int l = wave; l < L; l += 4) {
@@ -3040,7 +3062,7 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         // k_rmf2 except at / 2.4 (rmf4_ab.jsonl): per output BYTE tap fragments gathered from
         // a 70 KB table cost more than the channel planes' deinterleave they replace
         const char *e4 = std::getenv("MIPX_RMF4");
-        if (e4 && (*e4 == '1' || *e4 == '2') && !forced) {
+        if (e4 && (*e4 == '1' || *e4 == '2') && !forced && rows_aligned) {
             const int sp = static_cast<int>(std::ceil((kRmXW - 1) * hs)) + sh.taps + 16;  // >= hi - org + 1
             int rsd = (b * (sp / 4 + 1) + 3) & ~3;
             while (((rsd & 63) >> 2) % 2 == 0) rsd += 4;

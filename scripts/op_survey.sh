@@ -22,6 +22,9 @@ shrink --w 4000 --h 3000 --b 3 --n 64 --s 8
 shrink --w 4000 --h 3000 --b 3 --n 64 --s 11
 shrink --w 3840 --h 2160 --b 3 --n 64 --s 4
 shrink --w 1920 --h 1080 --b 3 --n 64 --s 3
+shrink --w 3840 --h 2160 --b 3 --n 32 --s 2
+shrink --w 4000 --h 3000 --b 3 --n 32 --s 3
+reduce --w 1333 --h 1000 --b 3 --n 48 --s 1.6666666666666667
 blur --w 768 --h 512 --b 4 --n 512 --s 5
 blur --w 1920 --h 1080 --b 3 --n 64 --s 1
 blur --w 1920 --h 1080 --b 3 --n 64 --s 3
