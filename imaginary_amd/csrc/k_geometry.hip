@@ -31,6 +31,7 @@ struct RemapArgs {
     u8 fill[4];
     long long in_img, out_img;
     const int *origins;  // extract with per-image (left, top) from the device (smartcrop)
+    int q16;             // k_embed_rows: 16-byte source loads where the row offset is dword aligned
 };
 
 __device__ __forceinline__ uint32_t load_px(const u8 *p, int B) {
@@ -144,11 +145,17 @@ __global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
     } else if (j0 / B - ox >= 0 && (j0 + 15) / B - ox < a.w) {  // interior: shifted row copy
         const int o = sy * a.w * B + (j0 - ox * B);
         const int o4 = o & ~3, sh = o & 3;
-        uint32_t w[5];
+        if (sh == 0 && a.q16) {  // dword-aligned source: one 16-byte load (r02: was 5 dword loads)
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+            const u4v t = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+            v[0] = t[0], v[1] = t[1], v[2] = t[2], v[3] = t[3];
+        } else {
+            uint32_t w[5];
 #pragma unroll
-        for (int d = 0; d < 5; ++d) w[d] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 4 * d, 0, 0));
+            for (int d = 0; d < 5; ++d) w[d] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 4 * d, 0, 0));
 #pragma unroll
-        for (int d = 0; d < 4; ++d) v[d] = __builtin_amdgcn_alignbyte(w[d + 1], w[d], sh);  // (hi:lo) >> 8 sh
+            for (int d = 0; d < 4; ++d) v[d] = __builtin_amdgcn_alignbyte(w[d + 1], w[d], sh);  // (hi:lo) >> 8 sh
+        }
     } else {
         const long long rowb = static_cast<long long>(sy) * a.w * B;
 #pragma unroll 1
@@ -433,6 +440,8 @@ int embed_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x, int y
     a.in_img = img_bytes(w, h, b);
     a.out_img = img_bytes(ow, oh, b);
     a.origins = d_origins;
+    const char *eq = std::getenv("MIPX_EMBED_Q16");  // A/B: 0 keeps the 5-dword loads
+    a.q16 = aligned4(in) && a.in_img % 4 == 0 && !(eq && *eq == '0');
     if (b == 4 && !(aligned4(in) && aligned4(out))) return MIPX_EINVAL;
     if (aligned4(in) && (a.in_img % 4) == 0 && a.in_img < 0x7fffffffLL && oh <= 65535) {
         const dim3 grid((ow * b + 4095) / 4096, oh, n);
