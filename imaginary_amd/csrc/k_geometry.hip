@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8
 // per tile (= contiguous output pixels per output row of the tile).
 template <int B, bool CW, int TH>
 __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
-                                                   long long img_bytes_, int tiles_x, int tiles_y, int xcd) {
+                                                   long long img_bytes_, int tiles_x, int tiles_y, int xcd, int q16) {
     constexpr int T = 64;
     constexpr int RS = (T * B + 3) / 4 + 1;  // dwords per staged row (+1: the unaligned pixel read spills)
     __shared__ uint32_t tile[TH * RS];
@@ -263,7 +263,38 @@ __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8
     const u8 *src = in + img * img_bytes_;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, img_bytes_, &delta);
     const int nd = (tw * B + 3) >> 2;
-    {
+    if (q16) {  // r02: 16 bytes of a row per item (one b128 + one b32 load, 4 alignbytes)
+        const int nq = (nd + 3) >> 2;
+        constexpr int kPer = (TH * (((T * B + 3) / 4 + 3) / 4) + 255) / 256;
+        uint32_t v[kPer][4];
+        int slot[kPer], cnt[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            slot[k] = -1;
+            cnt[k] = 0;
+            if (i < th * nq) {
+                const int r = i / nq, q = i - r * nq;
+                const int abs0 = delta + ((ty0 + r) * w + tx0) * B;
+                const int o = (abs0 & ~3) + 16 * q;
+                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                const u4v p = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+                const uint32_t e = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 16, 0, 0));
+                const int sh = abs0 & 3;
+                v[k][0] = __builtin_amdgcn_alignbyte(p[1], p[0], sh);
+                v[k][1] = __builtin_amdgcn_alignbyte(p[2], p[1], sh);
+                v[k][2] = __builtin_amdgcn_alignbyte(p[3], p[2], sh);
+                v[k][3] = __builtin_amdgcn_alignbyte(e, p[3], sh);
+                slot[k] = r * RS + 4 * q;
+                cnt[k] = min(4, nd - 4 * q);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (j < cnt[k]) tile[slot[k] + j] = v[k][j];
+    } else {
         constexpr int kPer = (TH * ((T * B + 3) / 4) + 255) / 256;
         uint32_t v[kPer];
         int slot[kPer];
@@ -503,9 +534,11 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
         // A/B (profiles/r01/v18/rotxcd_ab.jsonl): contiguous runs win 3-8% on 4K RGB, where a
         // 64-pixel tile row (192 B) splits a 128-byte line, and lose 2% on RGBA (whole lines)
         const int xcd = ex && *ex ? (*ex != '0') : ((64 * b) % 128 != 0);
+        const char *eq = std::getenv("MIPX_ROT_Q16");  // A/B: 0 keeps the b64-per-dword staging
+        const int q16 = !(eq && *eq == '0');
 #define MIPX_ROT(CW_, TH_)                                                                                     \
     MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, CW_, TH_>), grid, dim3(256), 0, st, in, out, w, h, ib, \
-                                              tx, ty, xcd))
+                                              tx, ty, xcd, q16))
         if (th == 128) {
             if (angle == 90) { MIPX_ROT(true, 128); } else { MIPX_ROT(false, 128); }
         } else {
