@@ -32,6 +32,7 @@ struct RemapArgs {
     long long in_img, out_img;
     const int *origins;  // extract with per-image (left, top) from the device (smartcrop)
     int q16;             // k_embed_rows: 16-byte source loads where the row offset is dword aligned
+    int rpb;             // k_embed_rows: output rows per block
 };
 
 __device__ __forceinline__ uint32_t load_px(const u8 *p, int B) {
@@ -118,12 +119,10 @@ __device__ __forceinline__ int extend_index(int v, int n, int ext) {  // -1 = fi
 }
 
 template <int B>
-__global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
-    const int Y = blockIdx.y;
-    const int img = blockIdx.z;
+// fw: the fill bytes packed (byte c = fill[c]), so no per-lane index into the argument
+// struct forces it into scratch memory
+__device__ __forceinline__ void embed_chunk(const RemapArgs &a, uint32_t fw, int img, int Y, int j0) {
     const int row_out = a.ow * B;
-    const int j0 = (blockIdx.x * 256 + threadIdx.x) * 16;
-    if (j0 >= row_out) return;
     int ox = a.x, oy = a.y;
     if (a.origins) {
         ox = -a.origins[2 * img];
@@ -139,7 +138,7 @@ __global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
         for (int d = 0; d < 4; ++d) {
             uint32_t w = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) w |= static_cast<uint32_t>(a.fill[(j0 + 4 * d + k) % B]) << (8 * k);
+            for (int k = 0; k < 4; ++k) w |= ((fw >> (8 * ((j0 + 4 * d + k) % B))) & 0xffu) << (8 * k);
             v[d] = w;
         }
     } else if (j0 / B - ox >= 0 && (j0 + 15) / B - ox < a.w) {  // interior: shifted row copy
@@ -165,7 +164,7 @@ __global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
                 const int jb = j0 + 4 * d + k;
                 const int px = jb / B, c = jb - px * B;
                 const int sx = extend_index(px - ox, a.w, a.extend);
-                const uint32_t byte = sx < 0 ? a.fill[c] : src[rowb + static_cast<long long>(sx) * B + c];
+                const uint32_t byte = sx < 0 ? (fw >> (8 * c)) & 0xffu : src[rowb + static_cast<long long>(sx) * B + c];
                 w |= byte << (8 * k);
             }
             v[d] = w;
@@ -180,6 +179,18 @@ __global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
     } else {
         for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
     }
+}
+
+// a block: 4 KiB of a.rpb consecutive output rows (r02: 4 rows per block, so a
+// border-fill row is not one 16-byte store per lane and wave; MIPX_EMBED_RPB=1 A/B)
+template <int B>
+__global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
+    const int img = blockIdx.z;
+    const int j0 = (blockIdx.x * 256 + threadIdx.x) * 16;
+    if (j0 >= a.ow * B) return;
+    const uint32_t fw = a.fill[0] | (a.fill[1] << 8) | (a.fill[2] << 16) | (static_cast<uint32_t>(a.fill[3]) << 24);
+    const int y0 = blockIdx.y * a.rpb, y1 = min(y0 + a.rpb, a.oh);
+    for (int Y = y0; Y < y1; ++Y) embed_chunk<B>(a, fw, img, Y, j0);
 }
 
 // flip H / flip V / rot 180 as row remaps: output row Y = source row sy
@@ -475,7 +486,9 @@ int embed_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x, int y
     a.q16 = aligned4(in) && a.in_img % 4 == 0 && !(eq && *eq == '0');
     if (b == 4 && !(aligned4(in) && aligned4(out))) return MIPX_EINVAL;
     if (aligned4(in) && (a.in_img % 4) == 0 && a.in_img < 0x7fffffffLL && oh <= 65535) {
-        const dim3 grid((ow * b + 4095) / 4096, oh, n);
+        const char *er = std::getenv("MIPX_EMBED_RPB");
+        a.rpb = (er && *er) ? std::max(1, std::atoi(er)) : 4;
+        const dim3 grid((ow * b + 4095) / 4096, (oh + a.rpb - 1) / a.rpb, n);
         MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_embed_rows<B_>, grid, dim3(256), 0, st, a));
         return launch_check("k_embed_rows");
     }
