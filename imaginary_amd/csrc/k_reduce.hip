@@ -51,16 +51,18 @@ using namespace dev;
 constexpr int kR = 12;           // output rows per LDS chunk (2 ring periods)
 // WIDE level (variant bits 6 / 7): 128 << WIDE threads and strips 2x / 4x as
 // wide (less relative halo, longer contiguous row segments, fewer workgroups)
-template <int WIDE>
+// TIGHT (variant bit 8, WIDE 1 only): rows 264 dwords apart (== 8 mod 64) instead of 288,
+// 25.3 instead of 27.6 KB of LDS, so 6 workgroups share a CU instead of 5 (r02 A/B)
+template <int WIDE, int TIGHT = 0>
 struct R2T {
     static constexpr int kThreads = 128 << WIDE;
-    static constexpr int kPitch = WIDE == 2 ? 544 : WIDE == 1 ? 288 : 160;  // LDS dwords per row (== 32 mod 64)
+    static constexpr int kPitch = WIDE == 2 ? 544 : WIDE == 1 ? (TIGHT ? 264 : 288) : 160;  // LDS dwords per row
 };
 
-template <int B, int WIDE = 0>
+template <int B, int WIDE = 0, int TIGHT = 0>
 struct R2 {
-    static constexpr int kThreads = R2T<WIDE>::kThreads;
-    static constexpr int kPitch = R2T<WIDE>::kPitch;
+    static constexpr int kThreads = R2T<WIDE, TIGHT>::kThreads;
+    static constexpr int kPitch = R2T<WIDE, TIGHT>::kPitch;
     static constexpr int TW = B == 3 ? 80 << WIDE : WIDE == 0 ? 56 : 60 << WIDE;  // output pixels per strip
     static constexpr int NPX = 2 * TW + 9;           // intermediate px 2x0-5 .. 2x0+2TW+3
     static constexpr int K = B == 3 ? 4 : 2;         // output pixels per horizontal item
@@ -125,10 +127,10 @@ __device__ __forceinline__ uint32_t pack4b(float a, float b, float c, float d) {
     return __builtin_amdgcn_cvt_pk_u8_f32(d, 3, v);
 }
 
-template <int B, int R, bool PF, bool PK, bool MEM, int LAUX, bool NTS, int WIDE>
+template <int B, int R, bool PF, bool PK, bool MEM, int LAUX, bool NTS, int WIDE, int TIGHT>
 __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int strip, int band,
                                              uint32_t *lds) {
-    using G = R2<B, WIDE>;
+    using G = R2<B, WIDE, TIGHT>;
     constexpr int kThreads = G::kThreads, kPitch = G::kPitch;
     constexpr int TW = G::TW, K = G::K;
     const int tid = threadIdx.x;
@@ -341,7 +343,8 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 template <int B, int VAR>
 __global__ void __launch_bounds__(R2T<(VAR & 128) ? 2 : (VAR & 64) ? 1 : 0>::kThreads) k_reduce2x2(Reduce2Args a) {
     constexpr int WIDE = (VAR & 128) ? 2 : (VAR & 64) ? 1 : 0;
-    constexpr int kPitch = R2T<WIDE>::kPitch;
+    constexpr int TIGHT = (VAR & 256) ? 1 : 0;
+    constexpr int kPitch = R2T<WIDE, TIGHT>::kPitch;
     constexpr int R = (VAR & 1) ? 6 : 12;
     constexpr bool PF = (VAR & 2) != 0;
     constexpr bool PK = (VAR & 4) != 0;
@@ -362,7 +365,7 @@ __global__ void __launch_bounds__(R2T<(VAR & 128) ? 2 : (VAR & 64) ? 1 : 0>::kTh
         band = rest % a.n_bands;
         img = rest / a.n_bands;
     }
-    reduce2_tile<B, R, PF, PK, MEM, LAUX, NTS, WIDE>(a, img, strip, band, lds);
+    reduce2_tile<B, R, PF, PK, MEM, LAUX, NTS, WIDE, TIGHT>(a, img, strip, band, lds);
 }
 
 
@@ -501,7 +504,7 @@ int reduce2_variant() {
     if (!e || !*e) return kR2Default;
     const int v = std::atoi(e);
     switch (v) {
-        case 0: case 1: case 2: case 3: case 6: case 10: case 66: case 67: case 130: case 131: return v;
+        case 0: case 1: case 2: case 3: case 6: case 10: case 66: case 67: case 130: case 131: case 322: case 323: return v;
         default: return kR2Default;
     }
 }
@@ -564,6 +567,7 @@ int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int
     }
     switch (var) {
         MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3) MIPX_R2(6) MIPX_R2(10) MIPX_R2(66) MIPX_R2(67) MIPX_R2(130) MIPX_R2(131)
+        MIPX_R2(322) MIPX_R2(323)
         default: return MIPX_EINVAL;
     }
 #undef MIPX_R2
