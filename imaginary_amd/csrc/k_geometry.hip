@@ -199,10 +199,12 @@ __global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
 // then each lane gathers its 16 output bytes from LDS and stores them at once.
 template <int B, bool MIRROR>
 __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
-                                                   int vflip, long long img_bytes_) {
+                                                   int vflip, long long img_bytes_, int rpb) {
     __shared__ __attribute__((aligned(16))) uint32_t seg[1024 + 8];
-    const int Y = blockIdx.y;
     const int img = blockIdx.z;
+    // rpb output rows per block (r02: 4, like k_embed_rows; MIPX_FLIP_RPB=1 is the r01 grid)
+    for (int Y = blockIdx.y * rpb; Y < min((blockIdx.y + 1) * rpb, h); ++Y) {
+    if (Y != blockIdx.y * rpb) __syncthreads();  // the previous row's gather is done with seg
     const int row_bytes = w * B;
     const int j0 = blockIdx.x * 4096;              // output byte range [j0, j1) of the row
     const int j1 = min(j0 + 4096, row_bytes);
@@ -230,7 +232,7 @@ __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8
     __syncthreads();
     const u8 *sb = reinterpret_cast<const u8 *>(seg) + skew;
     const int jl = j0 + threadIdx.x * 16;
-    if (jl >= j1) return;
+    if (jl >= j1) continue;
     const int nb = min(16, j1 - jl);
     uint32_t v[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -247,6 +249,7 @@ __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8
         *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
     } else {
         for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
+    }
     }
 }
 
@@ -499,13 +502,15 @@ int flip_rows_launch(const u8 *in, u8 *out, int n, int w, int h, int b, bool mir
     if (h > 65535) return MIPX_EUNSUPPORTED;
     const long long ib = img_bytes(w, h, b);
     if (ib >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
-    const dim3 grid((w * b + 4095) / 4096, h, n);
+    const char *er = std::getenv("MIPX_FLIP_RPB");
+    const int rpb = (er && *er) ? std::max(1, std::atoi(er)) : 4;
+    const dim3 grid((w * b + 4095) / 4096, (h + rpb - 1) / rpb, n);
     if (mirror) {
         MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_flip_rows<B_, true>), grid, dim3(256), 0, st, in, out, w, h,
-                                                  vflip ? 1 : 0, ib));
+                                                  vflip ? 1 : 0, ib, rpb));
     } else {
         MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_flip_rows<B_, false>), grid, dim3(256), 0, st, in, out, w, h,
-                                                  vflip ? 1 : 0, ib));
+                                                  vflip ? 1 : 0, ib, rpb));
     }
     return launch_check("k_flip_rows");
 }

@@ -1519,7 +1519,10 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
                     int vo = B * org + 4 * (c * 64 + lane);
                     const int over = r * pitch + vo + 4 - static_cast<int>(a.in_img);
                     if (over > 0 && over < 4) vo -= over;
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4, vo, r * pitch, 0, 0);
+                    // the row offset rides in the VGPR offset: the buffer range check covers the
+                    // VGPR offset only (not the SGPR one), so bytes past the image read 0 instead
+                    // of the next image (or past the allocation), and a shifted dword stays >= 0
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4, r * pitch + vo, 0, 0, 0);
                 }
         }
     }
@@ -1821,7 +1824,7 @@ __global__ void __launch_bounds__(256) k_rmf4(RmArgs a) {
             for (int c = 0; c < chunks; ++c)
                 if (c * 64 + lane < RS)  // the last chunk stops at the row stride
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
-                                                             B * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
+                                                             r * pitch + B * org + 4 * (c * 64 + lane), 0, 0, 0);
         }
     }
     const int n = lane & 15, kg = lane >> 4;

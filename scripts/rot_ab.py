@@ -25,7 +25,7 @@ def main():
     for (w, h, b, n) in SHAPES:
         x = torch.randint(0, 256, (n * w * h * b,), dtype=torch.uint8, device=dev)
         y = torch.empty((n * w * h * b,), dtype=torch.uint8, device=dev)
-        for ang in (90, 270):
+        for ang in [int(v) for v in os.environ.get("ANGLES", "90,270").split(",")]:
             outs = {}
             for rep in range(2):
                 for v in variants:

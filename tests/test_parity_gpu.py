@@ -465,6 +465,19 @@ def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"rmfma={on} window gravity {g} bands {b}")
 
 
+@pytest.mark.parametrize("w", [1, 2, 5, 7, 13])
+def test_reduce_narrow_unaligned_rows(gpu, oracle, rng, w):
+    """k_rmf2 on images a few pixels wide with rows that are not a multiple of 4 bytes
+    (found by the 200-seed whole-plan fuzz, seed 75: a 1 x 23 RGB reduce).  A staged
+    row then spans several image rows and the last image row's dwords end past the
+    image; the row offset must ride in the range-checked VGPR offset."""
+    for h, s in ((23, 1.3529411764705883), (17, 1.6), (40, 2.4), (9, 1.25)):
+        imgs = np.stack([rand_img(rng, h, w, 3), smooth_img(rng, h, w, 3), rand_img(rng, h, w, 3)])
+        got = gpu.run_op("reduce", imgs, hshrink=s, vshrink=s)
+        for i in range(3):
+            assert_same(got[i], oracle.reduce(imgs[i], s, s), f"reduce {h}x{w}x3 /{s} img{i}")
+
+
 @pytest.mark.parametrize("rows", ["1", "8", "13"])
 def test_reduce2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows):
     """Fused generic reduce (k_reduce2d, an A/B variant behind MIPX_REDUCE2D=1:
