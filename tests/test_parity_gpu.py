@@ -472,6 +472,8 @@ def test_reduce_narrow_unaligned_rows(gpu, oracle, rng, w):
     row then spans several image rows and the last image row's dwords end past the
     image; the row offset must ride in the range-checked VGPR offset."""
     for h, s in ((23, 1.3529411764705883), (17, 1.6), (40, 2.4), (9, 1.25)):
+        if int(w / s + 0.5) < 1:  # libvips' reduce would make an empty image (EINVAL)
+            continue
         imgs = np.stack([rand_img(rng, h, w, 3), smooth_img(rng, h, w, 3), rand_img(rng, h, w, 3)])
         got = gpu.run_op("reduce", imgs, hshrink=s, vshrink=s)
         for i in range(3):
