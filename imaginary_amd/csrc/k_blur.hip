@@ -368,8 +368,9 @@ __global__ void __launch_bounds__(256) k_bmf(BmArgs a) {
             for (int c = 0; c < chunks; ++c)
                 if (c * 64 + lane < a.rsd)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, bm_lds(raw + l * a.rsd + c * 64), 4,
-                                                             static_cast<int>(a.in_base) + B * sx + 4 * (c * 64 + lane),
-                                                             r * a.in_pitch, 0, 0);
+                                                             static_cast<int>(a.in_base + static_cast<long long>(r) * a.in_pitch) +
+                                                                 B * sx + 4 * (c * 64 + lane),
+                                                             0, 0, 0);
         }
     }
     __syncthreads();

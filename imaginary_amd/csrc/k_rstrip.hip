@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(kRsThreads) k_rstrip(RsArgs a) {
         for (int i = 0; i < kRsPF; ++i) {
             const int p = min(p0 + wave + 4 * i, p1 - 1);  // past the end: a duplicate row, never committed
             const int a4 = static_cast<int>(row_off(p) & ~3LL);
-            pf[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * lane, a4, 0));
+            pf[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, a4 + 16 * lane, 0, 0));
         }
     };
     auto commit = [&](int p0, int p1) {

@@ -143,15 +143,17 @@ __device__ __forceinline__ void vstage_rows(const VPassArgs &a, uint32_t *rows, 
         for (int l = wave; l < L; l += 4) {
             const int r = clampi(r_lo + l, 0, a.hl - 1);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride), 16,
-                                                     static_cast<int>(col0) + lane * 16, r * a.in_pitch, 0, 0);
+                                                     static_cast<int>(col0 + static_cast<long long>(r) * a.in_pitch) + lane * 16,
+                                                     0, 0, 0);
         }
     } else if (DMA == 4) {
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
         for (int l = 0; l < L; ++l) {
             const int r = clampi(r_lo + l, 0, a.hl - 1);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + wave * 64), 4,
-                                                     static_cast<int>(col0) + wave * 256 + lane * 4,
-                                                     r * a.in_pitch, 0, 0);
+                                                     static_cast<int>(col0 + static_cast<long long>(r) * a.in_pitch) +
+                                                         wave * 256 + lane * 4,
+                                                     0, 0, 0);
         }
     } else {
         const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, delta);
@@ -159,9 +161,9 @@ __device__ __forceinline__ void vstage_rows(const VPassArgs &a, uint32_t *rows, 
             const int r = clampi(r_lo + l, 0, a.hl - 1);
             const int a4 = static_cast<int>(*delta + col0 + static_cast<long long>(r) * a.in_pitch) & ~3;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + wave * 64), 4,
-                                                     wave * 256 + lane * 4, a4, 0, 0);
+                                                     a4 + wave * 256 + lane * 4, 0, 0, 0);
             if (wave == 0 && lane == 0)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + 256), 4, 1024, a4, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(rows + l * kVStride + 256), 4, a4 + 1024, 0, 0, 0);
         }
     }
 }
@@ -618,7 +620,7 @@ __device__ __forceinline__ void hstage_issue(const HPassArgs &a, uint32_t *spx, 
         for_chunks(chunks, [&](int rr, int q) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs, to_lds(spx + rr * a.span_max + (cl4 - org) + q * 256), 16,
-                static_cast<int>(row0) + 4 * cl4 + 16 * (q * 64 + lane), rr * a.in_pitch, 0, 0);
+                static_cast<int>(row0 + static_cast<long long>(rr) * a.in_pitch) + 4 * cl4 + 16 * (q * 64 + lane), 0, 0, 0);
         });
     } else if (DW == 4) {  // B = 4, rows dword aligned
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(img_base, a.in_img);
@@ -626,7 +628,7 @@ __device__ __forceinline__ void hstage_issue(const HPassArgs &a, uint32_t *spx, 
         for_chunks(chunks, [&](int rr, int q) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(
                 rs, to_lds(spx + rr * a.span_max + (cl - org) + q * 64), 4,
-                static_cast<int>(row0) + 4 * (cl + q * 64 + lane), rr * a.in_pitch, 0, 0);
+                static_cast<int>(row0 + static_cast<long long>(rr) * a.in_pitch) + 4 * (cl + q * 64 + lane), 0, 0, 0);
         });
     } else {  // any alignment: each row's raw bytes from its dword-aligned-down start
         const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(img_base, a.in_img, &delta);
@@ -635,7 +637,7 @@ __device__ __forceinline__ void hstage_issue(const HPassArgs &a, uint32_t *spx, 
         for_chunks(chunks, [&](int rr, int q) {
             const int a4 = static_cast<int>(delta + row0 + static_cast<long long>(rr) * a.in_pitch + B * cl) & ~3;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + rr * a.raw_max + q * 64), 4,
-                                                     4 * (q * 64 + lane), a4, 0, 0);
+                                                     a4 + 4 * (q * 64 + lane), 0, 0, 0);
         });
     }
     g = HStage{x0, x_last, lo, hi, span, y_first, nr, cl, ch, org, delta, row0};
