@@ -77,7 +77,11 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
     return base + (b >> 3);
 }
 
-// Buffer descriptor over one image: out-of-range offsets read 0 (T8/T20).
+// Buffer descriptor over one image: out-of-range offsets read 0 (T8/T20).  The range
+// check covers the VGPR offset (+ the instruction offset) only, NOT the SGPR offset, so
+// any offset that can run past the image must ride in the VGPR operand (r02: a row
+// address in the SGPR offset let a 1 x 23 RGB reduce read a shifted dword as 0 and let
+// staging loads read past the last image of a batch).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc(const u8 *p, long long bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<u8 *>(p), 0, static_cast<int>(bytes), 0x00020000);
 }
