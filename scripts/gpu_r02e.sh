@@ -1,4 +1,4 @@
-set -u; cd $GRAFT_REPO_ROOT; O=gpurun_out/r02f; mkdir -p $O; export TMPDIR=/tmp
+set -u; cd $GRAFT_REPO_ROOT; O=gpurun_out/r02g; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
