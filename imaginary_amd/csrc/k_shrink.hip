@@ -358,6 +358,86 @@ __global__ void __launch_bounds__(256) k_shrink_q(ShrinkArgs a) {
     }
 }
 
+// Larger factors (5 <= S <= 12, both axes equal, rows of any alignment): one output pixel per
+// lane from its S x S box in registers, no LDS.  Each of the S rows is 3 x 16-byte loads from
+// the box's dword-aligned-down start, realigned with v_alignbyte and summed as packed u16
+// pairs; then the S column means of each channel are averaged (shrinkv, then shrinkh, each
+// (sum + S/2) / S).  A wave streams 64 S B contiguous bytes of each row.
+#ifndef MIPX_P1_UNROLL
+#define MIPX_P1_UNROLL 4
+#endif
+template <int B, int S>
+__global__ void __launch_bounds__(256) k_shrink_p1(ShrinkArgs a) {
+    constexpr int NB = S * B;             // box bytes per row
+    constexpr int ND = (NB + 3) / 4;      // realigned dwords
+    constexpr int NL = (NB + 3 + 15) / 16;  // 16-byte loads per row (<= 3)
+    static_assert(NL <= 3, "box too wide");
+    const unsigned gq = blockIdx.x * 256u + threadIdx.x;  // pixel within this image's window
+    const unsigned cols = static_cast<unsigned>(a.x_end - a.xb0);
+    if (gq >= cols * static_cast<unsigned>(a.y_end - a.y_base)) return;
+    const int img = blockIdx.y;
+    const unsigned yr = gq / cols;
+    const int y = a.y_base + static_cast<int>(yr);
+    const int x = a.xb0 + static_cast<int>(gq - yr * cols);
+    const int row_bytes = a.w * B;
+    uint8_t o[B];
+    if (S * (x + 1) <= a.w) {
+        int delta = 0;
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &delta);
+        uint32_t lo[ND], hi[ND];
+#pragma unroll
+        for (int i = 0; i < ND; ++i) lo[i] = hi[i] = 0u;
+#pragma unroll MIPX_P1_UNROLL
+        for (int k = 0; k < S; ++k) {
+            const int off = delta + min(S * y + k, a.h - 1) * row_bytes + S * x * B;
+            const int a4 = off & ~3, sh = off & 3;
+            uint32_t t[4 * NL + 1];
+#pragma unroll
+            for (int j = 0; j < NL; ++j) {
+                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                const u4v v = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, a4 + 16 * j, 0, 0));
+                t[4 * j] = v[0], t[4 * j + 1] = v[1], t[4 * j + 2] = v[2], t[4 * j + 3] = v[3];
+            }
+            t[4 * NL] = 0u;
+#pragma unroll
+            for (int i = 0; i < ND; ++i) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(t[i + 1], t[i], sh);
+                lo[i] += w & 0x00ff00ffu;
+                hi[i] += (w >> 8) & 0x00ff00ffu;
+            }
+        }
+        uint32_t sum[B];
+#pragma unroll
+        for (int c = 0; c < B; ++c) sum[c] = 0u;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+            const uint32_t m[4] = {((lo[i] & 0xffffu) + S / 2) / S, ((hi[i] & 0xffffu) + S / 2) / S,
+                                   ((lo[i] >> 16) + S / 2) / S, ((hi[i] >> 16) + S / 2) / S};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * i + j < NB) sum[(4 * i + j) % B] += m[j];
+        }
+#pragma unroll
+        for (int c = 0; c < B; ++c) o[c] = static_cast<uint8_t>((sum[c] + S / 2) / S);
+    } else {  // the box reaches past the row end: COPY border, byte by byte
+        const u8 *src = a.in + img * a.in_img;
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            uint32_t sum = 0;
+            for (int k = 0; k < S; ++k) {
+                const int xi = min(S * x + k, a.w - 1);
+                uint32_t vs = 0;
+                for (int r = 0; r < S; ++r) vs += src[static_cast<size_t>(min(S * y + r, a.h - 1)) * row_bytes + xi * B + c];
+                sum += (vs + S / 2) / S;
+            }
+            o[c] = static_cast<uint8_t>((sum + S / 2) / S);
+        }
+    }
+    u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
+#pragma unroll
+    for (int c = 0; c < B; ++c) q[c] = o[c];
+}
+
 }  // namespace
 
 int shrink_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int hs, int vs, hipStream_t st) {
@@ -415,6 +495,32 @@ int shrink_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int 
         if (hs == 2) { MIPX_SQ(2) } else if (hs == 3) { MIPX_SQ(3) } else { MIPX_SQ(4) }
 #undef MIPX_SQ
         return launch_check("k_shrink_q");
+    }
+    // equal factors 5-12 (RGBA 5-10): one output pixel per lane from registers, 1.03-1.25x
+    // k_shrink_x4 (profiles/r02/shrink_p1_ab.jsonl); MIPX_SHRINK_P1=0: off, =1: RGBA / 11 too
+    const char *ep = std::getenv("MIPX_SHRINK_P1");
+    const int p1_rgba_max = (ep && *ep == '1') ? 11 : 10;
+    if (!(ep && *ep == '0') && hs == vs && hs >= 5 && hs <= 12 && (b == 3 || (b == 4 && hs <= p1_rgba_max)) &&
+        n <= 65535) {
+        ShrinkArgs q = a;
+        q.xb0 = x0;  // in pixels here
+        const long long px = static_cast<long long>(x1 - x0) * (y1 - y0);  // per image (< 2^31: in_img is)
+        const dim3 g(static_cast<unsigned>((px + 255) / 256), static_cast<unsigned>(n));
+#define MIPX_SP(S_)                                                                                   \
+    if (b == 3) hipLaunchKernelGGL((k_shrink_p1<3, S_>), g, dim3(256), 0, st, q);                     \
+    else hipLaunchKernelGGL((k_shrink_p1<4, (S_ > 11 ? 11 : S_)>), g, dim3(256), 0, st, q);
+        switch (hs) {
+            case 5: MIPX_SP(5) break;
+            case 6: MIPX_SP(6) break;
+            case 7: MIPX_SP(7) break;
+            case 8: MIPX_SP(8) break;
+            case 9: MIPX_SP(9) break;
+            case 10: MIPX_SP(10) break;
+            case 11: MIPX_SP(11) break;
+            default: MIPX_SP(12) break;
+        }
+#undef MIPX_SP
+        return launch_check("k_shrink_p1");
     }
     const char *ex = std::getenv("MIPX_SHRINK_X4");  // A/B: 0 selects the dword kernel
     const bool x4 = (w * b) % 4 == 0 && a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0 &&

@@ -18,6 +18,8 @@ SHAPES = [  # w, h, b, n, s
     (4000, 3000, 3, 32, 3), (1920, 1080, 3, 64, 4), (3840, 2160, 3, 32, 4), (4000, 3000, 3, 32, 4),
     (2048, 2048, 4, 32, 2), (2048, 2048, 4, 32, 3),
 ]
+if os.environ.get("SHRINK_SHAPES"):  # e.g. "4000x3000x3x32x8;..."
+    SHAPES = [tuple(int(v) for v in t.split("x")) for t in os.environ["SHRINK_SHAPES"].split(";")]
 
 
 def vr(v):

@@ -246,6 +246,24 @@ def test_shrink_quad_kernel(gpu, oracle, rng, monkeypatch, q, s):
             assert_same(got[i], oracle.shrink(imgs[i], s, s), f"shrink q={q} {h}x{w}x{b} /{s}")
 
 
+@pytest.mark.parametrize("p1", ["1", "0"])
+@pytest.mark.parametrize("s", [5, 6, 7, 8, 9, 10, 11, 12])
+def test_shrink_p1_kernel(gpu, oracle, rng, monkeypatch, s, p1):
+    """Equal factors 5-12 on the one-pixel-per-lane register kernel (MIPX_SHRINK_P1=1,
+    RGBA up to 11) and on k_shrink_x4 / k_shrink_lds (=0): rows of any byte alignment,
+    widths ending inside a box (COPY border), heights past the last whole box, RGB and
+    RGBA, batches of 2."""
+    monkeypatch.setenv("MIPX_SHRINK_P1", p1)
+    for h, w, b in ((64, 400, 3), (37, 1001, 3), (s, s, 3), (2 * s + 1, 13 * s - 1, 3), (70, 333, 4),
+                    (41, 52, 4), (s + 3, 5 * s + 2, 4), (17, 1277, 3)):
+        if b == 4 and s > 11:
+            continue
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("shrink", imgs, hshrink=s, vshrink=s)
+        for i in range(2):
+            assert_same(got[i], oracle.shrink(imgs[i], s, s), f"shrink p1 {h}x{w}x{b} /{s}")
+
+
 # ---------------------------------------------------------------- gaussian blur
 @pytest.mark.parametrize("sigma", [0.8, 1.0, 3.0, 5.0, 12.5])
 @pytest.mark.parametrize("b", [1, 3, 4])
