@@ -256,14 +256,12 @@ template <int B, int S>
 __global__ void __launch_bounds__(256) k_shrink_q(ShrinkArgs a) {
     constexpr int N = S * B;  // input dwords per lane and row: 4 S pixels
     const int nq = (a.x_end - 4 * a.xb0 + 3) >> 2;  // quads per computed output row (xb0 in quads here)
-    const long long gq = static_cast<long long>(blockIdx.x) * 256 + threadIdx.x;
-    const int rows = a.y_end - a.y_base;
-    const long long per_img = static_cast<long long>(nq) * rows;
-    if (gq >= per_img * a.ry) return;  // a.ry = images
-    const int img = static_cast<int>(gq / per_img);
-    const int rem = static_cast<int>(gq - img * per_img);
-    const int y = a.y_base + rem / nq;
-    const int xq = a.xb0 + rem - (rem / nq) * nq;
+    const unsigned gq = blockIdx.x * 256u + threadIdx.x;  // quad within this image's window
+    if (gq >= static_cast<unsigned>(nq) * static_cast<unsigned>(a.y_end - a.y_base)) return;
+    const int img = blockIdx.y;
+    const unsigned yr = gq / static_cast<unsigned>(nq);
+    const int y = a.y_base + static_cast<int>(yr);
+    const int xq = a.xb0 + static_cast<int>(gq - yr * nq);
     const int x = 4 * xq;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
     const int row_bytes = a.w * B;
@@ -276,7 +274,7 @@ __global__ void __launch_bounds__(256) k_shrink_q(ShrinkArgs a) {
 #pragma unroll
         for (int k = 0; k < S; ++k) {
             uint32_t w[N];
-            load_row_words<B, S>(rs, S * x * B, min(S * y + k, a.h - 1) * row_bytes, w);
+            load_row_words<B, S>(rs, S * x * B + min(S * y + k, a.h - 1) * row_bytes, 0, w);
 #pragma unroll
             for (int i = 0; i < N; ++i) {
                 lo[i] += w[i] & 0x00ff00ffu;
@@ -480,15 +478,12 @@ int shrink_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int 
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     // S <= 4 on both axes, dword-aligned rows: the register-only quad kernel (MIPX_SHRINK_Q=0: off)
     const char *eq = std::getenv("MIPX_SHRINK_Q");
-    if (!(eq && *eq == '0') && hs == vs && hs >= 2 && hs <= 4 && (b == 3 || b == 4) && (w * b) % 4 == 0 &&
+    if (!(eq && *eq == '0') && hs == vs && hs >= 2 && hs <= 4 && (b == 3 || b == 4) && (w * b) % 4 == 0 && n <= 65535 &&
         a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0) {
         ShrinkArgs q = a;
         q.xb0 = x0 / 4;  // in quads
-        q.ry = n;        // images
-        const long long quads = static_cast<long long>((x1 - 4 * q.xb0 + 3) / 4) * (y1 - y0) * n;
-        const long long qblocks = (quads + 255) / 256;
-        if (!grid_ok(qblocks)) return MIPX_EINVAL;
-        const dim3 g(static_cast<unsigned>(qblocks));
+        const long long quads = static_cast<long long>((x1 - 4 * q.xb0 + 3) / 4) * (y1 - y0);  // per image
+        const dim3 g(static_cast<unsigned>((quads + 255) / 256), static_cast<unsigned>(n));  // image = blockIdx.y
 #define MIPX_SQ(S_)                                                                                   \
     if (b == 3) hipLaunchKernelGGL((k_shrink_q<3, S_>), g, dim3(256), 0, st, q);                      \
     else hipLaunchKernelGGL((k_shrink_q<4, S_>), g, dim3(256), 0, st, q);
