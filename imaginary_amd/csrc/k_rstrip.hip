@@ -136,7 +136,10 @@ __global__ void __launch_bounds__(kRsThreads) k_rstrip(RsArgs a) {
     };
 
     int delta = 0;
-    const __amdgpu_buffer_rsrc_t rsrc = image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &delta);
+    // img is block-uniform, but the compiler's divergence analysis lost that and wrapped every
+    // staging load in a readfirstlane waterfall loop over the descriptor; say so explicitly
+    const __amdgpu_buffer_rsrc_t rsrc =
+        image_rsrc_aligned(a.in + static_cast<long long>(__builtin_amdgcn_readfirstlane(img)) * a.in_img, a.in_img, &delta);
     // ---- row staging: wave w fetches rows p0 + w, p0 + w + 4, ... (lane: 16 bytes) ----
     uint4 pf[kRsPF];
     auto row_off = [&](int p) {
