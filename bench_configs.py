@@ -152,12 +152,22 @@ def c5_requests(count, seed=5):
     return workloads.c5_requests(count, seed, ia.fit_dimension)
 
 
+def c5_request_bytes(wh, opts):
+    """Input + output bytes of one C5 request (the planner's output geometry)."""
+    w, h = wh
+    p = plan_for(opts, w, h, 3)
+    return w * h * 3 + p.out_w * p.out_h * p.out_bands
+
+
 def c5(args, dev, sp, stream):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    reqs = c5_requests(args.c5_requests)[rank::world]  # shard requests across ranks
+    allreq = c5_requests(args.c5_requests)
+    # byte-balanced shards, each plan group on as few ranks as possible (SURVEY §8(e))
+    shard = workloads.shard_groups(workloads.c5_groups(allreq), world, c5_request_bytes)[rank]
+    reqs = [None] * sum(cnt for _, _, cnt in shard)
     groups = []
-    for (w, h), opts, cnt in workloads.c5_groups(reqs):
+    for (w, h), opts, cnt in shard:
         groups.append((Group(plan_for(opts, w, h, 3), cnt, dev, 5 + len(groups)), opts))
 
     def run_all():

@@ -114,6 +114,7 @@ _SIG = {
     "mipx_build_id": (C.c_char_p, []),
     "mipx_cancel": (C.c_int, [C.c_uint64]),
     "mipx_queue_count": (C.c_int, []),
+    "mipx_pick_queue": (C.c_int, [C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_int32]),
     "mipx_queue_stats": (C.c_int, [C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                    C.POINTER(C.c_int64)]),
     "mipx_abi_version": (C.c_int, []),
@@ -148,6 +149,7 @@ _SIG = {
     "mipx_op_colourspace_bw": (C.c_int, [_U8P, _U8P, _I, _I, _I, _I, _P]),
     "mipx_op_smartcrop_origin": (C.c_int, [_U8P, _P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _P]),
     "mipx_op_workspace_bytes": (C.c_size_t, [_I, _I, _I, _I, _I, C.c_double, C.c_double]),
+    "mipx_tuning_reload": (C.c_int, []),
     "mipx_set_device": (C.c_int, [C.c_int]),
     "mipx_dev_malloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
     "mipx_dev_free": (C.c_int, [_P]),
@@ -189,6 +191,20 @@ class MipxError(RuntimeError):
         if detail:
             msg += f" — {detail}"
         super().__init__(msg)
+
+
+_tuning_seen = None
+
+
+def sync_tuning() -> None:
+    """The library snapshots the MIPX_* kernel-selection knobs on first use; when the
+    Python process changed them since (tests, A/B scripts), take a new snapshot.  Call
+    between launches only (the library's rule for mipx_tuning_reload)."""
+    global _tuning_seen
+    cur = tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("MIPX_")))
+    if cur != _tuning_seen:
+        lib.mipx_tuning_reload()
+        _tuning_seen = cur
 
 
 def check(code: int, what: str = "mipx") -> int:

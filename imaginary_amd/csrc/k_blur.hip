@@ -506,7 +506,7 @@ int blur_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left
                      const std::vector<int> &mask, int scale, hipStream_t st) {
     // default RGB only: RGBA's tap window spans 16 + 4 (taps - 1) bytes, two K steps from
     // 13 taps on, and k_blur2d's dot4 path stays ahead there (blur_ab.jsonl); MIPX_BMF=1 forces
-    const char *ef = std::getenv("MIPX_BMF");
+    const char *ef = tune_env("MIPX_BMF");
     if (ef && *ef == '0') return MIPX_EUNSUPPORTED;
     const bool forced = ef && *ef == '1';
     const int taps = static_cast<int>(mask.size());
@@ -531,7 +531,7 @@ int blur_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left
     // and reload fewer rows; bmf_rg_ab.jsonl / bmf_rg3_ab.jsonl: 32 rows -17 to -21 % on
     // RGB at sigma 1-5, 48 rows a further -7 % at sigma 1 and +1-5 % at sigma 3-5);
     // MIPX_BMF_RG=1/2/3 forces 16 / 32 / 48
-    const char *eg = std::getenv("MIPX_BMF_RG");
+    const char *eg = tune_env("MIPX_BMF_RG");
     const int rg = (eg && *eg) ? std::min(3, std::max(1, std::atoi(eg)))
                                : (oh >= 48 && taps <= 7) ? 3 : (oh >= 32 ? 2 : 1);
     const int rows = 16 * rg;
@@ -585,7 +585,7 @@ int blur_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left
 // MIPX_BLUR2D=0 disables it (A/B), MIPX_BLUR2D_ROWS sets the rows per block.
 int blur2d_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, int top, int ow, int oh,
                   const std::vector<int> &mask, int scale, hipStream_t st) {
-    const char *ef = std::getenv("MIPX_BLUR2D");
+    const char *ef = tune_env("MIPX_BLUR2D");
     if (ef && *ef == '0') return MIPX_EUNSUPPORTED;
     const int taps = static_cast<int>(mask.size());
     const int nq = (taps + 6) >> 2;
@@ -604,7 +604,7 @@ int blur2d_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, i
     a.h = oh;
     const int xblk = (ow + 255) / 256;
     a.bw = ((ow + xblk - 1) / xblk + 3) & ~3;
-    const char *er = std::getenv("MIPX_BLUR2D_ROWS");
+    const char *er = tune_env("MIPX_BLUR2D_ROWS");
     int kb = (er && *er) ? std::atoi(er) : 128;  // 64: +5 %, 32: +14 % (v17/ab_blur2d_c3.log)
     kb = std::max(4, std::min(kb, 1024)) & ~3;
     a.kb = std::min(kb, (oh + 3) & ~3);
@@ -617,7 +617,7 @@ int blur2d_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, i
     a.mag = static_cast<uint32_t>(((1ULL << 32) + scale - 1) / scale);
     a.inv = 1.0f / static_cast<float>(scale);
     a.fofs = (static_cast<float>(a.rnd) + 0.5f) * a.inv;
-    const char *efr = std::getenv("MIPX_BLUR2D_FROUND");
+    const char *efr = tune_env("MIPX_BLUR2D_FROUND");
     const bool fr = efr && *efr == '1';  // fp32 rounding: 2-3 % slower (v17/ab_blur2d_fround_*.log)
     for (int p = 0; p < 4; ++p)
         for (int j = 0; j < kB2MaxQ; ++j) {

@@ -485,11 +485,11 @@ int embed_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x, int y
     a.in_img = img_bytes(w, h, b);
     a.out_img = img_bytes(ow, oh, b);
     a.origins = d_origins;
-    const char *eq = std::getenv("MIPX_EMBED_Q16");  // A/B: 0 keeps the 5-dword loads
+    const char *eq = tune_env("MIPX_EMBED_Q16");  // A/B: 0 keeps the 5-dword loads
     a.q16 = aligned4(in) && a.in_img % 4 == 0 && !(eq && *eq == '0');
     if (b == 4 && !(aligned4(in) && aligned4(out))) return MIPX_EINVAL;
     if (aligned4(in) && (a.in_img % 4) == 0 && a.in_img < 0x7fffffffLL && oh <= 65535) {
-        const char *er = std::getenv("MIPX_EMBED_RPB");
+        const char *er = tune_env("MIPX_EMBED_RPB");
         a.rpb = (er && *er) ? std::max(1, std::atoi(er)) : 4;
         const dim3 grid((ow * b + 4095) / 4096, (oh + a.rpb - 1) / a.rpb, n);
         MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_embed_rows<B_>, grid, dim3(256), 0, st, a));
@@ -502,7 +502,7 @@ int flip_rows_launch(const u8 *in, u8 *out, int n, int w, int h, int b, bool mir
     if (h > 65535) return MIPX_EUNSUPPORTED;
     const long long ib = img_bytes(w, h, b);
     if (ib >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
-    const char *er = std::getenv("MIPX_FLIP_RPB");
+    const char *er = tune_env("MIPX_FLIP_RPB");
     const int rpb = (er && *er) ? std::max(1, std::atoi(er)) : 4;
     const dim3 grid((w * b + 4095) / 4096, (h + rpb - 1) / rpb, n);
     if (mirror) {
@@ -541,18 +541,18 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
     if (angle == 180 && img_bytes(w, h, b) < 0x7fffffffLL && h <= 65535)
         return flip_rows_launch(in, out, n, w, h, b, true, true, st);
     if ((angle == 90 || angle == 270) && img_bytes(w, h, b) < 0x7fffffffLL) {
-        const char *eth = std::getenv("MIPX_ROT_TH");
+        const char *eth = tune_env("MIPX_ROT_TH");
         const int th = eth && *eth ? (std::atoi(eth) == 128 ? 128 : 64) : 64;
         const int tx = (w + 63) / 64, ty = (h + th - 1) / th;
         const long long nblk = static_cast<long long>(tx) * ty * n;
         if (nblk > 0x7fffffffLL) return MIPX_EUNSUPPORTED;
         const dim3 grid(static_cast<unsigned>(nblk));
         const long long ib = img_bytes(w, h, b);
-        const char *ex = std::getenv("MIPX_ROT_XCD");
+        const char *ex = tune_env("MIPX_ROT_XCD");
         // A/B (profiles/r01/v18/rotxcd_ab.jsonl): contiguous runs win 3-8% on 4K RGB, where a
         // 64-pixel tile row (192 B) splits a 128-byte line, and lose 2% on RGBA (whole lines)
         const int xcd = ex && *ex ? (*ex != '0') : ((64 * b) % 128 != 0);
-        const char *eq = std::getenv("MIPX_ROT_Q16");  // A/B: 0 keeps the b64-per-dword staging
+        const char *eq = tune_env("MIPX_ROT_Q16");  // A/B: 0 keeps the b64-per-dword staging
         const int q16 = !(eq && *eq == '0');
 #define MIPX_ROT(CW_, TH_)                                                                                     \
     MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, CW_, TH_>), grid, dim3(256), 0, st, in, out, w, h, ib, \

@@ -405,18 +405,23 @@ int reduceh_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hsh
 }
 
 // Both shrinks > 1 in one launch, output window [ox0, ox0 + ow) x [oy0, oy0 + oh):
-// k_rmf2 (matrix cores) first, then the small-image strip walker (rows k_rmf2 does
-// not take: unaligned, > 16 taps), then the A/B fused kernels; MIPX_EUNSUPPORTED
-// leaves it to the two separable passes.  small_ab.jsonl: k_rmf2 2x faster than the
-// strip walker on small images (C1's 480x270 / 1.6 0.161 -> 0.075 ms);
-// MIPX_RSTRIP=1 puts the strip walker first again.
+// the column walker k_rcol (matrix cores, LDS row ring; dword-aligned input rows,
+// <= 16 taps) first, then k_rmf2 (matrix cores, rows of any alignment), then the
+// small-image strip walker and fused kernel (> 16 taps); MIPX_EUNSUPPORTED leaves it
+// to the two separable passes.  MIPX_RCOL=0 / MIPX_RMFMA=0 turn the first two off
+// (A/B); MIPX_RSTRIP=1 puts the strip walker first.
 int reduce_one_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
                       int ow, int oh, hipStream_t st) {
-    const char *ef = std::getenv("MIPX_RSTRIP");
+    const char *ef = tune_env("MIPX_RSTRIP");
     const bool strip_first = ef && *ef == '1';
     if (strip_first) {
         const int se = reduce_strip_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
         if (se != MIPX_EUNSUPPORTED) return se;
+    }
+    const char *ec = tune_env("MIPX_RCOL");
+    if (!(ec && *ec == '0')) {
+        const int ce = reduce_col_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
+        if (ce != MIPX_EUNSUPPORTED) return ce;
     }
     const int me = reduce_mfma_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
     if (me != MIPX_EUNSUPPORTED) return me;
@@ -424,9 +429,7 @@ int reduce_one_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
         const int se = reduce_strip_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
         if (se != MIPX_EUNSUPPORTED) return se;
     }
-    const int fe = reduce_fused_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
-    if (fe != MIPX_EUNSUPPORTED) return fe;
-    return reduce2d_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
+    return reduce_fused_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
 }
 
 // vips_reduce followed by vips_extract_area(left, top, ow, oh): only the
@@ -496,15 +499,16 @@ bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
     return shape_ok;
 }
 
-// MIPX_R2_VARIANT overrides the default variant of k_reduce2x2 for A/B runs
-// (scripts/ab_reduce.py); read per launch so one process can interleave them.
+// k_reduce2x2 build variant.  Only the shipped one (66) is compiled now; the r01 / r02
+// A/B builds (strip widths, register prefetch, LDS row strides) are recorded under
+// profiles/r01 and profiles/r02 (scripts/ab_reduce.py ran them).
 constexpr int kR2Default = 66;  // wide strips, R = 12 + register prefetch: measured best (profiles/r01/v10_wide_ab.log)
 int reduce2_variant() {
-    const char *e = std::getenv("MIPX_R2_VARIANT");
+    const char *e = tune_env("MIPX_R2_VARIANT");
     if (!e || !*e) return kR2Default;
     const int v = std::atoi(e);
     switch (v) {
-        case 0: case 1: case 2: case 3: case 6: case 10: case 66: case 67: case 130: case 131: case 322: case 323: return v;
+        case 66: return v;
         default: return kR2Default;
     }
 }
@@ -539,7 +543,7 @@ int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int
     a.n_strips = (x1 + tw - 1) / tw - a.s_base;
     const int chunks = (y1 - a.y_base + kR - 1) / kR;
     // rows per workgroup: 2 chunks of 12 (measured best, profiles/r01/geom_ab.log; MIPX_R2_BAND overrides)
-    const char *eb = std::getenv("MIPX_R2_BAND");
+    const char *eb = tune_env("MIPX_R2_BAND");
     const int cpb = (eb && *eb) ? std::max(1, std::atoi(eb)) : 2;
     const int chunks_per_band = std::max(1, std::min(chunks, cpb));
     a.band_rows = chunks_per_band * kR;
@@ -551,9 +555,9 @@ int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int
     a.c3 = c[2] / 4096.0f;
     a.c5 = c[3] / 4096.0f;
     a.bias = 1.0f / 8192.0f;
-    const char *er = std::getenv("MIPX_R2_REMAP");
+    const char *er = tune_env("MIPX_R2_REMAP");
     a.remap = (er && *er) ? std::atoi(er) : 1;
-    const char *eo = std::getenv("MIPX_R2_ORDER");
+    const char *eo = tune_env("MIPX_R2_ORDER");
     a.band_major = (eo && *eo) ? std::atoi(eo) : 0;
     const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
@@ -566,8 +570,7 @@ int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int
         break;                                                                                          \
     }
     switch (var) {
-        MIPX_R2(0) MIPX_R2(1) MIPX_R2(2) MIPX_R2(3) MIPX_R2(6) MIPX_R2(10) MIPX_R2(66) MIPX_R2(67) MIPX_R2(130) MIPX_R2(131)
-        MIPX_R2(322) MIPX_R2(323)
+        MIPX_R2(66)
         default: return MIPX_EINVAL;
     }
 #undef MIPX_R2

@@ -390,7 +390,7 @@ int reduce_strip_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
     // passes): faster on small images (364x273 / 480x270 RGB: -16 / -21 %), even at
     // 500x375, slower on large ones (1080p RGB / 1.6: +9 %), where both are VALU-
     // issue bound and the two passes keep more waves busy.  MIPX_RSTRIP=0/1 forces.
-    const char *ef = std::getenv("MIPX_RSTRIP");
+    const char *ef = tune_env("MIPX_RSTRIP");
     if (ef && *ef) {
         if (*ef == '0') return MIPX_EUNSUPPORTED;
     } else if (img_bytes(w, h, b) > 512 * 1024) {
@@ -421,7 +421,7 @@ int reduce_strip_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
     a.padh = a.th / 2 - 1;
     a.vs = vs;
     a.hs = hs;
-    const char *edg = std::getenv("MIPX_RSTRIP_DIAG");
+    const char *edg = tune_env("MIPX_RSTRIP_DIAG");
     a.diag = (edg && *edg) ? std::atoi(edg) : 0;
     // every row of every image starts dword aligned: no per-row byte skew
     const bool sk = (a.pitch % 4) != 0 || (a.in_img % 4) != 0 || (reinterpret_cast<uintptr_t>(in) % 4) != 0;
@@ -431,7 +431,7 @@ int reduce_strip_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
         const int span = static_cast<int>(std::ceil((tw - 1) * hs)) + a.th + 2;
         return (span + 3 + 3) / 4 + 1;
     };
-    const char *etw = std::getenv("MIPX_RSTRIP_TW");
+    const char *etw = tune_env("MIPX_RSTRIP_TW");
     int tw = (etw && *etw && std::atoi(etw) == 64) ? 64
              : (units_for(128) <= 64 && units_for(128) * b + 1 <= 256 ? 128 : 64);
     if (ow <= 64) tw = 64;
@@ -443,7 +443,7 @@ int reduce_strip_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
     const int tpv = (a.tv + 2) / 2;
     // rows one chunk reads (through its last aligned pair) + one
     a.ring = static_cast<int>(std::ceil((kRsR - 1) * vs)) + 2 * tpv + 4;
-    const char *eb = std::getenv("MIPX_RSTRIP_BAND");
+    const char *eb = tune_env("MIPX_RSTRIP_BAND");
     int band = (eb && *eb) ? std::max(kRsR, std::atoi(eb) / kRsR * kRsR) : 64;
     band = std::min(band, ((oh + kRsR - 1) / kRsR) * kRsR);
     a.band = band;

@@ -41,10 +41,8 @@ struct SepTaps {
     float rounding, inv_scale;  // conv rounding
     int dot;                 // integer dot paths (MIPX_SEP_DOT=0 selects the float path)
     int tq;                  // conv vpass: rows transposed once per 4-row quad (MIPX_SEP_TQ=0: per output row)
-    int share;               // reduce vpass: byte pairs shared by the block's rows (MIPX_VP_SHARE=1, A/B)
 };
 
-constexpr int kShareRows = 12;  // output rows per block on the shared-pair reduce path
 constexpr int kVpPairs = 8;     // tap pairs of the unrolled vertical reduce (taps <= 16: shrink < 2.75)
 
 // Reduce masks are 12-bit signed integers (x 4096), so tap pairs fit packed
@@ -121,7 +119,6 @@ struct VPassArgs {
     int col_blocks, kr_blocks;
     int kr;               // output rows per block
     int lrows;            // LDS input-row capacity (>= (kr - 1) * shrink + taps + 1)
-    int np;               // shared-pair reduce: staged row pairs a block can touch
     SepTaps tp;
 };
 
@@ -283,27 +280,7 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
         }
         cpk[tq + tid] = w;
     }
-    const int tpa = taps / 2 + 1;  // shared pairs: a row's window spans tpa staged-row pairs
-    if (MODE == kSepReduce && a.tp.dot && a.tp.share && DMA != 0) {
-        // row k starts at staged row soff[k]; staged pair jp = rows (2jp, 2jp + 1) is
-        // pair m = jp - (soff[k] >> 1) of row k, taps (2m - al, 2m + 1 - al) with
-        // al = soff[k] & 1.  Table [jp][kShareRows], 0 where the row does not cover jp.
-        for (int i = tid; i < a.np * kShareRows; i += 256) {
-            const int jp = i / kShareRows, k = i - jp * kShareRows;
-            uint32_t w = 0;
-            if (k < nk) {
-                int st;
-                sep_position(a.tp, a.oy0 + y0 + k, &st, &ph);
-                const int so = st - r_lo, m = jp - (so >> 1);
-                if (m >= 0 && m < tpa) {
-                    const float *c = a.tp.tab + ph * taps;
-                    const int t0 = 2 * m - (so & 1);
-                    w = pack_pair(t0 >= 0 && t0 < taps ? c[t0] : 0.f, t0 + 1 < taps ? c[t0 + 1] : 0.f);
-                }
-            }
-            cpk[i] = w;
-        }
-    } else if (MODE == kSepReduce && a.tp.dot) {
+    if (MODE == kSepReduce && a.tp.dot) {
         for (int i = tid; i < nk * tp2; i += 256) {
             const int k = i / tp2, m = i - k * tp2;
             int st;
@@ -378,57 +355,6 @@ __global__ void __launch_bounds__(256) k_vpass(VPassArgs a) {
             uint32_t o = 0;
 #pragma unroll
             for (int z = 0; z < 4; ++z) o |= sep_round<MODE>(static_cast<float>(acc[z]), a.tp) << (8 * z);
-            u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
-            if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
-                *reinterpret_cast<uint32_t *>(q) = o;
-            } else {
-                for (int z = 0; z < nb; ++z) q[z] = static_cast<u8>(o >> (8 * z));
-            }
-        }
-        return;
-    }
-    if (MODE == kSepReduce && a.tp.dot && a.tp.share && DMA != 0) {
-        // Pair-outer: each staged row pair is read and byte-paired (2 LDS reads +
-        // 4 v_perm) once for all of the block's output rows whose window covers it,
-        // instead of once per output row; coverage tests are uniform (SGPR) branches.
-        int jk[kShareRows];
-#pragma unroll
-        for (int k = 0; k < kShareRows; ++k) jk[k] = __builtin_amdgcn_readfirstlane(k < nk ? soff[k] >> 1 : 1 << 20);
-        const int npair = __builtin_amdgcn_readfirstlane((soff[nk - 1] >> 1) + tpa);
-        int acc[kShareRows][4];
-#pragma unroll
-        for (int k = 0; k < kShareRows; ++k)
-#pragma unroll
-            for (int z = 0; z < 4; ++z) acc[k][z] = 0;
-        const uint32_t *rp = rows + tid;
-        for (int jp = 0; jp < npair; ++jp) {
-            const uint32_t v0 = rp[(2 * jp) * kVStride], v1 = rp[(2 * jp + 1) * kVStride];
-            uint32_t pr[4];
-#pragma unroll
-            for (int z = 0; z < 4; ++z) pr[z] = __builtin_amdgcn_perm(v1, v0, 0x0C040C00u + 0x00010001u * z);
-            uint32_t cw[kShareRows];  // this pair's coefficient for every row: 3 broadcast b128 reads
-            const uint4 *cq = reinterpret_cast<const uint4 *>(cpk + jp * kShareRows);
-#pragma unroll
-            for (int q = 0; q < kShareRows / 4; ++q) {
-                const uint4 c4 = cq[q];
-                cw[4 * q] = c4.x, cw[4 * q + 1] = c4.y, cw[4 * q + 2] = c4.z, cw[4 * q + 3] = c4.w;
-            }
-#pragma unroll
-            for (int k = 0; k < kShareRows; ++k) {
-                if (static_cast<unsigned>(jp - jk[k]) < static_cast<unsigned>(tpa)) {
-#pragma unroll
-                    for (int z = 0; z < 4; ++z)
-                        acc[k][z] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pr[z]),
-                                                           __builtin_bit_cast(short2v, cw[k]), acc[k][z], false);
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kShareRows; ++k) {
-            if (k >= nk) continue;
-            uint32_t o = 0;
-#pragma unroll
-            for (int z = 0; z < 4; ++z) o |= fixed_round_i(acc[k][z]) << (8 * z);
             u8 *q = dst + static_cast<long long>(k) * a.row_bytes;
             if (nb == 4 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
                 *reinterpret_cast<uint32_t *>(q) = o;
@@ -1003,7 +929,7 @@ __global__ void __launch_bounds__(256) k_hreduce(HPassArgs a) {
 }
 
 // ===========================================================================
-// horizontal reduce on the matrix cores (k_hmfma)
+// banded products on the i8 matrix cores (k_rmf2's horizontal pass)
 // ===========================================================================
 // A 16-pixel output group of 16 image rows is a banded product: out[px][row] =
 // sum_k C[px][k] * in[row][base + k], k over the 64-pixel K steps covering the
@@ -1020,22 +946,6 @@ __global__ void __launch_bounds__(256) k_hreduce(HPassArgs a) {
 // row per channel: 12 / 16 contiguous bytes to store.
 constexpr int kHmRows = 16;  // image rows per block (the MFMA N)
 typedef int hm_v4i __attribute__((ext_vector_type(4)));
-
-struct HmArgs {
-    const u8 *in;
-    u8 *out;
-    int in_pitch;
-    long long in_base, in_img, out_img;
-    int wl, rows, ox0, ow;
-    int x_blocks, rb_blocks;
-    int plane_w;  // staged bytes per channel row (multiple of 16; covers every group's K steps)
-    int row_w;    // bytes per staged image row (B planes; / 16 odd: the 16 rows' b128 reads hit distinct banks)
-    int nks;      // 64-pixel K steps per group
-    int raw_max;  // LDS dwords per DMA-staged raw row
-    const signed char *tab;  // device_reduce_i8
-    const int *tsum;
-    SepTaps tp;
-};
 
 // The 16-byte fragment of an i8 tap row at window offset o (tap o + j in byte j,
 // 0 outside the taps): rows hold taps <= 16 after kHmTabPad zeros, so windows
@@ -1054,209 +964,9 @@ __device__ __forceinline__ hm_v4i load_taps16(const signed char *row, int o) {
     return r;
 }
 
-// XW output pixels per block (XW / 64 groups per wave)
-template <int B, int XW>
-__global__ void __launch_bounds__(256) k_hmfma(HmArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hsm[];
-    constexpr int GPW = XW / 64;            // groups per wave
-    int *ps = reinterpret_cast<int *>(hsm);  // [XW] first tap pixel of each output pixel
-    int *pph = ps + XW;                      // [XW] phase
-    int *pbias = pph + XW;                   // [XW] 128 * tap sum + 2048
-    u8 *planes = reinterpret_cast<u8 *>(pbias + XW);  // [kHmRows][row_w: B x plane_w] pixel - 128
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int xb = t % a.x_blocks;
-    const int rest = t / a.x_blocks;
-    const int rb = rest % a.rb_blocks;
-    const int img = rest / a.rb_blocks;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int x0 = xb * XW;
-    const int x_last = min(x0 + XW - 1, a.ow - 1);
-    int lo, ph0;
-    sep_position(a.tp, a.ox0 + x0, &lo, &ph0);
-    const int org = lo & ~15;  // plane byte 0 = input pixel org (floor to 16)
-    int hi;
-    sep_position(a.tp, a.ox0 + x_last, &hi, &ph0);
-    hi += a.tp.taps - 1;
-    const int cl = max(lo, 0), ch = min(hi, a.wl - 1);  // pixels DMA'd per row
-    const int y_first = rb * kHmRows;
-    const int nr = min(kHmRows, a.rows - y_first);
-    uint32_t *raw = reinterpret_cast<uint32_t *>(planes + kHmRows * a.row_w);  // [kHmRows][raw_max]
-    // ---- raw bytes of the span, every row in flight (direct-to-LDS dword DMA) ----
-    // (byte offsets fit int: the launcher requires images < 2 GiB)
-    int delta = 0;
-    const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &delta);
-    const int row0 = delta + static_cast<int>(a.in_base) + y_first * a.in_pitch + B * cl;
-    const int chunks = ((B * (ch - cl + 1) + 6) / 4 + 63) >> 6;
-    for (int r = wave; r < nr; r += 4) {
-        const int a4 = (row0 + r * a.in_pitch) & ~3;
-        for (int c = 0; c < chunks; ++c)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + r * a.raw_max + c * 64), 4, 4 * (c * 64 + lane),
-                                                     a4, 0, 0);
-    }
-    if (tid < XW) {
-        int sp, ph;
-        sep_position(a.tp, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
-        ps[tid] = sp;
-        pph[tid] = ph;
-        pbias[tid] = 128 * a.tsum[ph] + 2048;
-    }
-    __syncthreads();
-    // this wave's 4 groups: first K step's taps requested now, consumed after the repack
-    const int n = lane & 15, kg = lane >> 4;
-    int go[GPW];
-    const signed char *gt[GPW];
-    hm_v4i ah0[GPW], al0[GPW];
-#pragma unroll
-    for (int gi = 0; gi < GPW; ++gi) {
-        const int g = wave * GPW + gi;
-        const int p = min(16 * g + n, x_last - x0);
-        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
-        go[gi] = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
-        gt[gi] = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
-        ah0[gi] = load_taps16(gt[gi], go[gi]);
-        al0[gi] = load_taps16(gt[gi] + kHmTabW, go[gi]);
-    }
-    // ---- channel-planar repack (pixel - 128), COPY edges by clamping into [cl, ch] ----
-    // rows per wave (uniform skew and shift), 4-pixel quads per lane
-    const int q_lo = (lo - org) >> 2, q_hi = (hi - org) >> 2;  // quads holding taps (the rest stays stale)
-    for (int r = wave; r < kHmRows; r += 4) {
-        const int rr = min(r, nr - 1);  // rows past the image: any staged row (never stored)
-        const int skew = (row0 + rr * a.in_pitch) & 3;
-        const int ob0 = (org - cl) * B + skew;  // raw byte of plane pixel 0 (may be < 0: clamped path)
-        const int sh = ob0 & 3;
-        const uint32_t *rwr = raw + rr * a.raw_max;
-        const u8 *rw8 = reinterpret_cast<const u8 *>(rwr) + skew;
-        u8 *pl = planes + r * a.row_w;
-        for (int q = q_lo + lane; q <= q_hi; q += 64) {
-            const int p0 = org + 4 * q;
-            uint32_t w[B];
-            // pixels outside [lo, hi] have zero taps, so only quads past an image edge
-            // need the clamp; inside a block the raw row (and its neighbours) is read as is
-            if (!((lo < 0 && p0 < 0) || (hi >= a.wl && p0 + 3 >= a.wl))) {
-                const uint32_t *rw = rwr + ((ob0 + 4 * B * q) >> 2);
-                uint32_t x[B];
-#pragma unroll
-                for (int k = 0; k < B; ++k) x[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], sh);
-                if (B == 3) {  // x = [r0 g0 b0 r1] [g1 b1 r2 g2] [b2 r3 g3 b3]
-                    w[0] = __builtin_amdgcn_perm(x[2 % B], __builtin_amdgcn_perm(x[1], x[0], 0x0c060300u), 0x05020100u);
-                    w[1] = __builtin_amdgcn_perm(x[2 % B], __builtin_amdgcn_perm(x[1], x[0], 0x0c070401u), 0x06020100u);
-                    w[2 % B] = __builtin_amdgcn_perm(x[2 % B], __builtin_amdgcn_perm(x[1], x[0], 0x0c0c0502u), 0x07040100u);
-                } else {
-                    uint32_t tt[4];
-                    transpose4x4(x[0], x[1 % B], x[2 % B], x[3 % B], tt);
-#pragma unroll
-                    for (int z = 0; z < B; ++z) w[z] = tt[z];
-                }
-            } else {
-#pragma unroll
-                for (int z = 0; z < B; ++z) w[z] = 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const u8 *px = rw8 + (clampi(p0 + j, cl, ch) - cl) * B;
-#pragma unroll
-                    for (int z = 0; z < B; ++z) w[z] |= static_cast<uint32_t>(px[z]) << (8 * j);
-                }
-            }
-#pragma unroll
-            for (int z = 0; z < B; ++z) reinterpret_cast<uint32_t *>(pl + z * a.plane_w)[q] = w[z] ^ 0x80808080u;
-        }
-    }
-    __syncthreads();
-    // ---- GPW groups of 16 output pixels per wave ----
-    u8 *ob = a.out + img * a.out_img;
-    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
-#pragma unroll
-    for (int gi = 0; gi < GPW; ++gi) {
-        const int g = wave * GPW + gi;
-        if (x0 + 16 * g > x_last) break;
-        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
-        const int4 bias = *reinterpret_cast<const int4 *>(pbias + 16 * g + 4 * kg);
-        hm_v4i acc_h[B], acc_l[B];
-#pragma unroll
-        for (int z = 0; z < B; ++z) {
-            acc_h[z] = hm_v4i{0, 0, 0, 0};
-            acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
-        }
-        for (int ks = 0; ks < a.nks; ++ks) {
-            const hm_v4i ah = ks == 0 ? ah0[gi] : load_taps16(gt[gi], go[gi] + 64 * ks);
-            const hm_v4i al = ks == 0 ? al0[gi] : load_taps16(gt[gi] + kHmTabW, go[gi] + 64 * ks);
-#pragma unroll
-            for (int z = 0; z < B; ++z) {
-                const hm_v4i bz =
-                    *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 64 * ks + 16 * kg);
-                acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bz, acc_h[z], 0, 0, 0);
-                acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bz, acc_l[z], 0, 0, 0);
-            }
-        }
-        uint32_t wz[4];  // channel z of output pixels 4 kg .. 4 kg + 3 of row n
-#pragma unroll
-        for (int z = 0; z < B; ++z)
-            wz[z] = round_pack4((acc_h[z][0] << 6) + acc_l[z][0], (acc_h[z][1] << 6) + acc_l[z][1],
-                                (acc_h[z][2] << 6) + acc_l[z][2], (acc_h[z][3] << 6) + acc_l[z][3]);
-        if (n >= nr) continue;
-        const int x = x0 + 16 * g + 4 * kg;
-        if (x > x_last) continue;
-        uint32_t o[4];
-        if (B == 3) {  // [R G B] x 4 pixels -> [r0 g0 b0 r1] [g1 b1 r2 g2] [b2 r3 g3 b3]
-            o[0] = __builtin_amdgcn_perm(wz[2 % B], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
-            o[1] = __builtin_amdgcn_perm(wz[2 % B], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
-            o[2] = __builtin_amdgcn_perm(wz[2 % B], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
-        } else {
-            transpose4x4(wz[0], wz[1 % B], wz[2 % B], wz[3 % B], o);
-        }
-        if (B == 3) {  // into the block's output tile (the raw rows are dead after the repack)
-            uint32_t *tq = reinterpret_cast<uint32_t *>(reinterpret_cast<u8 *>(raw) + n * (XW * 3 + 4) + (x - x0) * 3);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) tq[k] = o[k];
-            continue;
-        }
-        const int qo = ((y_first + n) * a.ow + x) * B;  // byte offset in the output image
-        if (x + 3 <= x_last) {
-            __builtin_amdgcn_raw_buffer_store_b128(
-                hm_v4i{static_cast<int>(o[0]), static_cast<int>(o[1 % B]), static_cast<int>(o[2 % B]),
-                       static_cast<int>(o[3 % B])}, os, qo, 0, 0);
-        } else {
-            const int np = min(4, x_last - x + 1);
-            for (int k = 0; k < np * B; ++k) ob[qo + k] = static_cast<u8>(o[k >> 2] >> (8 * (k & 3)));
-        }
-    }
-    if (B == 3) {  // each tile row to its output row as whole dwords at the row's own alignment
-        __syncthreads();
-        const int nb = (x_last - x0 + 1) * 3;
-        for (int r = wave; r < nr; r += 4) {
-            const u8 *tr = reinterpret_cast<const u8 *>(raw) + r * (XW * 3 + 4);
-            const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
-            const int qo0 = ((y_first + r) * a.ow + x0) * 3;
-            const int d0 = qo0 >> 2, nd = ((qo0 + nb + 3) >> 2) - d0;
-            const int sh = (4 - (qo0 & 3)) & 3;  // tile byte of dword i's first byte: 4 i - (qo0 & 3)
-            for (int i = lane; i < nd; i += 64) {
-                const int e = 4 * (d0 + i) - qo0;
-                if (e >= 0 && e + 4 <= nb) {
-                    const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
-                    __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i), 0, 0);
-                } else {
-                    for (int k = 0; k < 4; ++k)
-                        if (e + k >= 0 && e + k < nb)
-                            __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k, 0, 0);
-                }
-            }
-        }
-    }
-}
-
 // ===========================================================================
-// fused reduce: vertical dot2 pass into channel-planar LDS, horizontal pass on
-// the matrix cores (k_rmfma)
+// fused reduce on the matrix cores (k_rmf2): both passes on v_mfma_i32_16x16x64_i8
 // ===========================================================================
-// A block = 128 output pixels x 16 output rows of one RGB image.  The input rows
-// the 16 rows need are DMA'd to LDS from byte 3 * org (org = the block's first tap
-// pixel floored to 16, so every 4-pixel quad is 3 aligned dwords); each wave then
-// computes 4 intermediate rows (reducev: k_vreduce's dot2 sums, rounding and
-// clamping) quad by quad, deinterleaves them to channel planes as pixel - 128
-// (the MFMA's signed i8), and after one barrier the horizontal pass runs as in
-// k_hmfma: no intermediate in HBM, and the horizontal products off the VALU.
-// Rows must be dword aligned (3 w % 4 == 0, aligned batch); taps <= 16 each way.
 constexpr int kRmRows = 16;
 constexpr int kRmXW = 128;
 constexpr int kRmMaxCt = 16;  // k_rmf2: 16-byte column tiles per wave (staged span <= 1024 bytes)
@@ -1268,201 +978,21 @@ struct RmArgs {
     long long in_img, out_img;
     int x_blocks, y_blocks;
     int lrows;    // staged input rows per block (>= 15 vs + vtaps)
-    int rs;       // LDS dwords per staged row (DMA chunks of 64)
     int plane_w;  // bytes per channel plane row (multiple of 16)
-    int row_w;    // bytes per intermediate row (3 planes; / 16 odd)
+    int row_w;    // bytes per intermediate row (B planes; / 16 odd)
     int nks;      // 64-pixel K steps per horizontal group
-    const uint32_t *vpairs;  // device_reduce_pairs(vs): [129][2][tpav]
-    int tpav;
-    const signed char *tab;  // device_reduce_i8(hs)
+    const signed char *tab;   // device_reduce_i8(hs)
     const int *tsum;
-    const signed char *tabv;  // k_rmf2: device_reduce_i8(vs)
+    const signed char *tabv;  // device_reduce_i8(vs)
     const int *tsumv;
-    int iw;                   // k_rmf2: bytes per row-major intermediate row (16 x column tiles)
-    int direct;               // k_rmf2: output rows and images dword aligned (12-byte stores, no tile)
-    int tiles;                // k_rmf3: 16-row x 128-pixel tiles of the batch (column-major)
-    int rsd;                  // k_rmf2: staged row stride in dwords, (rsd mod 64) / 4 odd
-    const signed char *tabs;  // k_rmf4: device_reduce_i8s(hs, B), taps at a byte stride of B
-    int orgmask;              // k_rmf2: first staged pixel = lo & orgmask (~3; ~15 is the r02 A/B)
-    int dbg;                  // k_rmf2 timing experiments (MIPX_RMF2_DBG, wrong pixels): 1 no staging
-                              // loads, 2 no products, 4 no position set-up (rmf2_parts.jsonl)
+    int iw;                   // bytes per row-major intermediate row (16 x column tiles)
+    int direct;               // output rows and images dword aligned (12-byte stores, no tile)
+    int rsd;                  // staged row stride in dwords, (rsd mod 64) / 4 odd
     SepTaps tv, th;
 };
 
-// RS: LDS dwords per staged row (compile time, so row offsets are immediates)
-template <int TV, int RS>
-__global__ void __launch_bounds__(256) k_rmfma(RmArgs a) {
-    constexpr int B = 3, XW = kRmXW, GPW = XW / 64;
-    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
-    int *ps = reinterpret_cast<int *>(rsm);  // [XW] horizontal: first tap pixel
-    int *pph = ps + XW;                      // [XW] phase
-    int *pbias = pph + XW;                   // [XW] 128 * tap sum + 2048
-    int *vso = pbias + XW;                   // [kRmRows] vertical: first staged row of each output row
-    uint32_t *vcp = reinterpret_cast<uint32_t *>(vso + kRmRows);  // [kRmRows][8] vertical tap pairs
-    u8 *planes = reinterpret_cast<u8 *>(vcp + kRmRows * 8);      // [kRmRows][row_w]
-    uint32_t *raw = reinterpret_cast<uint32_t *>(planes + kRmRows * a.row_w + 64);  // [lrows][RS]
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int xb = t % a.x_blocks;
-    const int rest = t / a.x_blocks;
-    const int yb = rest % a.y_blocks;
-    const int img = rest / a.y_blocks;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int x0 = xb * XW, x_last = min(x0 + XW - 1, a.ow - 1);
-    const int y0 = yb * kRmRows, nr = min(kRmRows, a.oh - y0);
-    int lo, hi, ph0, r_lo, r_last;
-    sep_position(a.th, a.ox0 + x0, &lo, &ph0);
-    sep_position(a.th, a.ox0 + x_last, &hi, &ph0);
-    hi += a.th.taps - 1;
-    sep_position(a.tv, a.oy0 + y0, &r_lo, &ph0);
-    sep_position(a.tv, a.oy0 + y0 + nr - 1, &r_last, &ph0);
-    const int org = lo & ~15;
-    const int nqv = ((hi - org) >> 2) + 1;  // quads holding horizontal taps
-    const int L = r_last + a.tv.taps - r_lo;
-    // ---- input rows [r_lo, r_lo + L) (COPY-clamped), bytes from 3 org, all in flight ----
-    {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
-        const int pitch = a.w * B;
-        const int chunks = (3 * nqv + 63) >> 6;
-        for (int l = wave; l < L; l += 4) {
-            const int r = clampi(r_lo + l, 0, a.h - 1);
-            for (int c = 0; c < chunks; ++c)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
-                                                         3 * org + 4 * (c * 64 + lane), r * pitch, 0, 0);
-        }
-    }
-    if (tid < XW) {
-        int sp, ph;
-        sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
-        ps[tid] = sp;
-        pph[tid] = ph;
-        pbias[tid] = 128 * a.tsum[ph] + 2048;
-    } else if (tid < XW + kRmRows * 8) {
-        const int i = tid - XW, k = i >> 3, m = i & 7;
-        int sv, ph;
-        sep_position(a.tv, a.oy0 + y0 + min(k, nr - 1), &sv, &ph);
-        vcp[i] = m < a.tpav ? a.vpairs[(ph * 2) * a.tpav + m] : 0u;
-        if (m == 0) vso[k] = sv - r_lo;
-    }
-    __syncthreads();
-    // ---- vertical pass: wave w makes intermediate rows w, w + 4, ... as channel planes ----
-    for (int k = wave; k < nr; k += 4) {
-        const uint32_t *rk = raw + __builtin_amdgcn_readfirstlane(vso[k]) * RS;
-        const uint4 c0 = reinterpret_cast<const uint4 *>(vcp + k * 8)[0];
-        const uint4 c1 = reinterpret_cast<const uint4 *>(vcp + k * 8)[1];
-        const uint32_t cw[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-        u8 *pl = planes + k * a.row_w;
-        for (int q = lane; q < nqv; q += 64) {
-            const uint32_t *rp = rk + 3 * q;
-            uint32_t v[2 * TV][3];  // every staged row's 3 dwords requested before the first sum
-#pragma unroll
-            for (int i = 0; i < 2 * TV; ++i)
-#pragma unroll
-                for (int d = 0; d < 3; ++d) v[i][d] = rp[i * RS + d];
-            int acc[12];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) acc[i] = 2048;
-#pragma unroll
-            for (int m = 0; m < TV; ++m)
-#pragma unroll
-                for (int d = 0; d < 3; ++d)
-#pragma unroll
-                    for (int z = 0; z < 4; ++z)
-                        acc[4 * d + z] = dot2_byte(v[2 * m][d], v[2 * m + 1][d], z, cw[m], acc[4 * d + z]);
-            uint32_t x[3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) x[d] = round_pack4(acc[4 * d], acc[4 * d + 1], acc[4 * d + 2], acc[4 * d + 3]);
-            // [r0 g0 b0 r1] [g1 b1 r2 g2] [b2 r3 g3 b3] -> R, G, B planes
-            const uint32_t wr = __builtin_amdgcn_perm(x[2], __builtin_amdgcn_perm(x[1], x[0], 0x0c060300u), 0x05020100u);
-            const uint32_t wg = __builtin_amdgcn_perm(x[2], __builtin_amdgcn_perm(x[1], x[0], 0x0c070401u), 0x06020100u);
-            const uint32_t wb = __builtin_amdgcn_perm(x[2], __builtin_amdgcn_perm(x[1], x[0], 0x0c0c0502u), 0x07040100u);
-            reinterpret_cast<uint32_t *>(pl)[q] = wr ^ 0x80808080u;
-            reinterpret_cast<uint32_t *>(pl + a.plane_w)[q] = wg ^ 0x80808080u;
-            reinterpret_cast<uint32_t *>(pl + 2 * a.plane_w)[q] = wb ^ 0x80808080u;
-        }
-    }
-    __syncthreads();
-    // ---- COPY edge of the horizontal pass: pixels outside the image repeat its edge ----
-    if (lo < 0 || hi >= a.w) {
-        for (int i = tid; i < nr * (hi - org + 1); i += 256) {
-            const int k = i / (hi - org + 1), pq = i - k * (hi - org + 1);
-            const int p = org + pq;
-            if (p >= 0 && p < a.w) continue;
-            const int src = clampi(p, 0, a.w - 1) - org;
-#pragma unroll
-            for (int z = 0; z < B; ++z) planes[k * a.row_w + z * a.plane_w + pq] = planes[k * a.row_w + z * a.plane_w + src];
-        }
-        __syncthreads();
-    }
-    // ---- horizontal pass on the matrix cores (k_hmfma's group loop) ----
-    const int n = lane & 15, kg = lane >> 4;
-    u8 *ob = a.out + img * a.out_img;
-    u8 *tile = reinterpret_cast<u8 *>(raw);  // output tile [kRmRows][XW * 3 + 4] (the staged rows are dead)
-    __syncthreads();
-#pragma unroll
-    for (int gi = 0; gi < GPW; ++gi) {
-        const int g = wave * GPW + gi;
-        if (x0 + 16 * g > x_last) break;
-        const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
-        const int p = min(16 * g + n, x_last - x0);
-        const int o0 = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
-        const signed char *thr = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
-        const int4 bias = *reinterpret_cast<const int4 *>(pbias + 16 * g + 4 * kg);
-        hm_v4i acc_h[B], acc_l[B];
-#pragma unroll
-        for (int z = 0; z < B; ++z) {
-            acc_h[z] = hm_v4i{0, 0, 0, 0};
-            acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
-        }
-        for (int ks = 0; ks < a.nks; ++ks) {
-            const hm_v4i ah = load_taps16(thr, o0 + 64 * ks);
-            const hm_v4i al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
-#pragma unroll
-            for (int z = 0; z < B; ++z) {
-                const hm_v4i bz =
-                    *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 64 * ks + 16 * kg);
-                acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bz, acc_h[z], 0, 0, 0);
-                acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bz, acc_l[z], 0, 0, 0);
-            }
-        }
-        uint32_t wz[3];
-#pragma unroll
-        for (int z = 0; z < B; ++z)
-            wz[z] = round_pack4((acc_h[z][0] << 6) + acc_l[z][0], (acc_h[z][1] << 6) + acc_l[z][1],
-                                (acc_h[z][2] << 6) + acc_l[z][2], (acc_h[z][3] << 6) + acc_l[z][3]);
-        const int x = x0 + 16 * g + 4 * kg;
-        if (n >= nr || x > x_last) continue;
-        uint32_t *tq = reinterpret_cast<uint32_t *>(tile + n * (XW * 3 + 4) + (x - x0) * 3);
-        tq[0] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
-        tq[1] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
-        tq[2] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
-    }
-    __syncthreads();
-    // ---- each tile row to its output row as whole dwords at the row's own alignment ----
-    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
-    const int nb = (x_last - x0 + 1) * 3;
-    for (int r = wave; r < nr; r += 4) {
-        const u8 *tr = tile + r * (XW * 3 + 4);
-        const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
-        const int qo0 = ((y0 + r) * a.ow + x0) * 3 + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
-        const int d0 = qo0 >> 2, nd = ((qo0 + nb + 3) >> 2) - d0;
-        const int sh = (4 - (qo0 & 3)) & 3;
-        const int bias0 = static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
-        for (int i = lane; i < nd; i += 64) {
-            const int e = 4 * (d0 + i) - qo0;
-            if (e >= 0 && e + 4 <= nb) {
-                const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
-                __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i) - bias0, 0, 0);
-            } else {
-                for (int k = 0; k < 4; ++k)
-                    if (e + k >= 0 && e + k < nb)
-                        __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
-            }
-        }
-    }
-}
-
-// k_rmf2: the same fused reduce with the VERTICAL products on the matrix cores too.
+// k_rmf2: reducev -> reduceh in one launch, the products of both passes on the i8
+// matrix cores (the generic reduce for unaligned rows and shapes k_rcol declines).
 // Per 16-byte column tile of the staged rows: D[byte column][output row] =
 // A[byte column][staged row] x B[staged row][output row] on v_mfma_i32_16x16x64_i8,
 // where A (the pixels, K = 64 staged rows) comes from two ds_read_b64_tr_b8 (the
@@ -1504,14 +1034,14 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     hi += a.th.taps - 1;
     sep_position(a.tv, a.oy0 + y0, &r_lo, &ph0);
     sep_position(a.tv, a.oy0 + y0 + nr - 1, &r_last, &ph0);
-    const int org = lo & a.orgmask;  // first staged pixel: floor to 4 (r02; 16 before, MIPX_RMF2_ORG=16)
+    const int org = lo & ~3;  // first staged pixel: floor to 4 pixels (B org stays dword aligned)
     const int nqv = ((hi - org) >> 2) + 1;
     const int L = r_last + a.tv.taps - r_lo;
     {
         const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
         const int pitch = a.w * B;
         const int chunks = (B * nqv + 63) >> 6;
-        for (int l = (a.dbg & 1) ? L : wave; l < L; l += 4) {  // dbg 1: no staging loads (timing only)
+        for (int l = wave; l < L; l += 4) {
             const int r = clampi(r_lo + l, 0, a.h - 1);
             for (int c = 0; c < chunks; ++c)
                 if (c * 64 + lane < RS) {  // the last chunk stops at the row stride
@@ -1555,8 +1085,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
             hal[gi] = load_taps16(thr + kHmTabW, o0);
         }
     }
-    if (a.dbg & 4) {  // dbg 4: no position set-up (timing only)
-    } else if (tid < XW) {
+    if (tid < XW) {
         int sp, ph;
         sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
         ps[tid] = sp;
@@ -1572,7 +1101,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     }
     __syncthreads();
     // ---- tail fix-up: blocks that stage the image's last row with a row end off the dword grid ----
-    if ((a.w * B) % 4 != 0 && r_lo + L > a.h - 1 && !(a.dbg & 1)) {  // uniform
+    if ((a.w * B) % 4 != 0 && r_lo + L > a.h - 1) {  // uniform
         const int pitch = a.w * B;
         const int chunks = (B * nqv + 63) >> 6;
         for (int l = wave; l < L; l += 4) {
@@ -1588,7 +1117,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
         __syncthreads();
     }
     // ---- vertical pass on the matrix cores, 16-byte column tiles dealt to the waves ----
-    if (!(a.dbg & 2)) {  // dbg 2: no vertical pass, deinterleave or horizontal products (timing only)
+    {
         const int n = lane & 15, kg = lane >> 4;
         hm_v4i bh = hbh, bl = hbl;
         if constexpr (HT == 0) {
@@ -1631,7 +1160,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
     }
     __syncthreads();
     // ---- row-major intermediate -> channel planes, 4 pixels per item ----
-    for (int k = (a.dbg & 2) ? nr : wave; k < nr; k += 4) {
+    for (int k = wave; k < nr; k += 4) {
         const uint32_t *ir = reinterpret_cast<const uint32_t *>(inter + k * a.iw);
         u8 *pl = planes + k * a.row_w;
         for (int q = lane; q < nqv; q += 64) {
@@ -1683,7 +1212,7 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
             acc_h[z] = hm_v4i{0, 0, 0, 0};
             acc_l[z] = hm_v4i{bias.x, bias.y, bias.z, bias.w};
         }
-        for (int ks = 0; ks < ((a.dbg & 2) ? 0 : a.nks); ++ks) {
+        for (int ks = 0; ks < a.nks; ++ks) {
             hm_v4i ah, al;
             if (HT != 0 && ks == 0) {
                 ah = hah[gi];
@@ -1755,547 +1284,6 @@ __global__ void __launch_bounds__(256) k_rmf2(RmArgs a) {
                     if (e + k >= tb && e + k < nb)
                         __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
             }
-        }
-    }
-}
-
-// The 16 bytes of a tap row from byte offset o (any alignment; the row's padding
-// keeps o within it)
-__device__ __forceinline__ hm_v4i load_frag16(const signed char *row, int o) {
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (o & ~3));
-    const int sh = o & 3;
-    const uint4 d = *reinterpret_cast<const uint4 *>(p);
-    const uint32_t e = p[4];
-    hm_v4i r;
-    r[0] = static_cast<int>(__builtin_amdgcn_alignbyte(d.y, d.x, sh));
-    r[1] = static_cast<int>(__builtin_amdgcn_alignbyte(d.z, d.y, sh));
-    r[2] = static_cast<int>(__builtin_amdgcn_alignbyte(d.w, d.z, sh));
-    r[3] = static_cast<int>(__builtin_amdgcn_alignbyte(e, d.w, sh));
-    return r;
-}
-
-// k_rmf4: k_rmf2 with the horizontal products on the INTERLEAVED intermediate bytes,
-// so the channel planes, their deinterleave pass and its barrier, and the output
-// re-interleave are gone.  A horizontal unit is 16 consecutive output bytes of one
-// row x 16 rows: output byte o = B x + c needs intermediate bytes B (s(x) + k) + c,
-// k = 0 .. taps - 1, so its operand row (M = o) holds tap k at K = B (s(x) - org) + c
-// + B k - kb, where kb is the unit's first tap byte rounded down to 8.  The rows come
-// from the stride-B tap table (device_reduce_i8s) at a per-lane byte offset; B (the
-// pixels) is two ds_read_b64 per lane from the row-major intermediate; the result
-// D[4 consecutive output bytes][row] is one output dword per lane.
-template <int B, int HT>
-__global__ void __launch_bounds__(256) k_rmf4(RmArgs a) {
-    constexpr int XW = kRmXW;
-    constexpr int NU = XW * B / 16;  // 16-byte output units per block row set
-    constexpr int UPW = NU / 4;      // units per wave
-    const int RS = a.rsd;
-    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
-    int *ps = reinterpret_cast<int *>(rsm);  // [XW] first tap pixel
-    int *pph = ps + XW;                      // [XW] phase
-    int *hbb = pph + XW;                     // [XW * B] per output byte: 128 * tap sum + 2048
-    int *vso = hbb + XW * B;                 // [kRmRows] vertical: first staged row of each output row
-    int *vph = vso + kRmRows;                // [kRmRows] phase
-    int *vbias = vph + kRmRows;              // [kRmRows] 128 * tap sum + 2048
-    uint32_t *raw = reinterpret_cast<uint32_t *>(vbias + kRmRows);  // [lrows][RS] staged rows
-    u8 *inter = reinterpret_cast<u8 *>(raw);                         // [kRmRows][iw] (pixel - 128), after the vertical pass
-    u8 *tile = inter + kRmRows * a.iw;                               // [kRmRows][XW * B + 4] unaligned output rows
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int xb = t % a.x_blocks;
-    const int rest = t / a.x_blocks;
-    const int yb = rest % a.y_blocks;
-    const int img = rest / a.y_blocks;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int x0 = xb * XW, x_last = min(x0 + XW - 1, a.ow - 1);
-    const int y0 = yb * kRmRows, nr = min(kRmRows, a.oh - y0);
-    int lo, hi, ph0, r_lo, r_last;
-    sep_position(a.th, a.ox0 + x0, &lo, &ph0);
-    sep_position(a.th, a.ox0 + x_last, &hi, &ph0);
-    hi += a.th.taps - 1;
-    sep_position(a.tv, a.oy0 + y0, &r_lo, &ph0);
-    sep_position(a.tv, a.oy0 + y0 + nr - 1, &r_last, &ph0);
-    const int org = lo & ~15;
-    const int nqv = ((hi - org) >> 2) + 1;
-    const int L = r_last + a.tv.taps - r_lo;
-    {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
-        const int pitch = a.w * B;
-        const int chunks = (B * nqv + 63) >> 6;
-        for (int l = wave; l < L; l += 4) {
-            const int r = clampi(r_lo + l, 0, a.h - 1);
-            for (int c = 0; c < chunks; ++c)
-                if (c * 64 + lane < RS)  // the last chunk stops at the row stride
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * RS + c * 64), 4,
-                                                             r * pitch + B * org + 4 * (c * 64 + lane), 0, 0, 0);
-        }
-    }
-    const int n = lane & 15, kg = lane >> 4;
-    hm_v4i hbh = hm_v4i{0, 0, 0, 0}, hbl = hbh;
-    if constexpr (HT & 1) {  // the lane's vertical tap fragments, while the rows are in flight
-        int sv, ph;
-        sep_position(a.tv, a.oy0 + y0 + min(n, nr - 1), &sv, &ph);
-        const signed char *tv = a.tabv + static_cast<size_t>(ph) * 2 * kHmTabW;
-        const int ov = 16 * kg - (sv - r_lo) + kHmTabPad;
-        hbh = load_taps16(tv, ov);
-        hbl = load_taps16(tv + kHmTabW, ov);
-    }
-    // HT 2: also every unit's first-K-step tap fragments (UPW x 8 registers)
-    const int nbytes = (x_last - x0 + 1) * B;  // output bytes of this block's rows
-    hm_v4i fh[HT >= 2 ? UPW : 1], fl[HT >= 2 ? UPW : 1];
-    if constexpr (HT >= 2) {
-#pragma unroll
-        for (int ui = 0; ui < UPW; ++ui) {
-            const int u = wave * UPW + ui;
-            fh[ui] = fl[ui] = hm_v4i{0, 0, 0, 0};
-            if (16 * u >= nbytes) continue;
-            const int xf = (16 * u) / B, cf = 16 * u - xf * B;
-            int sf, sp, pp;
-            sep_position(a.th, a.ox0 + x0 + xf, &sf, &pp);
-            const int kb = (B * (sf - org) + cf) & ~7;
-            const int m = min(16 * u + n, nbytes - 1);
-            const int xm = m / B, cm = m - xm * B;
-            sep_position(a.th, a.ox0 + x0 + xm, &sp, &pp);
-            const int off = kRsTabPad + 16 * kg + kb - (B * (sp - org) + cm);
-            const signed char *tr = a.tabs + static_cast<size_t>(pp) * 2 * kRsTabW;
-            fh[ui] = load_frag16(tr, off);
-            fl[ui] = load_frag16(tr + kRsTabW, off);
-        }
-    }
-    if (tid < XW) {
-        int sp, ph;
-        sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &sp, &ph);
-        ps[tid] = sp;
-        pph[tid] = ph;
-        const int bias = 128 * a.tsum[ph] + 2048;
-#pragma unroll
-        for (int z = 0; z < B; ++z) hbb[B * tid + z] = bias;
-    } else if (tid < XW + kRmRows) {
-        const int k = tid - XW;
-        int sv, ph;
-        sep_position(a.tv, a.oy0 + y0 + min(k, nr - 1), &sv, &ph);
-        vso[k] = sv - r_lo;
-        vph[k] = ph;
-        vbias[k] = 128 * a.tsumv[ph] + 2048;
-    }
-    __syncthreads();
-    // ---- vertical pass on the matrix cores (k_rmf2's), 16-byte column tiles dealt to the waves ----
-    {
-        hm_v4i bh = hbh, bl = hbl;
-        if constexpr ((HT & 1) == 0) {
-            const signed char *tv = a.tabv + static_cast<size_t>(vph[n]) * 2 * kHmTabW;
-            const int ov = 16 * kg - vso[n] + kHmTabPad;
-            bh = load_taps16(tv, ov);
-            bl = load_taps16(tv + kHmTabW, ov);
-        }
-        const int vb = vbias[n];
-        const int nt = (B * (hi - org + 1) + 15) >> 4;
-        const u8 *rawb = reinterpret_cast<const u8 *>(raw);
-        const int r1 = min(16 * kg + (n >> 1), L - 1), r2 = min(16 * kg + 8 + (n >> 1), L - 1);
-        uint32_t res[kRmMaxCt];
-        typedef int v2i_t __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int i = 0; i < kRmMaxCt; ++i) {
-            const int ct = wave + 4 * i;
-            if (ct >= nt) continue;
-            const int cb = 16 * ct + 8 * (n & 1);
-            const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r1 * RS * 4 + cb))));
-            const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r2 * RS * 4 + cb))));
-            const hm_v4i av = hm_v4i{t1.x ^ static_cast<int>(0x80808080u), t1.y ^ static_cast<int>(0x80808080u),
-                                     t2.x ^ static_cast<int>(0x80808080u), t2.y ^ static_cast<int>(0x80808080u)};
-            hm_v4i dh = hm_v4i{0, 0, 0, 0}, dl = hm_v4i{vb, vb, vb, vb};
-            dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
-            dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
-            const uint32_t w = round_pack4((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
-                                           (dh[3] << 6) + dl[3]);
-            res[i] = w ^ 0x80808080u;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < kRmMaxCt; ++i) {
-            const int ct = wave + 4 * i;
-            if (ct >= nt) continue;
-            *reinterpret_cast<uint32_t *>(inter + n * a.iw + 16 * ct + 4 * kg) = res[i];
-        }
-    }
-    __syncthreads();
-    // ---- COPY edge of the horizontal pass: pixels outside the image repeat its edge ----
-    if (lo < 0 || hi >= a.w) {
-        const int np = hi - org + 1;
-        for (int i = tid; i < nr * np; i += 256) {
-            const int k = i / np, pq = i - k * np;
-            const int p = org + pq;
-            if (p >= 0 && p < a.w) continue;
-            const int src = clampi(p, 0, a.w - 1) - org;
-#pragma unroll
-            for (int z = 0; z < B; ++z) inter[k * a.iw + B * pq + z] = inter[k * a.iw + B * src + z];
-        }
-        __syncthreads();
-    }
-    // ---- horizontal pass: 16-byte output units on the interleaved intermediate ----
-    u8 *ob = a.out + img * a.out_img;
-    const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
-    typedef int v2i_t __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int ui = 0; ui < UPW; ++ui) {
-        const int u = wave * UPW + ui;
-        if (16 * u >= nbytes) break;  // uniform
-        // the unit's first tap byte (output byte 16 u: pixel (16 u) / B, channel (16 u) % B), down to 8
-        const int xf = (16 * u) / B, cf = 16 * u - xf * B;
-        const int kb = (B * (__builtin_amdgcn_readfirstlane(ps[xf]) - org) + cf) & ~7;
-        // this lane's operand row: output byte m = 16 u + n
-        const int m = min(16 * u + n, nbytes - 1);
-        const int xm = m / B, cm = m - xm * B;
-        const int off = kRsTabPad + 16 * kg + kb - (B * (ps[xm] - org) + cm);
-        const signed char *tr = a.tabs + static_cast<size_t>(pph[xm]) * 2 * kRsTabW;
-        const int4 bias = *reinterpret_cast<const int4 *>(hbb + 16 * u + 4 * kg);
-        hm_v4i acc_h = hm_v4i{0, 0, 0, 0}, acc_l = hm_v4i{bias.x, bias.y, bias.z, bias.w};
-        for (int ks = 0; ks < a.nks; ++ks) {
-            hm_v4i ah, al;
-            if (HT >= 2 && ks == 0) {
-                ah = fh[HT >= 2 ? ui : 0];
-                al = fl[HT >= 2 ? ui : 0];
-            } else {
-                ah = load_frag16(tr, off + 64 * ks);
-                al = load_frag16(tr + kRsTabW, off + 64 * ks);
-            }
-            const u8 *src = inter + n * a.iw + kb + 64 * ks + 16 * kg;
-            const v2i_t b0 = *reinterpret_cast<const v2i_t *>(src);
-            const v2i_t b1 = *reinterpret_cast<const v2i_t *>(src + 8);
-            const hm_v4i bv = hm_v4i{b0.x, b0.y, b1.x, b1.y};
-            acc_h = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bv, acc_h, 0, 0, 0);
-            acc_l = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bv, acc_l, 0, 0, 0);
-        }
-        const uint32_t wv = round_pack4((acc_h[0] << 6) + acc_l[0], (acc_h[1] << 6) + acc_l[1],
-                                        (acc_h[2] << 6) + acc_l[2], (acc_h[3] << 6) + acc_l[3]);
-        const int e = 16 * u + 4 * kg;  // first output byte of this lane in the block's row
-        if (n >= nr || e >= nbytes) continue;
-        if (a.direct && e + 4 <= nbytes) {
-            __builtin_amdgcn_raw_buffer_store_b32(wv, os, ((y0 + n) * a.ow + x0) * B + e, 0, 0);
-        } else {
-            *reinterpret_cast<uint32_t *>(tile + n * (XW * B + 4) + e) = wv;
-        }
-    }
-    __syncthreads();
-    // ---- rows through the tile: unaligned output rows, and the partial dword at a row end ----
-    const int tb = a.direct ? (nbytes & ~3) : 0;  // bytes already stored
-    for (int r = wave; r < nr && tb < nbytes; r += 4) {
-        const u8 *tr = tile + r * (XW * B + 4);
-        const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
-        const int qo0 = ((y0 + r) * a.ow + x0) * B + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
-        const int d0 = qo0 >> 2, nd = ((qo0 + nbytes + 3) >> 2) - d0;
-        const int sh = (4 - (qo0 & 3)) & 3;
-        const int bias0 = static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
-        for (int i = lane; i < nd; i += 64) {
-            const int e = 4 * (d0 + i) - qo0;
-            if (e + 4 <= tb) continue;
-            if (e >= tb && e + 4 <= nbytes) {
-                const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
-                __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i) - bias0, 0, 0);
-            } else {
-                for (int k = 0; k < 4; ++k)
-                    if (e + k >= tb && e + k < nbytes)
-                        __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
-            }
-        }
-    }
-}
-
-// LDS-only workgroup barrier: orders LDS accesses without draining outstanding
-// global loads (the next tile's rows stay in flight across it)
-__device__ __forceinline__ void lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// k_rmf3: k_rmf2 as a persistent kernel.  The batch's 16-row x 128-pixel tiles,
-// column-major (a column's tiles top to bottom, then the next column), are split into
-// one equal run per resident workgroup; the input rows of the run's next tile are
-// loaded into registers (kRmPf dwords per lane) while the current one computes, then
-// written to LDS, so a tile's HBM latency hides behind the previous tile's work
-// instead of stalling the workgroup, and a column's horizontal taps load once.
-constexpr int kRmPf = 27;  // prefetch dwords per lane: staged rows (<= 36) / 4 waves x 3 chunks
-template <int B, int RS>
-__global__ void __launch_bounds__(256) k_rmf3(RmArgs a) {
-    constexpr int XW = kRmXW, GPW = XW / 64;
-    extern __shared__ __attribute__((aligned(16))) uint32_t rsm[];
-    int *ps = reinterpret_cast<int *>(rsm);
-    int *pph = ps + XW;
-    int *pbias = pph + XW;
-    uint32_t *junk = reinterpret_cast<uint32_t *>(pbias + XW);  // [64] sink of the unused prefetch slots
-    uint32_t *raw = junk + 64;                                  // [lrows][RS]
-    u8 *inter = reinterpret_cast<u8 *>(raw);
-    u8 *planes = inter + kRmRows * a.iw + 64;
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring runs on one XCD's L2
-    const int tt0 = static_cast<int>(static_cast<long long>(t) * a.tiles / gridDim.x);
-    const int tt1 = static_cast<int>(static_cast<long long>(t + 1) * a.tiles / gridDim.x);
-    if (tt0 >= tt1) return;  // uniform, before any barrier
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // tile tt: column (image, 128-pixel block) and 16-row block
-    auto column_of = [&](int tt, int *img, int *x0, int *x_last, int *lo, int *hi) {
-        const int col = tt / a.y_blocks;
-        *img = col / a.x_blocks;
-        *x0 = (col - *img * a.x_blocks) * XW;
-        *x_last = min(*x0 + XW - 1, a.ow - 1);
-        int ph;
-        sep_position(a.th, a.ox0 + *x0, lo, &ph);
-        sep_position(a.th, a.ox0 + *x_last, hi, &ph);
-        *hi += a.th.taps - 1;
-    };
-    auto rows_of = [&](int tt, int *y0, int *nr, int *r_lo, int *L) {
-        *y0 = (tt % a.y_blocks) * kRmRows;
-        *nr = min(kRmRows, a.oh - *y0);
-        int r_last, ph;
-        sep_position(a.tv, a.oy0 + *y0, r_lo, &ph);
-        sep_position(a.tv, a.oy0 + *y0 + *nr - 1, &r_last, &ph);
-        *L = r_last + a.tv.taps - *r_lo;
-    };
-    // rows of tile tt into registers: wave w takes staged rows w, w + 4, ..., lane one dword
-    // per 256-byte chunk.  Every slot issues a load (rows past the tile repeat its last row,
-    // an L2 hit; past the run, the run's last tile again), so the load count is static and
-    // later waits count past them; the row offset is uniform (soffset).
-    uint32_t pf[kRmPf];
-    auto fetch = [&](int tt) {
-        const int tc = min(tt, tt1 - 1);
-        int img, x0, x_last, lo, hi, y0, nr, rl, Lf;
-        column_of(tc, &img, &x0, &x_last, &lo, &hi);
-        rows_of(tc, &y0, &nr, &rl, &Lf);
-        const __amdgpu_buffer_rsrc_t rsi = image_rsrc(a.in + img * a.in_img, a.in_img);
-        const int vo = B * (lo & ~15) + 4 * lane;
-#pragma unroll
-        for (int i = 0; i < kRmPf; ++i) {
-            const int l = wave + 4 * (i / 3), c = i % 3;
-            const int r = __builtin_amdgcn_readfirstlane(clampi(rl + min(l, Lf - 1), 0, a.h - 1));
-            pf[i] = __builtin_amdgcn_raw_buffer_load_b32(rsi, vo + 256 * c, r * a.w * B, 0);
-        }
-    };
-    hm_v4i hah[GPW], hal[GPW];  // the column's horizontal taps (first 64-pixel step), per lane
-    int reg_col = -1, lds_col = -1;
-    // iteration tt0 - 1 only issues the first fetch: one fetch site, one set of registers
-    for (int tt = tt0 - 1; tt < tt1; ++tt) {
-        // lane-derived LDS addresses recomputed per tile (an opaque copy of the lane id) rather
-        // than hoisted out of the loop into registers the prefetch needs
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        const bool live = tt >= tt0;
-        const int tc = max(tt, tt0), col = tc / a.y_blocks;
-        int img, x0, x_last, lo, hi, y0, nr, r_lo, L;
-        column_of(tc, &img, &x0, &x_last, &lo, &hi);
-        rows_of(tc, &y0, &nr, &r_lo, &L);
-        const int org = lo & ~15;
-        const int nqv = ((hi - org) >> 2) + 1;
-        const int n = ln & 15, kg = ln >> 4;
-        // this tile's global reads (vertical taps, a new column's horizontal taps) go before the
-        // next fetch, so their waits do not cover it
-        int sv, vph;
-        sep_position(a.tv, a.oy0 + y0 + min(n, nr - 1), &sv, &vph);
-        const signed char *tv = a.tabv + static_cast<size_t>(vph) * 2 * kHmTabW;
-        const int ov = 16 * kg - (sv - r_lo) + kHmTabPad;
-        const hm_v4i bh = load_taps16(tv, ov), bl = load_taps16(tv + kHmTabW, ov);
-        const int vb = 128 * a.tsumv[vph] + 2048;
-        if (col != reg_col) {
-            reg_col = col;
-#pragma unroll
-            for (int gi = 0; gi < GPW; ++gi) {
-                const int g = wave * GPW + gi, p = min(16 * g + n, x_last - x0);
-                int s16, sp, ph;
-                sep_position(a.th, a.ox0 + min(x0 + 16 * g, x_last), &s16, &ph);
-                sep_position(a.th, a.ox0 + x0 + p, &sp, &ph);
-                const int o0 = (s16 & ~15) + 16 * kg - sp + kHmTabPad;
-                const signed char *thr = a.tab + static_cast<size_t>(ph) * 2 * kHmTabW;
-                hah[gi] = load_taps16(thr, o0);
-                hal[gi] = load_taps16(thr + kHmTabW, o0);
-            }
-        }
-        int hps = 0, hph = 0, hbias = 0;
-        const bool new_lds_col = live && col != lds_col;  // uniform
-        if (new_lds_col && tid < XW) {
-            sep_position(a.th, a.ox0 + min(x0 + tid, x_last), &hps, &hph);
-            hbias = 128 * a.tsum[hph] + 2048;
-        }
-        lds_sync();  // the previous tile is done with every LDS region
-        if (live) {
-#pragma unroll
-            for (int i = 0; i < kRmPf; ++i) {
-                const int l = wave + 4 * (i / 3), c = i % 3;
-                *(l < L ? raw + l * RS + c * 64 + ln : junk + ln) = pf[i];
-            }
-            if (new_lds_col) {
-                lds_col = col;
-                if (tid < XW) {
-                    ps[tid] = hps;
-                    pph[tid] = hph;
-                    pbias[tid] = hbias;
-                }
-            }
-        }
-        fetch(tt + 1);  // in flight across this tile's LDS-only barriers
-        if (!live) continue;
-        lds_sync();
-        {
-            // ---- vertical pass on the matrix cores, 16-byte column tiles dealt to the waves ----
-            {
-                const int nt = (B * (hi - org + 1) + 15) >> 4;
-                const u8 *rawb = reinterpret_cast<const u8 *>(raw);
-                const int r1 = min(16 * kg + (n >> 1), L - 1), r2 = min(16 * kg + 8 + (n >> 1), L - 1);
-                uint32_t res[kRmMaxCt];  // this wave's tiles, written after every wave has read the staged rows
-                typedef int v2i_t __attribute__((ext_vector_type(2)));
-        #pragma unroll
-                for (int i = 0; i < kRmMaxCt; ++i) {
-                    const int ct = wave + 4 * i;
-                    if (ct >= nt) continue;  // uniform; no break: results of skipped tiles stay undefined, no copies
-                    const int cb = 16 * ct + 8 * (n & 1);  // the tile's 16 staged rows of this ln's byte column
-                    const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                        (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r1 * RS * 4 + cb))));
-                    const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                        (__attribute__((address_space(3))) v2i_t *)(to_lds(const_cast<u8 *>(rawb + r2 * RS * 4 + cb))));
-                    const hm_v4i av = hm_v4i{t1.x ^ static_cast<int>(0x80808080u), t1.y ^ static_cast<int>(0x80808080u),
-                                             t2.x ^ static_cast<int>(0x80808080u), t2.y ^ static_cast<int>(0x80808080u)};
-                    hm_v4i dh = hm_v4i{0, 0, 0, 0}, dl = hm_v4i{vb, vb, vb, vb};
-                    dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
-                    dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
-                    const uint32_t w = round_pack4((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
-                                                   (dh[3] << 6) + dl[3]);
-                    res[i] = w ^ 0x80808080u;
-                    __builtin_amdgcn_sched_barrier(0);  // one column tile at a time: registers for the prefetch
-                }
-                lds_sync();
-        #pragma unroll
-                for (int i = 0; i < kRmMaxCt; ++i) {
-                    const int ct = wave + 4 * i;
-                    if (ct >= nt) continue;
-                    *reinterpret_cast<uint32_t *>(inter + n * a.iw + 16 * ct + 4 * kg) = res[i];
-                }
-            }
-            lds_sync();
-            // ---- row-major intermediate -> channel planes, 4 pixels per item ----
-            for (int k = wave; k < nr; k += 4) {
-                const uint32_t *ir = reinterpret_cast<const uint32_t *>(inter + k * a.iw);
-                u8 *pl = planes + k * a.row_w;
-                for (int q = ln; q < nqv; q += 64) {
-                    uint32_t xw[4], pw[4];
-        #pragma unroll
-                    for (int d = 0; d < B; ++d) xw[d] = ir[B * q + d];
-                    if (B == 3) {
-                        pw[0] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c060300u), 0x05020100u);
-                        pw[1] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c070401u), 0x06020100u);
-                        pw[2] = __builtin_amdgcn_perm(xw[2], __builtin_amdgcn_perm(xw[1], xw[0], 0x0c0c0502u), 0x07040100u);
-                    } else {
-                        transpose4x4(xw[0], xw[1], xw[2], xw[3], pw);
-                    }
-        #pragma unroll
-                    for (int z = 0; z < B; ++z) reinterpret_cast<uint32_t *>(pl + z * a.plane_w)[q] = pw[z];
-                }
-            }
-            lds_sync();
-            // ---- COPY edge of the horizontal pass: pixels outside the image repeat its edge ----
-            if (lo < 0 || hi >= a.w) {
-                for (int i = tid; i < nr * (hi - org + 1); i += 256) {
-                    const int k = i / (hi - org + 1), pq = i - k * (hi - org + 1);
-                    const int p = org + pq;
-                    if (p >= 0 && p < a.w) continue;
-                    const int src = clampi(p, 0, a.w - 1) - org;
-        #pragma unroll
-                    for (int z = 0; z < B; ++z) planes[k * a.row_w + z * a.plane_w + pq] = planes[k * a.row_w + z * a.plane_w + src];
-                }
-                lds_sync();
-            }
-            // ---- horizontal pass on the matrix cores (k_hmfma's group loop) ----
-            const int n = ln & 15, kg = ln >> 4;
-            u8 *ob = a.out + img * a.out_img;
-            u8 *tile = inter;  // output tile [kRmRows][XW * 3 + 4] over the intermediate (dead after the deinterleave)
-            const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
-            lds_sync();
-        #pragma unroll
-            for (int gi = 0; gi < GPW; ++gi) {
-                const int g = wave * GPW + gi;
-                if (x0 + 16 * g > x_last) break;
-                const int qb = (__builtin_amdgcn_readfirstlane(ps[16 * g]) & ~15) - org;
-                const int p = min(16 * g + n, x_last - x0);
-                const int o0 = qb + 16 * kg - (ps[p] - org) + kHmTabPad;
-                const signed char *thr = a.tab + static_cast<size_t>(pph[p]) * 2 * kHmTabW;
-                const int4 bias = *reinterpret_cast<const int4 *>(pbias + 16 * g + 4 * kg);
-                // step 0 from the column's registers; later steps (wide shrinks) load their taps,
-                // and only there do waits (which also cover the prefetch) appear
-                hm_v4i acc_h[B], acc_l[B];
-        #pragma unroll
-                for (int z = 0; z < B; ++z) {
-                    const hm_v4i bz = *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 16 * kg);
-                    acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(hah[gi], bz, hm_v4i{0, 0, 0, 0}, 0, 0, 0);
-                    acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(hal[gi], bz, hm_v4i{bias.x, bias.y, bias.z, bias.w}, 0, 0, 0);
-                }
-                for (int ks = 1; ks < a.nks; ++ks) {
-                    const hm_v4i ah = load_taps16(thr, o0 + 64 * ks);
-                    const hm_v4i al = load_taps16(thr + kHmTabW, o0 + 64 * ks);
-        #pragma unroll
-                    for (int z = 0; z < B; ++z) {
-                        const hm_v4i bz =
-                            *reinterpret_cast<const hm_v4i *>(planes + n * a.row_w + z * a.plane_w + qb + 64 * ks + 16 * kg);
-                        acc_h[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ah, bz, acc_h[z], 0, 0, 0);
-                        acc_l[z] = __builtin_amdgcn_mfma_i32_16x16x64_i8(al, bz, acc_l[z], 0, 0, 0);
-                    }
-                }
-                uint32_t wz[4];
-        #pragma unroll
-                for (int z = 0; z < B; ++z)
-                    wz[z] = round_pack4((acc_h[z][0] << 6) + acc_l[z][0], (acc_h[z][1] << 6) + acc_l[z][1],
-                                        (acc_h[z][2] << 6) + acc_l[z][2], (acc_h[z][3] << 6) + acc_l[z][3]);
-                const int x = x0 + 16 * g + 4 * kg;
-                if (n >= nr || x > x_last) continue;
-                uint32_t wo[4];  // the 4 pixels interleaved: B dwords
-                if (B == 3) {
-                    wo[0] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x010c0400u), 0x03040100u);
-                    wo[1] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x06020c05u), 0x03020500u);
-                    wo[2] = __builtin_amdgcn_perm(wz[2], __builtin_amdgcn_perm(wz[1], wz[0], 0x0c07030cu), 0x07020106u);
-                } else {
-                    transpose4x4(wz[0], wz[1], wz[2], wz[3], wo);
-                }
-                if (a.direct && x + 3 <= x_last) {  // dword-aligned output rows: the ln's 4 pixels in one store
-                    const int qo = ((y0 + n) * a.ow + x) * B;
-                    if (B == 3) {
-                        typedef int v3i_t __attribute__((ext_vector_type(3)));
-                        __builtin_amdgcn_raw_buffer_store_b96(
-                            v3i_t{static_cast<int>(wo[0]), static_cast<int>(wo[1]), static_cast<int>(wo[2])}, os, qo, 0, 0);
-                    } else {
-                        __builtin_amdgcn_raw_buffer_store_b128(hm_v4i{static_cast<int>(wo[0]), static_cast<int>(wo[1]),
-                                                                      static_cast<int>(wo[2]), static_cast<int>(wo[3])},
-                                                               os, qo, 0, 0);
-                    }
-                    continue;
-                }
-                uint32_t *tq = reinterpret_cast<uint32_t *>(tile + n * (XW * B + 4) + (x - x0) * B);
-        #pragma unroll
-                for (int d = 0; d < B; ++d) tq[d] = wo[d];
-            }
-            lds_sync();
-            // ---- each tile row to its output row as whole dwords at the row's own alignment ----
-            // (direct mode: only the partial last group of the row's last block went through the tile)
-            const int nb = (x_last - x0 + 1) * B;
-            const int tb = a.direct ? ((x_last - x0 + 1) & ~3) * B : 0;  // tile bytes already stored
-            for (int r = wave; r < nr && tb < nb; r += 4) {
-                const u8 *tr = tile + r * (XW * B + 4);
-                const uint32_t *tw = reinterpret_cast<const uint32_t *>(tr);
-                const int qo0 = ((y0 + r) * a.ow + x0) * B + static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
-                const int d0 = qo0 >> 2, nd = ((qo0 + nb + 3) >> 2) - d0;
-                const int sh = (4 - (qo0 & 3)) & 3;
-                const int bias0 = static_cast<int>(reinterpret_cast<uintptr_t>(ob) & 3u);
-                for (int i = ln; i < nd; i += 64) {
-                    const int e = 4 * (d0 + i) - qo0;
-                    if (e + 4 <= tb) continue;
-                    if (e >= tb && e + 4 <= nb) {
-                        const uint32_t w = sh ? __builtin_amdgcn_alignbyte(tw[(e >> 2) + 1], tw[e >> 2], e & 3) : tw[e >> 2];
-                        __builtin_amdgcn_raw_buffer_store_b32(w, os, 4 * (d0 + i) - bias0, 0, 0);
-                    } else {
-                        for (int k = 0; k < 4; ++k)
-                            if (e + k >= tb && e + k < nb)
-                                __builtin_amdgcn_raw_buffer_store_b8(tr[e + k], os, 4 * (d0 + i) + k - bias0, 0, 0);
-                    }
-                }
-            }
-
         }
     }
 }
@@ -2494,171 +1482,6 @@ __global__ void __launch_bounds__(256) k_reduce_fused(FusedArgs a) {
     }
 }
 
-// ===========================================================================
-// k_reduce2d<B>: reducev -> reduceh in one launch for any shrink pair, sized for
-// large images.  A block = up to 256 output pixels (one per lane) x kr output
-// rows of one image.  The input rows it needs over the block's column span are
-// DMA'd to LDS (dwords from each row's aligned-down start, any alignment); the
-// vertical pass runs on dword lanes (channel agnostic, int16 v_dot2 on byte
-// pairs, integer (sum + 2048) >> 12) into kr rounded uchar rows kept in LDS as
-// raw bytes; the horizontal pass reads each pixel's bytes back with
-// v_alignbyte and sums its <= 16 taps with v_dot2.  The intermediate never
-// reaches HBM (libvips materialises it; the values are the same).
-// ===========================================================================
-constexpr int kR2MaxTaps = 16;   // horizontal taps held per lane
-
-struct R2DArgs {
-    const u8 *in;
-    u8 *out;
-    int w, h, in_pitch;
-    long long in_img, out_img;
-    int ox0, oy0, ow, oh;        // output window (op-output coordinates) and its size
-    int bw, kr;                  // output pixels / rows per block
-    int x_blocks, y_blocks;
-    int raw_stride;              // LDS dwords per staged input row (multiple of 64)
-    int mid_stride;              // LDS dwords per intermediate row
-    int lrows;                   // staged input rows capacity (+1 for the odd tap pair)
-    SepTaps tv, thz;
-};
-
-template <int B>
-__global__ void __launch_bounds__(256) k_reduce2d(R2DArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t r2sm[];
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int xb = t % a.x_blocks;
-    const int rest = t / a.x_blocks;
-    const int yb = rest % a.y_blocks;
-    const int img = rest / a.y_blocks;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int tv = a.tv.taps, thz = a.thz.taps;
-    const int tp2 = (tv + 1) >> 1;
-    const int x0 = xb * a.bw, y0 = yb * a.kr;
-    const int nx = min(a.bw, a.ow - x0), ny = min(a.kr, a.oh - y0);
-    int lo, hi, r_lo, r_last, ph;
-    sep_position(a.thz, a.ox0 + x0, &lo, &ph);
-    sep_position(a.thz, a.ox0 + x0 + nx - 1, &hi, &ph);
-    hi += thz - 1;
-    sep_position(a.tv, a.oy0 + y0, &r_lo, &ph);
-    sep_position(a.tv, a.oy0 + y0 + ny - 1, &r_last, &ph);
-    const int L = r_last + tv - r_lo;
-    const int cl = max(lo, 0), ch = min(hi, a.w - 1);   // intermediate columns actually computed
-    const int ncol = ch - cl + 1;
-    const int nd = (B * ncol + 3) >> 2;                 // intermediate dwords per row
-    uint32_t *raw = r2sm;                                // lrows x raw_stride
-    uint32_t *mid = raw + a.lrows * a.raw_stride;        // kr x mid_stride
-    uint32_t *cpv = mid + a.kr * a.mid_stride;           // kr x tp2 packed int16 tap pairs
-    int *vso = reinterpret_cast<int *>(cpv + a.kr * tp2);  // kr start rows
-    int *rsk = vso + a.kr;                                 // lrows byte skews
-    // ---- DMA the input rows: dwords from each row's aligned-down start ----
-    int delta = 0;
-    const u8 *src = a.in + img * a.in_img;
-    const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, &delta);
-    const int ndl = nd + 1;                              // + the dword a skewed row spills into
-    const int chunks = (ndl + 63) >> 6;
-    {
-        int l = 0, q = wave;
-        while (q >= chunks) q -= chunks, ++l;
-        while (l < L) {
-            const int r = clampi(r_lo + l, 0, a.h - 1);
-            const int a4 = static_cast<int>(delta + static_cast<long long>(r) * a.in_pitch + B * cl) & ~3;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, to_lds(raw + l * a.raw_stride + q * 64), 4,
-                                                     4 * (q * 64 + lane), a4, 0, 0);
-            q += 4;
-            while (q >= chunks) q -= chunks, ++l;
-        }
-    }
-    for (int i = tid; i < L + 1; i += 256) {
-        const int r = clampi(r_lo + min(i, L - 1), 0, a.h - 1);
-        rsk[i] = static_cast<int>(delta + static_cast<long long>(r) * a.in_pitch + B * cl) & 3;
-    }
-    for (int i = tid; i < ny * tp2; i += 256) {
-        const int k = i / tp2, m = i - k * tp2;
-        int s2;
-        sep_position(a.tv, a.oy0 + y0 + k, &s2, &ph);
-        const float *c = a.tv.tab + ph * tv;
-        cpv[i] = pack_pair(c[2 * m], 2 * m + 1 < tv ? c[2 * m + 1] : 0.f);
-    }
-    if (tid < ny) {
-        int s2;
-        sep_position(a.tv, a.oy0 + y0 + tid, &s2, &ph);
-        vso[tid] = s2 - r_lo;
-    }
-    // this lane's horizontal taps (int16 pairs) and the byte offsets of its pixels
-    const int xi = tid;
-    int xs = 0, xph = 0;
-    sep_position(a.thz, a.ox0 + x0 + min(xi, nx - 1), &xs, &xph);
-    uint32_t cp[kR2MaxTaps / 2];
-    int boff[kR2MaxTaps];
-    {
-        const float *c = a.thz.tab + xph * thz;
-#pragma unroll
-        for (int m = 0; m < kR2MaxTaps / 2; ++m)
-            cp[m] = pack_pair(2 * m < thz ? c[2 * m] : 0.f, 2 * m + 1 < thz ? c[2 * m + 1] : 0.f);
-#pragma unroll
-        for (int i = 0; i < kR2MaxTaps; ++i) boff[i] = B * (clampi(xs + min(i, thz - 1), 0, a.w - 1) - cl);
-    }
-    __syncthreads();
-    // ---- vertical pass: ny intermediate rows x nd dwords ----
-    for (int k = 0; k < ny; ++k) {
-        const int s0 = vso[k];
-        const uint32_t *ck = cpv + k * tp2;
-        for (int d = tid; d < nd; d += 256) {
-            int acc[4] = {0, 0, 0, 0};
-            for (int m = 0; m < tp2; ++m) {
-                const int l0 = s0 + 2 * m;
-                const uint32_t *p0 = raw + l0 * a.raw_stride + d;
-                const uint32_t v0 = __builtin_amdgcn_alignbyte(p0[1], p0[0], rsk[l0]);
-                const uint32_t v1 = __builtin_amdgcn_alignbyte(p0[a.raw_stride + 1], p0[a.raw_stride], rsk[l0 + 1]);
-                const uint32_t cw = ck[m];
-#pragma unroll
-                for (int z = 0; z < 4; ++z) acc[z] = dot2_byte(v0, v1, z, cw, acc[z]);
-            }
-            uint32_t o = 0;
-#pragma unroll
-            for (int z = 0; z < 4; ++z) o |= fixed_round_i(acc[z]) << (8 * z);
-            mid[k * a.mid_stride + d] = o;
-        }
-    }
-    __syncthreads();
-    // ---- horizontal pass: lane = output column x0 + xi ----
-    if (xi >= nx) return;
-    u8 *q = a.out + img * a.out_img + (static_cast<long long>(y0) * a.ow + x0 + xi) * B;
-    for (int k = 0; k < ny; ++k) {
-        const uint32_t *mr = mid + k * a.mid_stride;
-        int acc[B];
-#pragma unroll
-        for (int z = 0; z < B; ++z) acc[z] = 0;
-#pragma unroll
-        for (int m = 0; m < kR2MaxTaps / 2; ++m) {
-            if (2 * m < thz) {
-                uint32_t v[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int bo = boff[2 * m + u];
-                    if (B == 4) {
-                        v[u] = mr[bo >> 2];
-                    } else {
-                        v[u] = __builtin_amdgcn_alignbyte(mr[(bo >> 2) + 1], mr[bo >> 2], bo & 3);
-                    }
-                }
-#pragma unroll
-                for (int z = 0; z < B; ++z) acc[z] = dot2_byte(v[0], v[1], z, cp[m], acc[z]);
-            }
-        }
-        u8 *p = q + static_cast<long long>(k) * a.ow * B;
-        if (B == 4 && (reinterpret_cast<uintptr_t>(p) & 3u) == 0) {
-            uint32_t o = 0;
-#pragma unroll
-            for (int z = 0; z < B; ++z) o |= fixed_round_i(acc[z]) << (8 * z);
-            *reinterpret_cast<uint32_t *>(p) = o;
-        } else {
-#pragma unroll
-            for (int z = 0; z < B; ++z) p[z] = static_cast<u8>(fixed_round_i(acc[z]));
-        }
-    }
-}
-
 bool aligned4(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
 
 SepTaps make_taps(const SepSpec &s) {
@@ -2670,9 +1493,9 @@ SepTaps make_taps(const SepSpec &s) {
     t.shrink = s.shrink;
     t.rounding = static_cast<float>((s.scale + 1) / 2);
     t.inv_scale = s.scale > 0 ? 1.0f / s.scale : 1.0f;
-    const char *e = std::getenv("MIPX_SEP_DOT");
+    const char *e = tune_env("MIPX_SEP_DOT");
     t.dot = !(e && *e == '0');
-    const char *eq = std::getenv("MIPX_SEP_TQ");
+    const char *eq = tune_env("MIPX_SEP_TQ");
     t.tq = !(eq && *eq == '0') && s.taps >= 7;  // 3-tap masks lose to the transpose (v14/ab_conv_quad_transpose.log)
     return t;
 }
@@ -2708,7 +1531,7 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     a.col_blocks = (a.row_bytes + 1023) / 1024;
     // staged input rows per block (1 KiB each); MIPX_VP_ROWS overrides for A/B runs
-    const char *erb = std::getenv("MIPX_VP_ROWS");
+    const char *erb = tune_env("MIPX_VP_ROWS");
     // 24 rows measured best at 9-17 taps (v12_vpass_ab.log, v14/ab_vpass_rows_blur.log); taller
     // masks need room for several output rows per block (25 taps: 40 rows 2.6 vs 1.7 TB/s,
     // v14/ab_vpass_budget.log)
@@ -2716,13 +1539,6 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     constexpr int kRowMax = 60;
     int kr = taps >= kRowBudget ? 1 : static_cast<int>(std::floor((kRowBudget - taps - 1) / s)) + 1;
     kr = std::max(1, std::min({kr, 32, a.oh}));
-    const char *esh = std::getenv("MIPX_VP_SHARE");
-    // A/B variant, off by default: 2-15% slower than per-row pairs on the op_survey shapes
-    // (profiles/r02/vp_share_ab.jsonl) -- coefficient reads and coverage branches cost what
-    // the shared perms save
-    a.tp.share = spec.mode == kSepReduce && a.tp.dot && esh && *esh == '1';
-    if (a.tp.share) kr = std::min(kr, kShareRows);
-    a.np = static_cast<int>(std::ceil((kr - 1) * s)) / 2 + 1 + taps / 2 + 1;
     auto rows_for = [&](int k) {  // conv: taps read in 4s
         return static_cast<int>(std::ceil((k - 1) * s)) + taps + 2 + (spec.mode == kSepConv ? 2 : 0);
     };
@@ -2732,8 +1548,7 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     a.kr_blocks = (a.oh + kr - 1) / kr;
     const dim3 blk(256);
     const size_t lds = static_cast<size_t>(a.lrows) * kVStride * 4 + static_cast<size_t>(kr) * taps * 4 + kr * 4 +
-                       static_cast<size_t>(std::max({(taps + 3) / 4 + 4 * ((taps + 6) / 4), kr * std::max((taps + 1) / 2, kVpPairs),
-                                                     a.tp.share ? a.np * kShareRows : 0}) + 4) * 4;
+                       static_cast<size_t>(std::max({(taps + 3) / 4 + 4 * ((taps + 6) / 4), kr * std::max((taps + 1) / 2, kVpPairs)}) + 4) * 4;
     if (a.lrows > kRowMax || lds > 64 * 1024) {  // very tall masks: gather through L1
         const dim3 grid((a.row_bytes + 1023) / 1024, a.oh, n);
         if (spec.mode == kSepReduce) hipLaunchKernelGGL(k_vpass_gather<kSepReduce>, grid, blk, 0, st, a);
@@ -2745,16 +1560,15 @@ int vpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     const uintptr_t ip = reinterpret_cast<uintptr_t>(in);
     bool al16 = (ip % 16) == 0 && (a.in_pitch % 16) == 0 && (a.in_base % 16) == 0 && (a.in_img % 16) == 0;
     bool al4 = (ip % 4) == 0 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0;
-    const char *edm = std::getenv("MIPX_VP_DMA");  // A/B: cap the DMA width (16 / 4 / 0)
+    const char *edm = tune_env("MIPX_VP_DMA");  // A/B: cap the DMA width (16 / 4 / 0)
     if (edm && *edm) {
         const int cap = std::atoi(edm);
         al16 = al16 && cap >= 16;
         al4 = al4 && cap >= 4;
     }
-    if (!al4) a.tp.share = 0;  // byte-shifted (DMA 0) rows keep the per-row path
-    const char *evf = std::getenv("MIPX_VP_FAST");  // A/B: 0 keeps k_vpass's generic reduce loop
+    const char *evf = tune_env("MIPX_VP_FAST");  // A/B: 0 keeps k_vpass's generic reduce loop
     const int tp2 = (taps + 1) / 2;
-    const bool vfast = spec.mode == kSepReduce && a.tp.dot && !a.tp.share && !(evf && *evf == '0') &&
+    const bool vfast = spec.mode == kSepReduce && a.tp.dot && !(evf && *evf == '0') &&
                        tp2 <= kVpPairs && a.row_bytes % 4 == 0 && a.out_img % 4 == 0 &&
                        reinterpret_cast<uintptr_t>(out) % 4 == 0 && a.out_img < 0x7fffffffLL;
     const dim3 grid(static_cast<unsigned>(blocks));
@@ -2806,16 +1620,16 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     if (spec.mode != kSepReduce) a.ntab += 4 * ((a.tp.taps + 6) / 4);  // conv: packed phase-shifted tap sets
     const double s = a.tp.phased ? spec.shrink : 1.0;
     a.span_max = (static_cast<int>(std::ceil(255 * s)) + a.tp.taps + 2 + 64 + 3) & ~3;  // 16-byte rows
-    const char *erp = std::getenv("MIPX_HP_REPACK");
+    const char *erp = tune_env("MIPX_HP_REPACK");
     a.repack4 = !(erp && *erp == '0');
-    const char *ep3 = std::getenv("MIPX_HP_PACK3");
+    const char *ep3 = tune_env("MIPX_HP_PACK3");
     // A/B (profiles/r01/v18/pack3_ab.jsonl): packed stores win 7% on reduceh / 2.4 and
     // lose 3% on / 1.6 and on the two-pass blur, so they are on for shrinks >= 2 only
     a.pack3 = ep3 && *ep3 ? *ep3 != '0' : (spec.mode == kSepReduce && spec.shrink >= 2.0);
     a.raw_max = (a.span_max * b + 8 + 3) / 4 + 64;
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     const bool dw = b == 4 && (a.in_pitch % 4) == 0 && (a.in_base % 4) == 0 && (a.in_img % 4) == 0 && aligned4(in);
-    const char *ehd = std::getenv("MIPX_HP_DMA");  // A/B: cap the DMA width (16 / 4)
+    const char *ehd = tune_env("MIPX_HP_DMA");  // A/B: cap the DMA width (16 / 4)
     const bool dw16 = dw && (a.in_pitch % 16) == 0 && (a.in_base % 16) == 0 && (a.in_img % 16) == 0 &&
                       (reinterpret_cast<uintptr_t>(in) % 16) == 0 && !(ehd && *ehd && std::atoi(ehd) < 16);
     if (dw16) {  // rows staged in whole 256-pixel dwordx4 waves from a 4-pixel-aligned origin
@@ -2843,54 +1657,7 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const size_t lds = lds_for(rb);
     const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
-    // i8 MFMA horizontal reduce, an A/B variant (MIPX_HP_MFMA=1): bit-exact, but it
-    // only ties k_hreduce (-8..+20 % by shape and box, slower on RGBA and on odd
-    // output widths; profiles/r02/hmfma_ab.jsonl) -- the pass is bound by staging
-    // latency and stores, not by the dot products the matrix cores take over
-    const char *ehm = std::getenv("MIPX_HP_MFMA");
-    const bool hm_on = ehm && *ehm == '1';
-    if (spec.mode == kSepReduce && a.tp.dot && (b == 3 || b == 4) && hm_on && a.out_img < 0x7fffffffLL) {
-        HmArgs m{};
-        m.in = in;
-        m.out = out;
-        m.in_pitch = a.in_pitch;
-        m.in_base = a.in_base;
-        m.in_img = a.in_img;
-        m.out_img = a.out_img;
-        m.wl = a.wl;
-        m.rows = a.rows;
-        m.ox0 = a.ox0;
-        m.ow = a.ow;
-        m.tp = a.tp;
-        const char *exw = std::getenv("MIPX_HM_XW");  // output pixels per block: 128 (default) / 256
-        const int xw = exw && *exw == '2' ? 256 : 128;
-        m.x_blocks = (a.ow + xw - 1) / xw;
-        m.rb_blocks = (a.rows + kHmRows - 1) / kHmRows;
-        m.nks = (static_cast<int>(std::ceil(15 * s)) + a.tp.taps + 16 + 63) / 64;
-        m.plane_w = ((static_cast<int>(std::ceil((xw - 16) * s)) + 32 + 64 * m.nks) + 15) & ~15;
-        int nt = 0;
-        m.tab = device_reduce_i8(spec.shrink, &nt, &m.tsum);
-        m.raw_max = std::max(((static_cast<int>(std::ceil((xw - 1) * s)) + a.tp.taps + 2) * b + 8 + 3) / 4 + 64,
-                             ((m.plane_w + 16) * b + 3) / 4 + 8);  // the repack may read a quad past the span
-        m.raw_max = std::max(m.raw_max, (xw * 3 + 4 + 3) / 4);      // RGB: output tile rows reuse the raw rows
-        m.row_w = b * m.plane_w + (((b * m.plane_w) / 16) % 2 == 0 ? 16 : 0);
-        const size_t lm = 3 * xw * 4 + static_cast<size_t>(kHmRows) * m.row_w +
-                          static_cast<size_t>(kHmRows) * m.raw_max * 4;
-        if (m.tab && nt == a.tp.taps && m.nks <= 4 && lm <= 64 * 1024) {
-            const long long hb = static_cast<long long>(m.x_blocks) * m.rb_blocks * n;
-            if (!grid_ok(hb)) return MIPX_EINVAL;
-            const dim3 hg(static_cast<unsigned>(hb));
-            if (xw == 256) {
-                if (b == 3) hipLaunchKernelGGL((k_hmfma<3, 256>), hg, dim3(256), lm, st, m);
-                else hipLaunchKernelGGL((k_hmfma<4, 256>), hg, dim3(256), lm, st, m);
-            } else {
-                if (b == 3) hipLaunchKernelGGL((k_hmfma<3, 128>), hg, dim3(256), lm, st, m);
-                else hipLaunchKernelGGL((k_hmfma<4, 128>), hg, dim3(256), lm, st, m);
-            }
-            return launch_check("k_hmfma");
-        }
-    }
-    const char *ehf = std::getenv("MIPX_HP_FAST");  // A/B: 0 keeps k_hpass's reduce path
+    const char *ehf = tune_env("MIPX_HP_FAST");  // A/B: 0 keeps k_hpass's reduce path
     const int tp2 = (a.tp.taps + 1) / 2;
     if (spec.mode == kSepReduce && treg && a.tp.dot && (b == 3 || b == 4) && tp2 <= kVpPairs &&
         !(ehf && *ehf == '0') && a.out_img < 0x7fffffffLL) {
@@ -2942,33 +1709,25 @@ int hpass_launch(const u8 *in, u8 *out, int n, const SepSpec &spec, const SepWin
     return launch_check("k_hpass");
 }
 
-// Fused reduce on the matrix cores (k_rmf2, and the A/B variant k_rmfma with a VALU
-// vertical pass: bit-exact, but 1-20 % slower than the two passes -- its vertical
-// pass over the block's halo costs more than the intermediate it saves): RGB with
-// dword-aligned rows, <= 16 taps each way; MIPX_EUNSUPPORTED otherwise (the caller
-// runs another path).
+// k_rmf2: 3- / 4-band images with rows of any alignment, <= 16 taps each way;
+// MIPX_EUNSUPPORTED otherwise (the caller runs another path).  MIPX_RMFMA=0 turns it
+// off (A/B); MIPX_RMF2_XW=64/128 forces the column width, MIPX_RMF2_HT=0/1 the tap
+// hoisting; MIPX_RMF2_UNALIGNED=0 keeps unaligned rows off it (as when the device
+// fails the unaligned direct-to-LDS probe, lds_dma_unaligned_ok()).
 int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
                        int ow, int oh, hipStream_t st) {
-    // default: k_rmf2 where its LDS leaves >= 4 workgroups per CU (rmfma_ab.jsonl,
-    // rmf2_xw_ab.jsonl: -6 to -35 % against the two passes there); MIPX_RMFMA=0 off,
-    // 1 forces k_rmfma (VALU vertical pass, an A/B variant), 2 forces k_rmf2 (<= 64 KB),
-    // 3 the persistent k_rmf3 (A/B)
-    const char *e = std::getenv("MIPX_RMFMA");
+    const char *e = tune_env("MIPX_RMFMA");
     if (e && *e == '0') return MIPX_EUNSUPPORTED;
-    const bool forced = e && (*e == '1' || *e == '2' || *e == '3');
-    const bool v2 = !forced || *e == '2' || *e == '3';
-    const bool v3 = forced && *e == '3';
     const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
     if ((b != 3 && b != 4) || !(hs > 1.0) || !(vs > 1.0) || in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL)
         return MIPX_EUNSUPPORTED;
-    // k_rmf2 stages rows of any alignment: a direct-to-LDS dword load honours a byte
-    // offset that is not a multiple of 4 (scripts/probe/lds_dma_unaligned.hip,
-    // profiles/r02/lds_dma_unaligned.jsonl), so 1333 x 1000 RGB rows (3999 bytes) take
-    // it too; the A/B kernels k_rmfma / k_rmf3 keep the dword-aligned rows they were
-    // built for (MIPX_RMF2_UNALIGNED=0 restores that limit for k_rmf2 as well)
+    // rows of any alignment: a direct-to-LDS dword load honours a byte offset that is
+    // not a multiple of 4 (scripts/probe/lds_dma_unaligned.hip, profiles/r02/
+    // lds_dma_unaligned.jsonl); the device is probed once (lds_dma_unaligned_ok) and
+    // unaligned rows stay off k_rmf2 if it fails
     const bool rows_aligned = (w * b) % 4 == 0 && reinterpret_cast<uintptr_t>(in) % 4 == 0;
-    const char *eu = std::getenv("MIPX_RMF2_UNALIGNED");
-    if (!rows_aligned && ((e && (*e == '1' || *e == '3')) || (eu && *eu == '0'))) return MIPX_EUNSUPPORTED;
+    const char *eu = tune_env("MIPX_RMF2_UNALIGNED");
+    if (!rows_aligned && ((eu && *eu == '0') || !lds_dma_unaligned_ok())) return MIPX_EUNSUPPORTED;
     SepSpec sh, sv;
     if (!sep_spec_reduce(hs, &sh) || !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
     if (sh.taps > 16 || sv.taps > 16) return MIPX_EUNSUPPORTED;
@@ -2986,171 +1745,49 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
     a.th = make_taps(sh);
     a.tv = make_taps(sv);
     int nt = 0;
-    a.vpairs = device_reduce_pairs(vs, &nt, &a.tpav);
-    if (!a.vpairs || nt != sv.taps) return MIPX_EDEVICE;
     a.tab = device_reduce_i8(hs, &nt, &a.tsum);
     if (!a.tab || nt != sh.taps) return MIPX_EDEVICE;
-    if (v2) {
-        a.tabv = device_reduce_i8(vs, &nt, &a.tsumv);
-        if (!a.tabv || nt != sv.taps) return MIPX_EDEVICE;
-    }
-    a.x_blocks = (ow + kRmXW - 1) / kRmXW;
+    a.tabv = device_reduce_i8(vs, &nt, &a.tsumv);
+    if (!a.tabv || nt != sv.taps) return MIPX_EDEVICE;
     a.y_blocks = (oh + kRmRows - 1) / kRmRows;
-    a.lrows = static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps + 2;
-    const int span = static_cast<int>(std::ceil((kRmXW - 1) * hs)) + sh.taps + 16;  // >= hi - org + 1
-    if (!v2 && b != 3) return MIPX_EUNSUPPORTED;  // k_rmfma is RGB only
-    a.rs = ((b * (span / 4 + 1) + 63) / 64) * 64;
-    if (a.rs < 192) a.rs = 192;
-    if (a.rs > 256) return MIPX_EUNSUPPORTED;
-    a.plane_w = (span + 15) & ~15;
-    a.row_w = b * a.plane_w + ((b * a.plane_w / 16) % 2 == 0 ? 16 : 0);
     a.nks = (static_cast<int>(std::ceil(15 * hs)) + sh.taps + 16 + 63) / 64;
-    a.iw = ((b * span + 15) & ~15) + 16;
-    if (v2 && (static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps > 64 || 4 * a.rs < a.iw))
-        return MIPX_EUNSUPPORTED;
-    const size_t lds = static_cast<size_t>(3 * kRmXW + kRmRows + kRmRows * 8) * 4 +
-                       static_cast<size_t>(kRmRows) * a.row_w + 64 + static_cast<size_t>(a.lrows) * a.rs * 4;
-    if (a.nks > 4 || (!v2 && (lds > 64 * 1024 || static_cast<size_t>(kRmRows) * (kRmXW * 3 + 4) >
-                                                      static_cast<size_t>(a.lrows) * a.rs * 4)))
-        return MIPX_EUNSUPPORTED;
-    const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
-    if (!grid_ok(blocks)) return MIPX_EINVAL;
-    const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
-#define MIPX_RM(RS_)                                                                                    \
-    switch ((sv.taps + 1) / 2) {                                                                        \
-        case 2: hipLaunchKernelGGL((k_rmfma<2, RS_>), grid, blk, lds, st, a); break;                    \
-        case 3: hipLaunchKernelGGL((k_rmfma<3, RS_>), grid, blk, lds, st, a); break;                    \
-        case 4: hipLaunchKernelGGL((k_rmfma<4, RS_>), grid, blk, lds, st, a); break;                    \
-        case 5: hipLaunchKernelGGL((k_rmfma<5, RS_>), grid, blk, lds, st, a); break;                    \
-        case 6: hipLaunchKernelGGL((k_rmfma<6, RS_>), grid, blk, lds, st, a); break;                    \
-        case 7: hipLaunchKernelGGL((k_rmfma<7, RS_>), grid, blk, lds, st, a); break;                    \
-        default: hipLaunchKernelGGL((k_rmfma<8, RS_>), grid, blk, lds, st, a); break;                   \
+    if (a.nks > 4 || static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps > 64) return MIPX_EUNSUPPORTED;
+    a.direct = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
+    // 128- or 64-pixel columns; staged rows at the narrowest stride whose (dwords mod 64)
+    // / 4 is odd, so a transposed read's 8 rows x 2 halves hit 16 distinct bank pairs.
+    // The smaller the LDS, the more workgroups share a CU (<= 32 KB: 5).
+    const char *xe = tune_env("MIPX_RMF2_XW");
+    const int xw_only = xe ? std::atoi(xe) : 0;
+    size_t l2 = 0;
+    int xw = 0;
+    const int lrows2 = static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps + 1;
+    for (const int x : {128, 64}) {
+        if (xw_only && x != xw_only) continue;
+        const int sp = static_cast<int>(std::ceil((x - 1) * hs)) + sh.taps + 4;  // >= hi - org + 1
+        int rsd = (b * (sp / 4 + 1) + 3) & ~3;
+        while (((rsd & 63) >> 2) % 2 == 0) rsd += 4;
+        const int pw = (sp + 15) & ~15;
+        const int rw = b * pw + ((b * pw / 16) % 2 == 0 ? 16 : 0);
+        const int iw = ((b * sp + 15) & ~15) + 16;
+        const size_t lx = static_cast<size_t>(3 * x + 3 * kRmRows) * 4 +
+                          std::max(static_cast<size_t>(lrows2) * rsd * 4, static_cast<size_t>(kRmRows) * (iw + rw) + 64 + 16);
+        if (b * sp > 16 * 4 * kRmMaxCt || x * b + 4 > iw) continue;
+        if (xw == 0 || (l2 > 32 * 1024 && lx < l2)) {
+            xw = x, l2 = lx, a.rsd = rsd, a.plane_w = pw, a.row_w = rw, a.iw = iw;
+            a.x_blocks = (ow + x - 1) / x;
+        }
     }
-    if (v2) {
-        a.direct = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
-        if (v3) {  // persistent, register prefetch of the next tile's rows (128-pixel columns, stride rs + 4)
-            const int rs2 = a.rs + 4;
-            const size_t l2 = static_cast<size_t>(3 * kRmXW + 3 * kRmRows) * 4 +
-                              std::max(static_cast<size_t>(a.lrows) * rs2 * 4,
-                                       static_cast<size_t>(kRmRows) * (a.iw + a.row_w) + 64 + 16);
-            if (l2 > 64 * 1024 || b * span > 16 * 4 * kRmMaxCt ||
-                static_cast<size_t>(kRmRows) * (kRmXW * b + 4) > static_cast<size_t>(kRmRows) * a.iw)
-                return MIPX_EUNSUPPORTED;
-            const int lmax = static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps;
-            if (lmax > 36 || (b * (span / 4 + 1) + 63) / 64 > 3) return MIPX_EUNSUPPORTED;
-            const long long tiles = blocks;
-            a.tiles = static_cast<int>(tiles);
-            const size_t l3 = l2 + 64 * 4;  // the prefetch sink
-            const void *fn = b == 3 ? (a.rs == 192 ? reinterpret_cast<const void *>(&k_rmf3<3, 196>)
-                                                  : reinterpret_cast<const void *>(&k_rmf3<3, 260>))
-                                    : (a.rs == 192 ? reinterpret_cast<const void *>(&k_rmf3<4, 196>)
-                                                  : reinterpret_cast<const void *>(&k_rmf3<4, 260>));
-            // one run per resident workgroup (occupancy x CUs), so every CU finishes together
-            int per_cu = 0, dev = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, l3) != hipSuccess || per_cu < 1) per_cu = 1;
-            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-                cus = 256;
-            long long g = static_cast<long long>(per_cu) * cus;
-            if (const char *ge = std::getenv("MIPX_RM3_G"); ge && std::atoll(ge) > 0) g = std::atoll(ge);  // A/B
-            const dim3 g3(static_cast<unsigned>(std::min(g, tiles)));
-            if (b == 3) {
-                if (a.rs == 192) hipLaunchKernelGGL((k_rmf3<3, 196>), g3, blk, l3, st, a);
-                else hipLaunchKernelGGL((k_rmf3<3, 260>), g3, blk, l3, st, a);
-            } else {
-                if (a.rs == 192) hipLaunchKernelGGL((k_rmf3<4, 196>), g3, blk, l3, st, a);
-                else hipLaunchKernelGGL((k_rmf3<4, 260>), g3, blk, l3, st, a);
-            }
-            return launch_check("k_rmf3");
-        }
-        // k_rmf4 (horizontal products on the interleaved bytes; an A/B variant, MIPX_RMF4=1,
-        // or 2 with the horizontal fragments hoisted): bit-exact but 1.2-1.5x slower than
-        // k_rmf2 except at / 2.4 (rmf4_ab.jsonl): per output BYTE tap fragments gathered from
-        // a 70 KB table cost more than the channel planes' deinterleave they replace
-        const char *e4 = std::getenv("MIPX_RMF4");
-        if (e4 && (*e4 == '1' || *e4 == '2') && !forced && rows_aligned) {
-            const int sp = static_cast<int>(std::ceil((kRmXW - 1) * hs)) + sh.taps + 16;  // >= hi - org + 1
-            int rsd = (b * (sp / 4 + 1) + 3) & ~3;
-            while (((rsd & 63) >> 2) % 2 == 0) rsd += 4;
-            const int iw = ((b * sp + 15) & ~15) + 16;
-            const int dx = (15 + b - 1) / b;  // pixels a 16-byte unit spans beyond its first
-            const int span = b * (static_cast<int>(std::ceil(dx * hs)) + sh.taps - 1) + b - 1 + 8;
-            const int nks = (span + 63) / 64;
-            const size_t l4 = static_cast<size_t>(2 * kRmXW + kRmXW * b + 3 * kRmRows) * 4 +
-                              std::max(static_cast<size_t>(a.lrows) * rsd * 4,
-                                       static_cast<size_t>(kRmRows) * (iw + kRmXW * b + 4));
-            const char *he = std::getenv("MIPX_RMF2_HT");
-            const bool ht = (he && *he) ? *he != '0' : b == 4;
-            int nt4 = 0;
-            a.tabs = device_reduce_i8s(hs, b, &nt4);
-            if (a.tabs && nt4 == sh.taps && nks <= 2 && b * sp <= 16 * 4 * kRmMaxCt && l4 <= 40 * 1024) {
-                a.rsd = rsd;
-                a.iw = iw;
-                a.nks = nks;
-                a.x_blocks = (ow + kRmXW - 1) / kRmXW;
-                a.direct = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0 &&
-                           !(std::getenv("MIPX_RMF2_DIRECT") && *std::getenv("MIPX_RMF2_DIRECT") == '0');
-                const long long blocks4 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
-                if (!grid_ok(blocks4)) return MIPX_EINVAL;
-                const dim3 grid4(static_cast<unsigned>(blocks4));
-                const bool hf = e4 && *e4 == '2';  // MIPX_RMF4=2: horizontal fragments hoisted too
-                if (b == 3) {
-                    if (hf) hipLaunchKernelGGL((k_rmf4<3, 3>), grid4, blk, l4, st, a);
-                    else if (ht) hipLaunchKernelGGL((k_rmf4<3, 1>), grid4, blk, l4, st, a);
-                    else hipLaunchKernelGGL((k_rmf4<3, 0>), grid4, blk, l4, st, a);
-                } else {
-                    if (hf) hipLaunchKernelGGL((k_rmf4<4, 3>), grid4, blk, l4, st, a);
-                    else if (ht) hipLaunchKernelGGL((k_rmf4<4, 1>), grid4, blk, l4, st, a);
-                    else hipLaunchKernelGGL((k_rmf4<4, 0>), grid4, blk, l4, st, a);
-                }
-                return launch_check("k_rmf4");
-            }
-        }
-        // k_rmf2: 128- or 64-pixel columns; staged rows at the narrowest stride whose
-        // (dwords mod 64) / 4 is odd, so a transposed read's 8 rows x 2 halves hit 16 distinct
-        // bank pairs.  The smaller the LDS, the more workgroups share a CU (<= 32 KB: 5).
-        const char *xe = std::getenv("MIPX_RMF2_XW");  // A/B: 128 or 64 forces the column width
-        const int xw_only = xe ? std::atoi(xe) : 0;
-        const char *re = std::getenv("MIPX_RMF2_RS");
-        const bool rs_wide = re && *re == '1';
-        size_t l2 = 0;
-        int xw = 0;
-        // staged pixels start at lo floored to 4 (the planes are indexed from there, so the
-        // horizontal windows need no 16-pixel origin): 12 fewer pixels per row, and staged
-        // rows for ceil(15 vs) + taps + 1 output-row windows; MIPX_RMF2_ORG=16 is the r02 layout
-        const char *eo = std::getenv("MIPX_RMF2_ORG");
-        const bool org16 = eo && std::atoi(eo) == 16;
-        a.orgmask = org16 ? ~15 : ~3;
-        const int lrows2 = org16 ? a.lrows : static_cast<int>(std::ceil((kRmRows - 1) * vs)) + sv.taps + 1;
-        for (const int x : {128, 64}) {
-            if (xw_only && x != xw_only) continue;
-            const int sp = static_cast<int>(std::ceil((x - 1) * hs)) + sh.taps + (org16 ? 16 : 4);  // >= hi - org + 1
-            int rsd = (b * (sp / 4 + 1) + 3) & ~3;
-            while (((rsd & 63) >> 2) % 2 == 0) rsd += 4;
-            if (rs_wide) rsd = std::max(192, (b * (sp / 4 + 1) + 63) / 64 * 64) + 4;  // A/B: the r02 stride
-            const int pw = (sp + 15) & ~15;
-            const int rw = b * pw + ((b * pw / 16) % 2 == 0 ? 16 : 0);
-            const int iw = ((b * sp + 15) & ~15) + 16;
-            const size_t lx = static_cast<size_t>(3 * x + 3 * kRmRows) * 4 +
-                              std::max(static_cast<size_t>(lrows2) * rsd * 4, static_cast<size_t>(kRmRows) * (iw + rw) + 64 + 16);
-            if (b * sp > 16 * 4 * kRmMaxCt || x * b + 4 > iw) continue;
-            if (xw == 0 || (l2 > 32 * 1024 && lx < l2)) {
-                xw = x, l2 = lx, a.rsd = rsd, a.plane_w = pw, a.row_w = rw, a.iw = iw;
-                a.x_blocks = (ow + x - 1) / x;
-            }
-        }
-        // RGB and RGBA by default (cfg_rmf2_ab.jsonl: C3 / C4 / C5 +2.7 / +1.7 / +0.2 % over the
-        // RGB-only default once the narrow stride took 1024^2 RGBA / 1.333 to 6 workgroups)
-        if (xw == 0 || l2 > (forced ? 64 : 40) * 1024) return MIPX_EUNSUPPORTED;
-        if (const char *de = std::getenv("MIPX_RMF2_DBG")) a.dbg = std::atoi(de);  // timing only: wrong pixels
-        if (const char *ds = std::getenv("MIPX_RMF2_DIRECT"); ds && *ds == '0') a.direct = 0;  // A/B: tile stores
-        const long long blocks2 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
-        if (!grid_ok(blocks2)) return MIPX_EINVAL;
-        const dim3 grid2(static_cast<unsigned>(blocks2));
-        // HT: tap fragments loaded while the staged rows are in flight.  ht_ab.jsonl: RGBA
-        // -5 % (1024^2 / 1.333 1.308 -> 1.246 ms, 1080p / 1.6 0.288 -> 0.275), RGB flat (+-2 %,
-        // the extra registers cost what the hidden latency saves); MIPX_RMF2_HT=0/1 forces
-        const char *he = std::getenv("MIPX_RMF2_HT");
-        const bool ht = (he && *he) ? *he != '0' : b == 4;
+    // RGB and RGBA (cfg_rmf2_ab.jsonl: C3 / C4 / C5 +2.7 / +1.7 / +0.2 % over the RGB-only
+    // default once the narrow stride took 1024^2 RGBA / 1.333 to 6 workgroups)
+    if (xw == 0 || l2 > 40 * 1024) return MIPX_EUNSUPPORTED;
+    const long long blocks2 = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
+    if (!grid_ok(blocks2)) return MIPX_EINVAL;
+    const dim3 grid2(static_cast<unsigned>(blocks2)), blk(256);
+    // HT: tap fragments loaded while the staged rows are in flight.  ht_ab.jsonl: RGBA
+    // -5 % (1024^2 / 1.333 1.308 -> 1.246 ms, 1080p / 1.6 0.288 -> 0.275), RGB flat (+-2 %,
+    // the extra registers cost what the hidden latency saves)
+    const char *he = tune_env("MIPX_RMF2_HT");
+    const bool ht = (he && *he) ? *he != '0' : b == 4;
 #define MIPX_RMF2_GO(HT_)                                                                 \
     if (b == 3) {                                                                         \
         if (xw == 128) hipLaunchKernelGGL((k_rmf2<3, 128, HT_>), grid2, blk, l2, st, a);  \
@@ -3159,18 +1796,13 @@ int reduce_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double
         if (xw == 128) hipLaunchKernelGGL((k_rmf2<4, 128, HT_>), grid2, blk, l2, st, a);  \
         else hipLaunchKernelGGL((k_rmf2<4, 64, HT_>), grid2, blk, l2, st, a);             \
     }
-        if (ht) {
-            MIPX_RMF2_GO(1)
-        } else {
-            MIPX_RMF2_GO(0)
-        }
-#undef MIPX_RMF2_GO
-        return launch_check("k_rmf2");
+    if (ht) {
+        MIPX_RMF2_GO(1)
+    } else {
+        MIPX_RMF2_GO(0)
     }
-    if (a.rs == 192) { MIPX_RM(192) }
-    else { MIPX_RM(256) }
-#undef MIPX_RM
-    return launch_check("k_rmfma");
+#undef MIPX_RMF2_GO
+    return launch_check("k_rmf2");
 }
 
 // Fused reducev -> reduceh of the output window [ox0, ox0 + ow) x [oy0, oy0 + oh);
@@ -3180,7 +1812,7 @@ int reduce_fused_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
     // Measured (profiles/r01/v11_fused_ab.log): the fused launch wins on small
     // images (<= ~0.5 MB, the thumbnail / smartcrop / post-shrink shapes) and loses
     // to the two DMA-staged passes on large ones.  MIPX_FUSED_REDUCE=0/1 forces it.
-    const char *ef = std::getenv("MIPX_FUSED_REDUCE");
+    const char *ef = tune_env("MIPX_FUSED_REDUCE");
     if (ef && *ef) {
         if (ef[0] == '0') return MIPX_EUNSUPPORTED;
     } else if (img_bytes(w, h, b) > 512 * 1024) {
@@ -3226,68 +1858,6 @@ int reduce_fused_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
     MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduce_fused<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds,
                                               st, a));
     return launch_check("k_reduce_fused");
-}
-
-// Fused reducev -> reduceh of the output window for large images (k_reduce2d);
-// MIPX_EUNSUPPORTED when a mask or the tile does not fit (caller runs two
-// passes).  Off unless MIPX_REDUCE2D=1: it loses to the two DMA-staged passes
-// (C3's 1024^2 RGBA / 1.333: 2.90 vs 1.95 ms, 1080p RGB / 2.47: 0.68 vs 0.33 ms,
-// profiles/r01/v17/ab_reduce2d_*.log); occupancy (3 workgroups per CU at 45 KB of
-// LDS) and the serial stage -> vertical -> horizontal chain per block bound it.
-// MIPX_REDUCE2D_ROWS sets rows per block.
-int reduce2d_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
-                    int ow, int oh, hipStream_t st) {
-    const char *ef = std::getenv("MIPX_REDUCE2D");
-    if (!(ef && *ef == '1')) return MIPX_EUNSUPPORTED;
-    SepSpec sh, sv;
-    if (!sep_spec_reduce(hs, &sh) || !sep_spec_reduce(vs, &sv)) return MIPX_EDEVICE;
-    if (sh.taps > kR2MaxTaps || sv.taps > 48) return MIPX_EUNSUPPORTED;
-    R2DArgs a{};
-    a.in = in;
-    a.out = out;
-    a.w = w;
-    a.h = h;
-    a.in_pitch = w * b;
-    a.in_img = img_bytes(w, h, b);
-    a.out_img = img_bytes(ow, oh, b);
-    if (a.in_img >= 0x7fffffffLL - 16) return MIPX_EUNSUPPORTED;
-    a.ox0 = ox0;
-    a.oy0 = oy0;
-    a.ow = ow;
-    a.oh = oh;
-    a.tv = make_taps(sv);
-    a.thz = make_taps(sh);
-    // column span of a block: <= 2 KiB of input bytes, <= 256 output pixels
-    constexpr int kSpanBytes = 2048;
-    int bw = static_cast<int>(std::floor((kSpanBytes / b - sh.taps - 3) / hs)) + 1;
-    bw = std::max(1, std::min(bw, 256));
-    const int xblk = (ow + bw - 1) / bw;
-    a.bw = (ow + xblk - 1) / xblk;
-    a.x_blocks = (ow + a.bw - 1) / a.bw;
-    const int span_px = static_cast<int>(std::ceil((a.bw - 1) * hs)) + sh.taps + 2;
-    const int nd = (span_px * b + 3) / 4;
-    a.mid_stride = nd + 2;
-    a.raw_stride = ((nd + 1 + 63) / 64) * 64;
-    const int tp2 = (sv.taps + 1) / 2;
-    auto lrows_for = [&](int kr) { return static_cast<int>(std::ceil((kr - 1) * vs)) + sv.taps + 3; };
-    auto lds_for = [&](int kr) {
-        return (static_cast<size_t>(lrows_for(kr)) * a.raw_stride + static_cast<size_t>(kr) * a.mid_stride +
-                static_cast<size_t>(kr) * (tp2 + 1) + lrows_for(kr) + 1) * 4;
-    };
-    const char *er = std::getenv("MIPX_REDUCE2D_ROWS");
-    int kr = (er && *er) ? std::max(1, std::atoi(er)) : 8;
-    constexpr size_t kBudget = 64 * 1024;
-    while (kr > 1 && lds_for(kr) > kBudget) --kr;
-    if (lds_for(kr) > kBudget) return MIPX_EUNSUPPORTED;
-    a.kr = std::min(kr, oh);
-    a.lrows = lrows_for(a.kr);
-    a.y_blocks = (oh + a.kr - 1) / a.kr;
-    const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
-    if (!grid_ok(blocks)) return MIPX_EINVAL;
-    const size_t lds = lds_for(a.kr);
-    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_reduce2d<B_>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds,
-                                              st, a));
-    return launch_check("k_reduce2d");
 }
 
 }  // namespace mipx

@@ -477,7 +477,7 @@ int shrink_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int 
     const long long blocks = static_cast<long long>(a.x_blocks) * (y1 - y0) * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     // S <= 4 on both axes, dword-aligned rows: the register-only quad kernel (MIPX_SHRINK_Q=0: off)
-    const char *eq = std::getenv("MIPX_SHRINK_Q");
+    const char *eq = tune_env("MIPX_SHRINK_Q");
     if (!(eq && *eq == '0') && hs == vs && hs >= 2 && hs <= 4 && (b == 3 || b == 4) && (w * b) % 4 == 0 && n <= 65535 &&
         a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0) {
         ShrinkArgs q = a;
@@ -493,7 +493,7 @@ int shrink_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int 
     }
     // equal factors 5-12 (RGBA 5-10): one output pixel per lane from registers, 1.03-1.25x
     // k_shrink_x4 (profiles/r02/shrink_p1_ab.jsonl); MIPX_SHRINK_P1=0: off, =1: RGBA / 11 too
-    const char *ep = std::getenv("MIPX_SHRINK_P1");
+    const char *ep = tune_env("MIPX_SHRINK_P1");
     const int p1_rgba_max = (ep && *ep == '1') ? 11 : 10;
     if (!(ep && *ep == '0') && hs == vs && hs >= 5 && hs <= 12 && (b == 3 || (b == 4 && hs <= p1_rgba_max)) &&
         n <= 65535) {
@@ -517,14 +517,14 @@ int shrink_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int 
 #undef MIPX_SP
         return launch_check("k_shrink_p1");
     }
-    const char *ex = std::getenv("MIPX_SHRINK_X4");  // A/B: 0 selects the dword kernel
+    const char *ex = tune_env("MIPX_SHRINK_X4");  // A/B: 0 selects the dword kernel
     const bool x4 = (w * b) % 4 == 0 && a.in_img % 4 == 0 && (reinterpret_cast<uintptr_t>(in) & 3u) == 0 &&
                     vs <= 257 && tws >= 4 && !(ex && *ex == '0');
     if (x4) {
         // output rows per block (small vs: enough to stream ~8 input rows), within 32 KB of LDS;
         // each row's chunks may run up to 16 bytes past its span (LDS rows rounded to whole chunks)
         a.lstride = static_cast<int>(((static_cast<size_t>(tws) * hs * b + 15) / 16 + 1) * 4);
-        const char *ery = std::getenv("MIPX_SHRINK_RY");
+        const char *ery = tune_env("MIPX_SHRINK_RY");
         // measured (profiles/r01/v14/ab_shrink_rows.log): only vs <= 3 gains from several rows per block
         int ry = (ery && *ery) ? std::max(1, std::atoi(ery)) : vs <= 3 ? (8 + vs - 1) / vs : 1;
         while (ry > 1 && static_cast<size_t>(ry) * a.lstride * 4 > 32768) --ry;

@@ -21,6 +21,16 @@ int hip_fail(hipError_t e, const char *what);  // records detail, returns MIPX_E
         if (e_ != hipSuccess) return ::mipx::hip_fail(e_, #call);         \
     } while (0)
 
+// ---- kernel-selection knobs (mipx_tuning.cpp) -------------------------------
+// The MIPX_* environment variables as snapshotted on first use (or by
+// mipx_tuning_reload): nullptr when unset.  Launchers call this, never getenv.
+const char *tune_env(const char *name);
+void tune_reload();
+
+// ---- device capability probes (k_probe.hip), run once per device -------------
+// Do direct-to-LDS dword buffer loads honour byte offsets that are not multiples of 4?
+bool lds_dma_unaligned_ok();
+
 // ---- libvips resample constants (resample/templates.h, [U]) ----------------
 constexpr int kTransformScale = 128;  // VIPS_TRANSFORM_SCALE: 129 sub-pixel phases
 constexpr int kInterpShift = 12;      // VIPS_INTERPOLATE_SHIFT
@@ -93,14 +103,15 @@ bool sep_spec_reduce(double shrink, SepSpec *s);
 bool sep_spec_gauss(double sigma, double min_ampl, SepSpec *s);
 int vpass_launch(const uint8_t *in, uint8_t *out, int n, const SepSpec &spec, const SepWindow &w, hipStream_t st);
 int hpass_launch(const uint8_t *in, uint8_t *out, int n, const SepSpec &spec, const SepWindow &w, hipStream_t st);
-int reduce2d_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
-                    int oy0, int ow, int oh, hipStream_t st);
 int reduce_fused_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                         int oy0, int ow, int oh, hipStream_t st);
 // k_rstrip.hip: streaming fused reduce (LDS row ring + LDS intermediate), any shrink pair
-// both shrinks > 1 in one launch (k_rmf2, else the strip walker, else the A/B fused
-// kernels); MIPX_EUNSUPPORTED = run the two separable passes
+// both shrinks > 1 in one launch (k_rcol, else k_rmf2, else the strip walker, else the
+// small-image fused kernel); MIPX_EUNSUPPORTED = run the two separable passes
 int reduce_one_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
+                      int oy0, int ow, int oh, hipStream_t st);
+// k_rcol.hip: the column walker (LDS row ring, both passes on the matrix cores)
+int reduce_col_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                       int oy0, int ow, int oh, hipStream_t st);
 int reduce_mfma_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                        int oy0, int ow, int oh, hipStream_t st);

@@ -1,0 +1,70 @@
+// mipx_tuning.cpp — kernel-selection knobs (MIPX_* environment variables) read once.
+//
+// The launchers pick kernels and layouts by geometry; a few MIPX_* variables force
+// an alternative for A/B runs and tests (e.g. MIPX_RCOL=0).  They are snapshotted
+// from the environment on first use into an immutable map, so no launch calls
+// getenv (which is not safe beside a concurrent setenv, and costs time on the
+// small-image path).  mipx_tuning_reload() takes a new snapshot; old snapshots are
+// kept alive, since a launcher on another thread may still hold one of their strings.
+#include <atomic>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mipx_internal.h"
+
+extern char **environ;
+
+namespace mipx {
+namespace {
+
+struct Snapshot {
+    std::map<std::string, std::string> kv;
+};
+std::atomic<const Snapshot *> g_snap{nullptr};
+std::mutex g_mu;
+std::vector<std::unique_ptr<Snapshot>> &g_all() {
+    static auto *v = new std::vector<std::unique_ptr<Snapshot>>();  // leaked on purpose: outlives static dtors
+    return *v;
+}
+
+const Snapshot *take_snapshot_locked() {
+    auto s = std::make_unique<Snapshot>();
+    for (char **e = environ; e && *e; ++e) {
+        if (std::strncmp(*e, "MIPX_", 5) != 0) continue;
+        const char *eq = std::strchr(*e, '=');
+        if (eq) s->kv.emplace(std::string(*e, static_cast<size_t>(eq - *e)), std::string(eq + 1));
+    }
+    const Snapshot *p = s.get();
+    g_all().push_back(std::move(s));
+    g_snap.store(p, std::memory_order_release);
+    return p;
+}
+
+}  // namespace
+
+const char *tune_env(const char *name) {
+    const Snapshot *s = g_snap.load(std::memory_order_acquire);
+    if (!s) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        s = g_snap.load(std::memory_order_acquire);
+        if (!s) s = take_snapshot_locked();
+    }
+    const auto it = s->kv.find(name);
+    return it == s->kv.end() ? nullptr : it->second.c_str();
+}
+
+void tune_reload() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    take_snapshot_locked();
+}
+
+}  // namespace mipx
+
+extern "C" int mipx_tuning_reload(void) {
+    mipx::tune_reload();
+    return MIPX_OK;
+}

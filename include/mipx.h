@@ -157,7 +157,9 @@ const char *mipx_build_id(void);
 int mipx_abi_version(void);
 const char *mipx_strerror(int code);
 const char *mipx_last_error(void);      /* thread-local detail of the last failure */
-int mipx_init(const mipx_cfg *cfg);     /* NULL = defaults; already up: MIPX_OK, running config kept */
+/* NULL = defaults.  Already up: MIPX_OK for NULL or the running configuration,
+ * MIPX_EINVAL (with mipx_last_error) for a different one — mipx_shutdown first. */
+int mipx_init(const mipx_cfg *cfg);
 void mipx_shutdown(void);
 int mipx_device_count(void);
 
@@ -190,6 +192,11 @@ int mipx_process(const mipx_plan *plan, const mipx_img *in, const mipx_img *wm,
  * queue of that device; device < 0 the least-loaded queue of all. */
 int mipx_stats(int device, uint64_t *batches, uint64_t *requests);
 int mipx_queue_count(void);                           /* 0 before mipx_init */
+/* The dispatch rule of mipx_submit, callable without a GPU: the queue (index into
+ * the n_queues arrays) with the fewest pending bytes among those of `device`
+ * (device < 0: among all), first on ties; MIPX_EINVAL when none qualifies. */
+int mipx_pick_queue(int32_t device, const int32_t *queue_device, const int64_t *pending_bytes,
+                    int32_t n_queues);
 int mipx_queue_stats(int queue, int32_t *device, uint64_t *batches, uint64_t *requests,
                      int64_t *pending_bytes);         /* pending = queued input bytes */
 
@@ -240,6 +247,12 @@ int mipx_op_smartcrop_origin(const uint8_t *d_in, int32_t *d_origins, int32_t n,
                              void *d_workspace, size_t workspace_bytes, void *stream);
 size_t mipx_op_workspace_bytes(int32_t op, int32_t n, int32_t w, int32_t h, int32_t bands,
                                double p0, double p1);
+
+/* ---- engine tuning (tests and benchmarks) ----
+ * Kernel-selection knobs (MIPX_* environment variables, e.g. MIPX_RCOL=0 for the
+ * previous generic reduce) are read once, on first use.  mipx_tuning_reload()
+ * re-reads them; call it only between launches (A/B scripts, tests). */
+int mipx_tuning_reload(void);
 
 /* ---- device memory helpers (so a binding needs no other HIP wrapper) ---- */
 int mipx_set_device(int device);

@@ -70,10 +70,11 @@ def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
 
 
-@pytest.mark.parametrize("var", [0, 1, 2, 3, 6, 66, 67, 130, 131])
+@pytest.mark.parametrize("var", [66])
 def test_reduce2x2_variants_exact(gpu, oracle, rng, var, monkeypatch):
-    """Every A/B build of the fused 2x2 kernel (MIPX_R2_VARIANT, read per launch)
-    is bit-exact, including strips that end at the image edge."""
+    """The fused 2x2 kernel (the shipped build, variant 66; the r01/r02 A/B builds
+    are recorded under profiles/ and no longer compiled) is bit-exact, including
+    strips that end at the image edge."""
     monkeypatch.setenv("MIPX_R2_VARIANT", str(var))
     for h, w, b in ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1001 * 4 // 4 - 1, 4), (200, 646, 3)):
         if (w * b) % 4:
@@ -88,10 +89,10 @@ def test_reduce2x2_variants_exact(gpu, oracle, rng, var, monkeypatch):
 def test_reduce_fused_and_two_pass_paths(gpu, oracle, rng, fused, monkeypatch):
     """Both generic reduce paths (one fused launch / two DMA-staged passes) on the
     same shapes, including output windows (reduce -> extract plans).  "0" turns
-    the small-image fused kernel off (k_reduce2d is off unless asked for)."""
+    the small-image fused kernel off."""
     monkeypatch.setenv("MIPX_FUSED_REDUCE", fused)
-    monkeypatch.setenv("MIPX_REDUCE2D", "0")
-    monkeypatch.setenv("MIPX_RMFMA", "0")  # k_rmf2 has its own test
+    monkeypatch.setenv("MIPX_RCOL", "0")   # k_rcol and k_rmf2 have their own tests
+    monkeypatch.setenv("MIPX_RMFMA", "0")
     for h, w, b, hs, vs in ((240, 427, 3, 1.4233, 1.4233), (273, 364, 3, 1.421875, 1.06640625),
                             (97, 130, 4, 1.3333333333333333, 1.3333333333333333), (45, 61, 1, 2.9, 1.7),
                             (60, 90, 2, 1.05, 3.3), (300, 200, 3, 2.4666666666666666, 2.4666666666666666)):
@@ -382,17 +383,17 @@ def test_reduce_passes_dot2_and_float_paths(gpu, oracle, rng, monkeypatch, dot, 
             assert_same(gh[i], oracle.reduceh(imgs[i], s), f"reduceh {s} {h}x{w}x{b} dot={dot}")
 
 
-@pytest.mark.parametrize("path", ["unrolled", "loop", "share"])
+@pytest.mark.parametrize("path", ["unrolled", "loop"])
 @pytest.mark.parametrize("s", [1.02, 1.3333333333333333, 1.6, 2.4, 2.7, 3.7, 5.9])
 def test_reducev_paths(gpu, oracle, rng, monkeypatch, path, s):
     """Vertical reduce kernels: k_vreduce with the tap pairs unrolled (default for
     <= 16 taps on 4-byte rows), k_vpass's generic loop (MIPX_VP_FAST=0, and every
-    case k_vreduce does not take) and the A/B variant that shares staged row pairs
-    between a block's output rows (MIPX_VP_SHARE=1): 16- and 4-byte-aligned
+    case k_vreduce does not take): 16- and 4-byte-aligned
     batches (DMA 16 / 4), odd row bytes and an unaligned batch (DMA 0), many row
     blocks, both pair alignments of each row, short images, windowed plans."""
     monkeypatch.setenv("MIPX_VP_FAST", "0" if path == "loop" else "1")
-    monkeypatch.setenv("MIPX_VP_SHARE", "1" if path == "share" else "0")
+    monkeypatch.setenv("MIPX_RCOL", "0")
+    monkeypatch.setenv("MIPX_RMFMA", "0")
     monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
     monkeypatch.setenv("MIPX_RSTRIP", "0")
     for h, w, b in ((301, 64, 4), (257, 100, 3), (97, 1030, 4), (45, 301, 1), (7, 80, 4), (333, 33, 3),
@@ -411,18 +412,17 @@ def test_reducev_paths(gpu, oracle, rng, monkeypatch, path, s):
         assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract {path}")
 
 
-@pytest.mark.parametrize("kernel,pack3", [("mfma", "0"), ("hreduce", "0"), ("hreduce", "1"), ("hpass", "0"),
-                                          ("hpass", "1")])
+@pytest.mark.parametrize("kernel,pack3", [("hreduce", "0"), ("hreduce", "1"), ("hpass", "0"), ("hpass", "1")])
 @pytest.mark.parametrize("s", [1.02, 1.3333333333333333, 1.6, 2.4, 2.7, 3.7, 6.3])
 def test_reduceh_paths(gpu, oracle, rng, monkeypatch, kernel, pack3, s):
-    """Horizontal reduce kernels: k_hmfma (i8 MFMA, RGB / RGBA, an A/B variant behind
-    MIPX_HP_MFMA=1), k_hreduce (default: compile-time tap pairs, up to 16 taps) and k_hpass
+    """Horizontal reduce kernels: k_hreduce (default: compile-time tap pairs, up to 16 taps) and k_hpass
     (MIPX_HP_FAST=0 as well, and 1 / 2 bands, longer masks): RGBA rows 16- / 4-byte
     aligned and unaligned (DW 16 / 4 / 0), RGB with and without the 3-dword group
     stores (MIPX_HP_PACK3), rows that end inside a 4-pixel group, images narrower
     than a group, several column blocks, windowed plans (reduce -> extract)."""
-    monkeypatch.setenv("MIPX_HP_MFMA", "1" if kernel == "mfma" else "0")
     monkeypatch.setenv("MIPX_HP_FAST", "0" if kernel == "hpass" else "1")
+    monkeypatch.setenv("MIPX_RCOL", "0")
+    monkeypatch.setenv("MIPX_RMFMA", "0")
     monkeypatch.setenv("MIPX_HP_PACK3", pack3)
     monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
     monkeypatch.setenv("MIPX_RSTRIP", "0")
@@ -443,26 +443,19 @@ def test_reduceh_paths(gpu, oracle, rng, monkeypatch, kernel, pack3, s):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce+extract b={b} {kernel}")
 
 
-@pytest.mark.parametrize("on", ["", "2o", "4", "4t", "4h", "3", "3g", "2", "2n", "2t", "1", "0"])
+@pytest.mark.parametrize("on", ["", "2n", "2t", "0"])
 @pytest.mark.parametrize("hs,vs", [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9),
                                    (2.7, 1.5), (1.46484375, 1.46484375), (1.1, 1.05)])
 def test_reduce_rmfma_fused(gpu, oracle, rng, monkeypatch, on, hs, vs):
-    """k_rmfma (vertical dot2 pass into channel-planar LDS, horizontal pass on the i8
-    matrix cores, one launch) against the oracle: RGB with dword-aligned rows, blocks
-    at both image edges, images narrower than a block and shorter than 16 rows, many
-    row and column blocks, windowed plans (reduce -> extract), and the cases it leaves
-    to other kernels (17 taps, unaligned rows).  It is an A/B variant (MIPX_RMFMA=1);
-    MIPX_RMFMA=0 runs the default kernels on the same cases; "3g" runs the persistent
-    k_rmf3 on 5 workgroups, so each one's run of tiles crosses columns and images; "2n"
-    forces k_rmf2's 64-pixel columns, "2t" k_rmf2 with its tap loads after the barriers.
-    "4" runs the A/B variant k_rmf4 (horizontal products on the interleaved bytes), "4t"
-    the same with its vertical taps loaded after the barrier, "4h" with every tap
-    fragment loaded while the rows are in flight."""
-    monkeypatch.setenv("MIPX_RMFMA", "" if on[:1] == "4" else on[:1])
-    monkeypatch.setenv("MIPX_RMF2_HT", "0" if on in ("2t", "4t") else "1")
-    monkeypatch.setenv("MIPX_RMF4", {"4": "1", "4t": "1", "4h": "2"}.get(on, "0"))
-    monkeypatch.setenv("MIPX_RMF2_ORG", "16" if on == "2o" else "4")  # "2o": the r02 16-pixel staging origin
-    monkeypatch.setenv("MIPX_RM3_G", "5" if on == "3g" else "0")
+    """k_rmf2 (both passes on the i8 matrix cores, channel-planar horizontal operands)
+    against the oracle, with k_rcol off so it takes every case it can: RGB / RGBA, rows
+    of any alignment, blocks at both image edges, images narrower than a block and
+    shorter than 16 rows, windowed plans (reduce -> extract), and the cases it leaves to
+    other kernels (17 taps).  "2n" forces its 64-pixel columns, "2t" its tap loads
+    after the barriers; "0" turns it off (the strip walker / two passes take over)."""
+    monkeypatch.setenv("MIPX_RCOL", "0")
+    monkeypatch.setenv("MIPX_RMFMA", "0" if on == "0" else "")
+    monkeypatch.setenv("MIPX_RMF2_HT", "0" if on == "2t" else "1")
     monkeypatch.setenv("MIPX_RMF2_XW", "64" if on == "2n" else "0")
     monkeypatch.setenv("MIPX_RSTRIP", "0")
     monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
@@ -496,34 +489,6 @@ def test_reduce_narrow_unaligned_rows(gpu, oracle, rng, w):
         got = gpu.run_op("reduce", imgs, hshrink=s, vshrink=s)
         for i in range(3):
             assert_same(got[i], oracle.reduce(imgs[i], s, s), f"reduce {h}x{w}x3 /{s} img{i}")
-
-
-@pytest.mark.parametrize("rows", ["1", "8", "13"])
-def test_reduce2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows):
-    """Fused generic reduce (k_reduce2d, an A/B variant behind MIPX_REDUCE2D=1:
-    DMA-staged rows, dot2 vertical pass into LDS, dot2 horizontal pass from it) on every band count, odd sizes, unaligned
-    batches, several column blocks, unequal shrinks and masks up to 16 horizontal
-    taps; the small-image fused kernel is switched off so this path runs."""
-    monkeypatch.setenv("MIPX_FUSED_REDUCE", "0")
-    monkeypatch.setenv("MIPX_REDUCE2D", "1")  # A/B variant, off by default
-    monkeypatch.setenv("MIPX_RMFMA", "0")
-    monkeypatch.setenv("MIPX_REDUCE2D_ROWS", rows)
-    for h, w, b, hs, vs in ((41, 57, 1, 1.1, 1.1), (37, 43, 2, 1.3333333333333333, 1.6), (64, 90, 3, 1.6, 1.6),
-                            (50, 128, 4, 2.5, 1.3333333333333333), (31, 17, 3, 1.3, 2.9), (40, 1100, 3, 1.3333333333333333, 1.4),
-                            (30, 700, 4, 1.75, 3.7), (23, 2100, 1, 2.4, 1.05), (19, 301, 2, 1.01, 6.5)):
-        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
-        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
-        for i in range(3):
-            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"reduce2d {h}x{w}x{b} {hs}x{vs} rows={rows} img{i}")
-    # a reduce -> extract window (C3's crop) through a whole plan
-    opts = dict(width=300, height=200, crop=1)
-    p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(640, 520, 4, "png"))
-    e, rp = oracle.plan(opts, dict(w=640, h=520, bands=4, type=3))
-    assert e == 0
-    imgs = rng.integers(0, 256, (2, 520, 640, 4), dtype=np.uint8)
-    got = gpu.execute(p, imgs)
-    for i in range(2):
-        assert_same(got[i], oracle.execute(rp, imgs[i]), f"reduce2d window rows={rows}")
 
 
 @pytest.mark.parametrize("repack", ["1", "0"])

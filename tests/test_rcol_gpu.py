@@ -1,0 +1,82 @@
+"""k_rcol, the column-walking generic Lanczos3 reduce (LDS row ring, both passes on
+the i8 matrix cores), against the oracle: strips at both image edges (the COPY edge
+folded into the horizontal operands), images narrower than a strip and shorter than
+a step, segment boundaries in tall images, RGB and RGBA, shrink pairs across
+(1, 2.75), windows (reduce -> extract), unaligned output rows (byte stores) and a
+seeded fuzz over shapes.  Unaligned input rows leave k_rcol (MIPX_EUNSUPPORTED) for
+k_rmf2; those cases check that the hand-off stays exact."""
+import numpy as np
+import pytest
+
+from test_parity_gpu import assert_same, rand_img, smooth_img
+
+pytestmark = pytest.mark.gpu
+
+SHRINKS = [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9), (2.7, 1.5),
+           (1.46484375, 1.46484375), (1.1, 1.05), (1.6, 1.5976331360946747), (2.0, 1.25), (1.25, 2.0)]
+SHAPES = [(301, 1100, 3), (97, 640, 3), (13, 200, 3), (40, 36, 3), (270, 480, 3), (37, 1028, 3), (150, 96, 3),
+          (201, 700, 4), (19, 333, 4), (64, 1024, 4), (1000, 1500, 3), (9, 4, 3), (700, 64, 4), (101, 1333, 3)]
+
+
+@pytest.mark.parametrize("hs,vs", SHRINKS)
+def test_rcol_matches_oracle(gpu, oracle, rng, hs, vs):
+    for h, w, b in SHAPES:
+        if int(w / hs + 0.5) < 1 or int(h / vs + 0.5) < 1:
+            continue
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
+        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+        for i in range(len(imgs)):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"rcol {h}x{w}x{b} {hs}x{vs} img{i}")
+
+
+@pytest.mark.parametrize("b", [3, 4])
+@pytest.mark.parametrize("g", [0, 1, 2, 3, 4])
+def test_rcol_windows(gpu, oracle, rng, b, g):
+    """reduce -> extract at every gravity: the window's rows and columns only."""
+    for (iw, ih, opts) in ((1500, 1000, dict(width=333, height=171, crop=1)),
+                           (1024, 1024, dict(width=768, height=512, crop=1)),
+                           (1200, 800, dict(width=700, height=300, crop=1))):
+        opts = dict(opts, gravity=g)
+        p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(iw, ih, b, "png"))
+        e, rp = oracle.plan(opts, dict(w=iw, h=ih, bands=b, type=3))
+        assert e == 0
+        imgs = rng.integers(0, 256, (2, ih, iw, b), dtype=np.uint8)
+        got = gpu.execute(p, imgs)
+        for i in range(2):
+            assert_same(got[i], oracle.execute(rp, imgs[i]), f"rcol window {iw}x{ih} {opts} bands {b}")
+
+
+def test_rcol_fuzz(gpu, oracle):
+    r = np.random.default_rng(20241220)
+    for case in range(60):
+        b = int(r.choice([3, 4]))
+        w = int(r.integers(1, 900))
+        if b == 3:
+            w = max(4, w & ~3)  # dword-aligned rows (k_rcol's domain)
+        h = int(r.integers(1, 500))
+        hs, vs = float(r.uniform(1.01, 2.74)), float(r.uniform(1.01, 2.74))
+        if int(w / hs + 0.5) < 1 or int(h / vs + 0.5) < 1:
+            continue
+        n = int(r.integers(1, 4))
+        imgs = r.integers(0, 256, (n, h, w, b), dtype=np.uint8)
+        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+        for i in range(n):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"fuzz {case}: {h}x{w}x{b} {hs}x{vs} img{i}")
+
+
+@pytest.mark.parametrize("probe", ["ok", "fail"])
+def test_unaligned_rows_probe_fallback(gpu, oracle, rng, monkeypatch, probe):
+    """Rows whose pitch is not a multiple of 4 bytes leave k_rcol for k_rmf2, whose
+    staging relies on direct-to-LDS loads at unaligned byte offsets.  Each device
+    runs a probe of that behaviour once; MIPX_LDS_PROBE=fail makes the engine act as
+    on a device that fails it, so those rows take the aligned-only kernels.  Both
+    routes must give the oracle's bytes."""
+    monkeypatch.setenv("MIPX_LDS_PROBE", "fail" if probe == "fail" else "")
+    for h, w, hs in ((101, 1333, 1.6666666666666667), (99, 1331, 1.6), (23, 1, 1.3529411764705883), (40, 7, 2.4),
+                     (64, 333, 1.46484375)):
+        if int(w / hs + 0.5) < 1:
+            continue
+        imgs = np.stack([rand_img(rng, h, w, 3), smooth_img(rng, h, w, 3)])
+        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=hs)
+        for i in range(2):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, hs), f"probe={probe} {h}x{w}x3 /{hs} img{i}")

@@ -58,3 +58,27 @@ def c5_groups(reqs):
         key = (w, h, json.dumps(opts, sort_keys=True))
         buckets.setdefault(key, [0, opts])[0] += 1
     return [((w, h), opts, cnt) for (w, h, _), (cnt, opts) in sorted(buckets.items())]
+
+
+def shard_groups(groups, world, bytes_per_request):
+    """Split the plan groups [((w, h), opts, count)] over `world` ranks by bytes
+    (greedy, largest first), keeping each group on as few ranks as
+    possible: a group goes whole to the least-loaded rank while it fits under the
+    per-rank target, and only the part that does not fit spills to the next
+    least-loaded rank.  bytes_per_request((w, h), opts) is the request's input +
+    output bytes.  Returns one group list per rank, same form as the input."""
+    sized = [((w, h), opts, cnt, bytes_per_request((w, h), opts)) for (w, h), opts, cnt in groups]
+    total = sum(cnt * b for _, _, cnt, b in sized)
+    target = total / world
+    load = [0] * world
+    out = [[] for _ in range(world)]
+    for (w, h), opts, cnt, b in sorted(sized, key=lambda g: (-g[2] * g[3], g[0], str(sorted(g[1].items())))):
+        left = cnt
+        while left > 0:
+            r = min(range(world), key=lambda k: (load[k], k))
+            room = -int(-(target - load[r]) // b) if b else left  # ceil: a rank fills to the target once
+            take = left if room >= left else max(1, room)
+            out[r].append(((w, h), opts, take))
+            load[r] += take * b
+            left -= take
+    return out
