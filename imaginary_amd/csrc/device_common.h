@@ -114,6 +114,14 @@ MIPX_RN_OP(dmul_rn, double, *)
 MIPX_RN_OP(dadd_rn, double, +)
 #undef MIPX_RN_OP
 
+// libvips reduce sample position of output o (reducev.cpp / reduceh.cpp): the corner
+// convention X = o * shrink (the [U] default, PARITY_ASSUMPTIONS.md row 1) or, with
+// the centre switch, X = (o + 0.5) * shrink - 0.5; separately rounded double ops, as
+// oracle/vips_ref.c reduce_pos computes them
+__device__ __forceinline__ double reduce_x(int o, double s, int centre) {
+    return centre ? dadd_rn(dmul_rn(o + 0.5, s), -0.5) : dmul_rn(static_cast<double>(o), s);
+}
+
 }  // namespace dev
 
 // ---- host-side helpers shared by the launchers ----

@@ -12,6 +12,7 @@
 // clipped — all int32 (restated in oracle/vips_ref.c ref_affine).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "device_common.h"
@@ -41,6 +42,7 @@ __device__ __forceinline__ int extend_idx(int v, int n, int ext) {  // -1 = fill
 
 __device__ __forceinline__ double affine_pos(int o, double scale) { return (o + 0.5) / scale - 0.5 + 1.0; }
 __device__ __forceinline__ int ufr(int v) { return (v + (kInterpScale >> 1)) >> kInterpShift; }
+typedef short af_s2 __attribute__((ext_vector_type(2)));
 
 template <int B>
 __global__ void __launch_bounds__(256) k_affine(AffineArgs a) {
@@ -83,6 +85,157 @@ __global__ void __launch_bounds__(256) k_affine(AffineArgs a) {
         }
         const int v = ufr(cy[0] * r[0] + cy[1] * r[1] + cy[2] * r[2] + cy[3] * r[3]);
         q[c] = static_cast<u8>(clampi(v, 0, 255));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_affine_sep: the same bicubic, staged and separable.  bicubic.cpp's uchar path
+// rounds each of the 4 window rows before the vertical taps, so the result is
+// exactly rows -> columns: H[r][x] = ufr(sum_i cx(x)[i] in[r][ix(x) - 2 + i]) for
+// every input row r the tile's output rows read, then out[y][x] = clip(ufr(sum_j
+// cy(y)[j] H[iy(y) - 2 + j][x])).  A block = 256 output pixels x TY output rows:
+//   1. the input window (rows iy(y0) - 2 .. iy(y1) + 1, columns ix(x0) - 2 ..
+//      ix(x1) + 1, through the embed's extend mode) is staged in LDS as bytes;
+//   2. lane x makes H for its output pixel on every staged row (one dword read per
+//      4 staged bytes, v_dot2 on byte pairs against the packed int16 taps) into an
+//      int16 LDS image: H is shared by the ~4 / yscale output rows that read a row;
+//   3. each output row is 64 B dword columns: 4 ds_read_b64 of H (4 bytes x 4 rows),
+//      v_dot2 over row pairs, v_ashr_pk_u8_i32 rounding + clip, one dword store.
+// Positions in fp64 exactly as affine_pos (affine.c centre convention + 1).
+constexpr int kAfTX = 256;
+
+struct AffSepArgs {
+    const u8 *in;
+    u8 *out;
+    int w, h, ow, oh, extend, fill;
+    double xscale, yscale;
+    const int *tab;  // 129 x 4
+    long long in_img, out_img;
+    int ty;          // output rows per tile
+    int ncb;         // staged bytes per input row (multiple of 4)
+    int nr_max;      // staged rows capacity
+    int hs;          // int16 per H row (kAfTX * B, multiple of 4)
+    int out_aligned; // output rows start on a dword
+};
+
+__device__ __forceinline__ int af_ix(int o, double scale, int *phase) {
+    const double X = affine_pos(o, scale);
+    *phase = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
+    return static_cast<int>(X);
+}
+
+template <int B>
+__global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t afs[];
+    u8 *stg = reinterpret_cast<u8 *>(afs);                                       // [nr_max][ncb]
+    int16_t *hrow = reinterpret_cast<int16_t *>(stg + ((a.nr_max * a.ncb + 15) & ~15));  // [nr_max][hs]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int x0 = blockIdx.x * kAfTX, y0 = blockIdx.y * a.ty;
+    const int img = blockIdx.z;
+    const int x_last = min(x0 + kAfTX - 1, a.ow - 1), y_last = min(y0 + a.ty - 1, a.oh - 1);
+    int ph;
+    const int c0 = af_ix(x0, a.xscale, &ph) - 2, c1 = af_ix(x_last, a.xscale, &ph) + 1;
+    const int r0 = af_ix(y0, a.yscale, &ph) - 2, r1 = af_ix(y_last, a.yscale, &ph) + 1;
+    const int nr = r1 - r0 + 1, ncb = (c1 - c0 + 1) * B;
+    const u8 *src = a.in + img * a.in_img;
+    // ---- 1. stage the input window (extend mode at the borders) ----
+    const bool interior = c0 >= 0 && c1 < a.w && r0 >= 0 && r1 < a.h;
+    if (interior) {  // dword gathers: two aligned loads + v_alignbyte per staged dword
+        int delta = 0;
+        const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, &delta);
+        const int nd = (ncb + 3) >> 2;
+        for (int i = tid; i < nr * nd; i += 256) {
+            const int rr = i / nd, d = i - rr * nd;
+            const int off = delta + ((r0 + rr) * a.w + c0) * B + 4 * d;
+            const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, off & ~3, 0, 0);
+            const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, (off & ~3) + 4, 0, 0);
+            *reinterpret_cast<uint32_t *>(stg + rr * a.ncb + 4 * d) = __builtin_amdgcn_alignbyte(hi, lo, off & 3);
+        }
+    } else {
+        for (int i = tid; i < nr * ncb; i += 256) {
+            const int rr = i / ncb, cb = i - rr * ncb;
+            const int cp = cb / B, ch = cb - cp * B;
+            const int sr = extend_idx(r0 + rr, a.h, a.extend), sc = extend_idx(c0 + cp, a.w, a.extend);
+            stg[rr * a.ncb + cb] = (sr < 0 || sc < 0) ? static_cast<u8>(a.fill)
+                                                      : src[(static_cast<long long>(sr) * a.w + sc) * B + ch];
+        }
+    }
+    __syncthreads();
+    // ---- 2. horizontal pass: lane = output pixel x0 + tid, every staged row ----
+    {
+        const int x = x0 + tid;
+        int tx;
+        const int ix = af_ix(min(x, x_last), a.xscale, &tx);
+        const int *cx = a.tab + tx * 4;
+        const uint32_t c01 = (static_cast<uint32_t>(cx[0]) & 0xffffu) | (static_cast<uint32_t>(cx[1]) << 16);
+        const uint32_t c23 = (static_cast<uint32_t>(cx[2]) & 0xffffu) | (static_cast<uint32_t>(cx[3]) << 16);
+        const int sb = (ix - 2 - c0) * B;  // staged byte of tap 0, channel 0
+        const int sh = sb & 3;
+        constexpr int ND = B + 1;          // dwords covering 4 B bytes from any alignment
+        for (int rr = 0; rr < nr; ++rr) {
+            const uint32_t *sp = reinterpret_cast<const uint32_t *>(stg + rr * a.ncb + (sb & ~3));
+            uint32_t v[ND], t[B];
+#pragma unroll
+            for (int k = 0; k < ND; ++k) v[k] = sp[k];
+#pragma unroll
+            for (int k = 0; k < B; ++k) t[k] = __builtin_amdgcn_alignbyte(v[k + 1], v[k], sh);
+            const u8 *tb = reinterpret_cast<const u8 *>(t);
+            int16_t hv[B];
+#pragma unroll
+            for (int c = 0; c < B; ++c) {
+                // byte pairs (tap 0, 1) and (2, 3) of channel c, zero-extended to int16
+                const uint32_t p01 = static_cast<uint32_t>(tb[c]) | (static_cast<uint32_t>(tb[c + B]) << 16);
+                const uint32_t p23 = static_cast<uint32_t>(tb[c + 2 * B]) | (static_cast<uint32_t>(tb[c + 3 * B]) << 16);
+                int acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, p01), __builtin_bit_cast(af_s2, c01), 2048, false);
+                acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, p23), __builtin_bit_cast(af_s2, c23), acc, false);
+                hv[c] = static_cast<int16_t>(acc >> 12);
+            }
+            int16_t *hq = hrow + rr * a.hs + tid * B;
+#pragma unroll
+            for (int c = 0; c < B; ++c) hq[c] = hv[c];
+        }
+    }
+    __syncthreads();
+    // ---- 3. vertical pass: wave rows y0 + wave, + 4, ...; lane dword columns lane + 64 k ----
+    u8 *ob = a.out + img * a.out_img;
+    const int vbytes = (x_last - x0 + 1) * B;
+    for (int y = y0 + wave; y <= y_last; y += 4) {
+        int ty;
+        const int iy = af_ix(y, a.yscale, &ty);
+        const int *cy = a.tab + ty * 4;
+        const uint32_t y01 = (static_cast<uint32_t>(cy[0]) & 0xffffu) | (static_cast<uint32_t>(cy[1]) << 16);
+        const uint32_t y23 = (static_cast<uint32_t>(cy[2]) & 0xffffu) | (static_cast<uint32_t>(cy[3]) << 16);
+        const int16_t *h0 = hrow + (iy - 2 - r0) * a.hs;
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const int d = lane + 64 * k;
+            if (4 * d >= vbytes) continue;
+            uint2 q[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const uint2 *>(h0 + j * a.hs + 4 * d);
+            int acc[4];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t lo0 = b < 2 ? q[0].x : q[0].y, lo1 = b < 2 ? q[1].x : q[1].y;
+                const uint32_t lo2 = b < 2 ? q[2].x : q[2].y, lo3 = b < 2 ? q[3].x : q[3].y;
+                const uint32_t sel = (b & 1) ? 0x07060302u : 0x05040100u;  // the int16 of byte b from each row
+                const uint32_t r01 = __builtin_amdgcn_perm(lo1, lo0, sel), r23 = __builtin_amdgcn_perm(lo3, lo2, sel);
+                int s0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, r01), __builtin_bit_cast(af_s2, y01), 2048, false);
+                acc[b] = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, r23), __builtin_bit_cast(af_s2, y23), s0, false);
+            }
+            uint32_t lo, hi;
+            asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(acc[0]), "v"(acc[1]));
+            asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(acc[2]), "v"(acc[3]));
+            const uint32_t o = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            const long long qo = (static_cast<long long>(y) * a.ow + x0) * B + 4 * d;
+            if (a.out_aligned && 4 * d + 4 <= vbytes) {
+                *reinterpret_cast<uint32_t *>(ob + qo) = o;
+            } else {
+                for (int b = 0; b < 4; ++b)
+                    if (4 * d + b < vbytes) ob[qo + b] = static_cast<u8>(o >> (8 * b));
+            }
+        }
     }
 }
 
@@ -134,6 +287,34 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
     if (!a.tab) return MIPX_EDEVICE;
     a.in_img = img_bytes(w, h, b);
     a.out_img = img_bytes(a.ow, a.oh, b);
+    if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
+    // the staged separable kernel: window spans from the positions, exact per tile size
+    const char *es = tune_env("MIPX_AFFINE_SEP");  // 0: the per-pixel gather kernel (A/B)
+    if (!(es && *es == '0') && n <= 65535) {
+        auto ixh = [](int o, double s) { return static_cast<int>((o + 0.5) / s - 0.5 + 1.0); };
+        for (const int ty : {32, 16, 8}) {
+            int ncols = 0, nrows = 0;
+            for (int x0 = 0; x0 < a.ow; x0 += kAfTX)
+                ncols = std::max(ncols, ixh(std::min(x0 + kAfTX, a.ow) - 1, xs) - ixh(x0, xs) + 4);
+            for (int y0 = 0; y0 < a.oh; y0 += ty)
+                nrows = std::max(nrows, ixh(std::min(y0 + ty, a.oh) - 1, ys) - ixh(y0, ys) + 4);
+            AffSepArgs g{};
+            g.in = in, g.out = out, g.w = w, g.h = h, g.ow = a.ow, g.oh = a.oh, g.extend = a.extend, g.fill = a.fill;
+            g.xscale = xs, g.yscale = ys, g.tab = a.tab, g.in_img = a.in_img, g.out_img = a.out_img;
+            g.ty = ty;
+            g.ncb = (ncols * b + 4 + 3) & ~3;  // + a dword: the horizontal pass reads B + 1 dwords
+            g.nr_max = nrows;
+            g.hs = kAfTX * b;
+            g.out_aligned = (a.ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
+            const size_t lds = ((static_cast<size_t>(g.nr_max) * g.ncb + 15) & ~size_t(15)) + static_cast<size_t>(g.nr_max) * g.hs * 2;
+            if (lds > 40 * 1024 || ncols * b > 4 * 4096) continue;
+            const long long ytiles = (a.oh + ty - 1) / ty;
+            if (ytiles > 65535) continue;
+            const dim3 grid((a.ow + kAfTX - 1) / kAfTX, static_cast<unsigned>(ytiles), n);
+            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_affine_sep<B_>, grid, dim3(256), lds, st, g));
+            return launch_check("k_affine_sep");
+        }
+    }
     if (a.oh > 65535) return MIPX_EUNSUPPORTED;
     const dim3 grid((a.ow + 255) / 256, a.oh, n);
     MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_affine<B_>, grid, dim3(256), 0, st, a));

@@ -262,15 +262,25 @@ __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8
 // contiguous run of tiles (neighbouring tiles share the 128-byte lines that a
 // 3-band tile edge splits, in one L2) instead of round robin.  TH: input rows
 // per tile (= contiguous output pixels per output row of the tile).
-template <int B, bool CW, int TH>
+template <int B, bool CW, int TH, int T>
 __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
-                                                   long long img_bytes_, int tiles_x, int tiles_y, int xcd, int q16) {
-    constexpr int T = 64;
+                                                   long long img_bytes_, int tiles_x, int tiles_y, int xcd, int q16,
+                                                   int yfast) {
     constexpr int RS = (T * B + 3) / 4 + 1;  // dwords per staged row (+1: the unaligned pixel read spills)
     __shared__ uint32_t tile[TH * RS];
     const uint32_t t = xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-    const int bx = static_cast<int>(t % tiles_x), rest = static_cast<int>(t / tiles_x);
-    const int by = rest % tiles_y, img = rest / tiles_y;
+    // yfast: consecutive blocks take consecutive input row bands = neighbouring output
+    // column ranges of the same output rows, so split output lines complete in one L2
+    int bx, by, img;
+    if (yfast) {
+        by = static_cast<int>(t % tiles_y);
+        const int rest = static_cast<int>(t / tiles_y);
+        bx = rest % tiles_x, img = rest / tiles_x;
+    } else {
+        bx = static_cast<int>(t % tiles_x);
+        const int rest = static_cast<int>(t / tiles_x);
+        by = rest % tiles_y, img = rest / tiles_y;
+    }
     const int tx0 = bx * T, ty0 = by * TH;  // input tile origin
     const int tw = min(T, w - tx0), th = min(TH, h - ty0);
     int delta = 0;
@@ -543,7 +553,16 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
     if ((angle == 90 || angle == 270) && img_bytes(w, h, b) < 0x7fffffffLL) {
         const char *eth = tune_env("MIPX_ROT_TH");
         const int th = eth && *eth ? (std::atoi(eth) == 128 ? 128 : 64) : 64;
-        const int tx = (w + 63) / 64, ty = (h + th - 1) / th;
+        // r03 A/B (profiles/r03/rot_ab.jsonl, same process): input rows a whole number of
+        // 128-byte lines (1080p / 4K RGB, 4K RGBA) rotate fastest with 64-column tiles taken
+        // row-band fastest (+4 / +9 / +8 %), rows that end mid-line (12 MP RGB: 12000 B)
+        // with 128-column tiles column-fastest (+47 %)
+        const bool line_rows = (static_cast<long long>(w) * b) % 128 == 0;
+        const char *etc = tune_env("MIPX_ROT_T");  // input columns per tile: 64 / 128 (A/B)
+        const int tc = th == 64 && (etc && *etc ? std::atoi(etc) == 128 : !line_rows) ? 128 : 64;
+        const char *eo = tune_env("MIPX_ROT_ORDER");  // 1: input row bands fastest (A/B)
+        const int yfast = eo && *eo ? *eo == '1' : line_rows;
+        const int tx = (w + tc - 1) / tc, ty = (h + th - 1) / th;
         const long long nblk = static_cast<long long>(tx) * ty * n;
         if (nblk > 0x7fffffffLL) return MIPX_EUNSUPPORTED;
         const dim3 grid(static_cast<unsigned>(nblk));
@@ -554,13 +573,15 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
         const int xcd = ex && *ex ? (*ex != '0') : ((64 * b) % 128 != 0);
         const char *eq = tune_env("MIPX_ROT_Q16");  // A/B: 0 keeps the b64-per-dword staging
         const int q16 = !(eq && *eq == '0');
-#define MIPX_ROT(CW_, TH_)                                                                                     \
-    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, CW_, TH_>), grid, dim3(256), 0, st, in, out, w, h, ib, \
-                                              tx, ty, xcd, q16))
+#define MIPX_ROT(CW_, TH_, T_)                                                                                 \
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90_lds<B_, CW_, TH_, T_>), grid, dim3(256), 0, st, in, out, w, h, \
+                                              ib, tx, ty, xcd, q16, yfast))
         if (th == 128) {
-            if (angle == 90) { MIPX_ROT(true, 128); } else { MIPX_ROT(false, 128); }
+            if (angle == 90) { MIPX_ROT(true, 128, 64); } else { MIPX_ROT(false, 128, 64); }
+        } else if (tc == 128) {
+            if (angle == 90) { MIPX_ROT(true, 64, 128); } else { MIPX_ROT(false, 64, 128); }
         } else {
-            if (angle == 90) { MIPX_ROT(true, 64); } else { MIPX_ROT(false, 64); }
+            if (angle == 90) { MIPX_ROT(true, 64, 64); } else { MIPX_ROT(false, 64, 64); }
         }
 #undef MIPX_ROT
         return launch_check("k_rot90_lds");

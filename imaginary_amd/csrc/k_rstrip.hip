@@ -55,8 +55,8 @@ __device__ __forceinline__ uint32_t rnd12(int sum) {
 }
 // libvips reduce geometry: output o samples X = o * shrink, taps from
 // floor(X) - (n/2 - 1), phase ((int(X * 256) & 255) + 1) >> 1 (reduceh.cpp)
-__device__ __forceinline__ void rs_position(double shrink, int pad, int o, int *start, int *phase) {
-    const double X = o * shrink;
+__device__ __forceinline__ void rs_position(double shrink, int pad, int o, int *start, int *phase, int centre) {
+    const double X = reduce_x(o, shrink, centre);
     *start = static_cast<int>(X) - pad;
     *phase = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
 }
@@ -75,6 +75,7 @@ struct RsArgs {
     int tv, th, padv, padh;
     int tpav, tpah;              // pair-table width (taps / 2 + 1)
     double vs, hs;
+    int centre;                  // MIPX_REDUCE_CENTRE
     const uint32_t *vpairs, *hpairs;  // [129][2][tpa] int16 tap pairs
     int diag;                    // A/B diagnostic (MIPX_RSTRIP_DIAG): 1 skip vertical, 2 skip horizontal
 };
@@ -111,8 +112,8 @@ __global__ void __launch_bounds__(kRsThreads) k_rstrip(RsArgs a) {
     const int x0 = strip * TW;
     const int nx = min(TW, a.ow - x0);
     int lo, hi, ph;
-    rs_position(a.hs, a.padh, a.ox0 + x0, &lo, &ph);
-    rs_position(a.hs, a.padh, a.ox0 + x0 + nx - 1, &hi, &ph);
+    rs_position(a.hs, a.padh, a.ox0 + x0, &lo, &ph, a.centre);
+    rs_position(a.hs, a.padh, a.ox0 + x0 + nx - 1, &hi, &ph, a.centre);
     hi += a.th - 1;
     const int org = lo & ~3;                            // pixel of slot 0 (floor to 4)
     const int cl4 = max(lo, 0) & ~3;                     // first staged pixel
@@ -126,7 +127,7 @@ __global__ void __launch_bounds__(kRsThreads) k_rstrip(RsArgs a) {
     const int tpv = (a.tv + 2) >> 1;                     // pairs a row can touch at either alignment
     auto first_pos = [&](int y) {
         int s, p;
-        rs_position(a.vs, a.padv, a.oy0 + y, &s, &p);
+        rs_position(a.vs, a.padv, a.oy0 + y, &s, &p, a.centre);
         return s;
     };
     auto end_pos = [&](int y0c) {  // exclusive end of the input positions chunk y0c reads
@@ -174,7 +175,7 @@ __global__ void __launch_bounds__(kRsThreads) k_rstrip(RsArgs a) {
     uint32_t hc[kRsMaxTP];
     {
         int s, p;
-        rs_position(a.hs, a.padh, a.ox0 + x0 + min(xl, nx - 1), &s, &p);
+        rs_position(a.hs, a.padh, a.ox0 + x0 + min(xl, nx - 1), &s, &p, a.centre);
         hbase = s - org;
         const uint32_t *c = a.hpairs + static_cast<size_t>(p) * 2 * a.tpah;  // alignment 0
 #pragma unroll
@@ -213,8 +214,8 @@ __global__ void __launch_bounds__(kRsThreads) k_rstrip(RsArgs a) {
             if (y0r < yb1) {
                 const bool two = y0r + 1 < yb1;
                 int s0, p0, s1, p1;
-                rs_position(a.vs, a.padv, a.oy0 + y0r, &s0, &p0);
-                rs_position(a.vs, a.padv, a.oy0 + y0r + (two ? 1 : 0), &s1, &p1);
+                rs_position(a.vs, a.padv, a.oy0 + y0r, &s0, &p0, a.centre);
+                rs_position(a.vs, a.padv, a.oy0 + y0r + (two ? 1 : 0), &s1, &p1, a.centre);
                 const int j0 = s0 >> 1;                      // first aligned pair (2j0, 2j0 + 1)
                 const int d1 = (s1 >> 1) - j0;               // row 1's first pair, relative (0..2)
                 const int np = d1 + tpv;                     // pairs either row touches
@@ -421,6 +422,7 @@ int reduce_strip_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
     a.padh = a.th / 2 - 1;
     a.vs = vs;
     a.hs = hs;
+    a.centre = reduce_centre();
     const char *edg = tune_env("MIPX_RSTRIP_DIAG");
     a.diag = (edg && *edg) ? std::atoi(edg) : 0;
     // every row of every image starts dword aligned: no per-row byte skew

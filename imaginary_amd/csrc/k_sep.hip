@@ -41,6 +41,7 @@ struct SepTaps {
     float rounding, inv_scale;  // conv rounding
     int dot;                 // integer dot paths (MIPX_SEP_DOT=0 selects the float path)
     int tq;                  // conv vpass: rows transposed once per 4-row quad (MIPX_SEP_TQ=0: per output row)
+    int centre;              // reduce: centre sampling convention (MIPX_REDUCE_CENTRE=1)
 };
 
 constexpr int kVpPairs = 8;     // tap pairs of the unrolled vertical reduce (taps <= 16: shrink < 2.75)
@@ -89,7 +90,7 @@ __device__ __forceinline__ uint32_t pack_taps(const float *c, int taps, int q) {
 
 __device__ __forceinline__ void sep_position(const SepTaps &t, int o, int *start, int *phase) {
     if (t.phased) {
-        const double X = o * t.shrink;
+        const double X = reduce_x(o, t.shrink, t.centre);
         *start = static_cast<int>(X) - t.pad;
         *phase = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
     } else {
@@ -1496,7 +1497,8 @@ SepTaps make_taps(const SepSpec &s) {
     const char *e = tune_env("MIPX_SEP_DOT");
     t.dot = !(e && *e == '0');
     const char *eq = tune_env("MIPX_SEP_TQ");
-    t.tq = !(eq && *eq == '0') && s.taps >= 7;  // 3-tap masks lose to the transpose (v14/ab_conv_quad_transpose.log)
+    t.tq = !(eq && *eq == '0') && s.taps >= 7;
+    t.centre = t.phased && reduce_centre();  // 3-tap masks lose to the transpose (v14/ab_conv_quad_transpose.log)
     return t;
 }
 

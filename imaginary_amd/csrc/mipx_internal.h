@@ -26,6 +26,10 @@ int hip_fail(hipError_t e, const char *what);  // records detail, returns MIPX_E
 // mipx_tuning_reload): nullptr when unset.  Launchers call this, never getenv.
 const char *tune_env(const char *name);
 void tune_reload();
+// MIPX_REDUCE_CENTRE=1: every Lanczos reduce samples output o at (o + 0.5) * shrink - 0.5
+// (libvips' centre convention) instead of o * shrink (PARITY_ASSUMPTIONS.md row 1)
+bool reduce_centre();
+inline double reduce_x_host(int o, double s, bool centre) { return centre ? (o + 0.5) * s - 0.5 : o * s; }
 
 // ---- device capability probes (k_probe.hip), run once per device -------------
 // Do direct-to-LDS dword buffer loads honour byte offsets that are not multiples of 4?
@@ -72,6 +76,8 @@ constexpr int kRsTabPad = 128;  // k_rmf4 stride-B tap rows: zero bytes in front
 constexpr int kRsTabW = 272;    // bytes per (phase, hi / lo) row: pad + 2 K steps + a fragment (70 KB per table)
 const signed char *device_reduce_i8(double shrink, int *n_taps, const int **sums);
 const signed char *device_reduce_i8s(double shrink, int bands, int *n_taps);  // taps at a byte stride of bands
+// the same with the COPY edge folded in: [2 sides][taps - 1][129][hi, lo][kRsTabW] (k_rcol)
+const signed char *device_reduce_i8s_fold(double shrink, int bands, int *n_taps);
 // k_bmf's i8 MFMA operands for a blur mask (cached per device): [nks][64][16]
 // horizontal taps at byte stride `bands` shifted by delta, then [64][16] vertical taps
 const signed char *device_blur_ops(const std::vector<int> &mask, int bands, int delta, int nks);

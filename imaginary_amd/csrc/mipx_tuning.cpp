@@ -57,6 +57,11 @@ const char *tune_env(const char *name) {
     return it == s->kv.end() ? nullptr : it->second.c_str();
 }
 
+bool reduce_centre() {
+    const char *e = tune_env("MIPX_REDUCE_CENTRE");
+    return e && *e == '1';
+}
+
 void tune_reload() {
     std::lock_guard<std::mutex> lk(g_mu);
     take_snapshot_locked();

@@ -15,6 +15,7 @@ times = {i: [] for i in range(len(configs))}
 for rnd in range(5):
     for i, cfg in enumerate(configs):
         os.environ.update(cfg)
+        lib.mipx_tuning_reload()  # the library snapshots MIPX_* knobs
         check(lib.mipx_op_reduce(x.data_ptr(), y.data_ptr(), n, W, H, B, 2.0, 2.0, None, 0, sp), "r")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)

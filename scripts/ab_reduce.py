@@ -36,6 +36,7 @@ sp = C.c_void_p(st.cuda_stream)
 
 def run(var, nimg=n):
     os.environ["MIPX_R2_VARIANT"] = str(var)
+    lib.mipx_tuning_reload()  # the library snapshots MIPX_* knobs
     check(lib.mipx_op_reduce(x.data_ptr(), y.data_ptr(), nimg, W, H, bands, 2.0, 2.0, None, 0, sp), "reduce")
 
 

@@ -3,7 +3,7 @@
 rocprofv3 passes see that kernel alone.
 
     python scripts/op_bench.py reducev --w 1024 --h 1024 --b 4 --n 512 --s 1.3333333333333333
-    ops: reduce reducev reduceh shrink blur embed rot flip extract
+    ops: reduce reducev reduceh shrink blur embed rot flip extract affine zoom
 """
 import argparse
 import ctypes as C
@@ -46,6 +46,11 @@ def main():
         oh = vips_round(h / s2) if a.op != "reduceh" else h
     elif a.op == "shrink":
         ow, oh = max(1, vips_round(w / a.s)), max(1, vips_round(h / s2))
+    elif a.op == "affine":
+        import math
+        ow, oh = math.ceil(w * a.s), math.ceil(h * s2)
+    elif a.op == "zoom":
+        ow, oh = w * int(a.s), h * int(s2)
     elif a.op == "rot":
         ow, oh = (h, w) if int(a.s) % 180 == 90 else (w, h)
     elif a.op in ("embed", "extract"):
@@ -79,6 +84,10 @@ def main():
             return lib.mipx_op_rot(X, Y, n, w, h, b, int(a.s), sp)
         if a.op == "flip":
             return lib.mipx_op_flip(X, Y, n, w, h, b, int(a.s), sp)
+        if a.op == "affine":
+            return lib.mipx_op_affine(X, Y, n, w, h, b, a.s, s2, a.extend, sp)
+        if a.op == "zoom":
+            return lib.mipx_op_zoom(X, Y, n, w, h, b, int(a.s), int(s2), sp)
         raise SystemExit(a.op)
 
     check(run(), a.op)

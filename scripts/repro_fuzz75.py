@@ -13,6 +13,7 @@ for env in [{}, {"MIPX_RMF2_UNALIGNED": "0"}, {"MIPX_RMF2_ORG": "16"}, {"MIPX_RM
     for k in ("MIPX_RMF2_UNALIGNED", "MIPX_RMF2_ORG", "MIPX_RMFMA", "MIPX_RMF2_HT"):
         os.environ.pop(k, None)
     os.environ.update(env)
+    ia.lib.mipx_tuning_reload()  # the library snapshots MIPX_* knobs
     got = ia.execute(p, imgs)
     bad = [int((got[i] != oracle.execute(rp, imgs[i])).sum()) for i in range(2)]
     print(json.dumps({"env": env, "bytes_differ": bad}))
@@ -22,6 +23,7 @@ for env in [{}, {"MIPX_RMF2_UNALIGNED": "0"}, {"MIPX_RMF2_ORG": "16"}]:
     for k in ("MIPX_RMF2_UNALIGNED", "MIPX_RMF2_ORG"):
         os.environ.pop(k, None)
     os.environ.update(env)
+    ia.lib.mipx_tuning_reload()  # the library snapshots MIPX_* knobs
     g = ia.run_op("reduce", x, hshrink=1.3529411764705883, vshrink=1.3529411764705883)
     bad = [int((g[i] != oracle.reduce(x[i], 1.3529411764705883, 1.3529411764705883)).sum()) for i in range(3)]
     print(json.dumps({"reduce_1x23": env, "bytes_differ": bad}))

@@ -30,6 +30,7 @@ def main():
             for rep in range(2):
                 for v in variants:
                     os.environ.update(v)
+                    lib.mipx_tuning_reload()  # the library snapshots MIPX_* knobs
 
                     def run():
                         check(lib.mipx_op_rot(x.data_ptr(), y.data_ptr(), n, w, h, b, ang, sp))

@@ -59,6 +59,7 @@ def main():
         for rep in range(2):
             for v in variants:
                 os.environ.update(v)
+                lib.mipx_tuning_reload()  # the library snapshots MIPX_* knobs
                 def run():
                     check(lib.mipx_op_reduce(x.data_ptr(), y.data_ptr(), n, w, h, b, hs, vs, ws.data_ptr(), wsb, sp))
                 for _ in range(3):

@@ -199,14 +199,18 @@ def test_rot_tiles_and_aligned_extract(gpu, oracle, rng, h, w, b):
                     oracle.extract(img, left, top, ew, eh), f"extract {left},{top}")
 
 
-@pytest.mark.parametrize("th", ["64", "128"])
+@pytest.mark.parametrize("th,tc,order", [("64", "64", "0"), ("128", "64", "0"), ("64", "128", "0"), ("64", "64", "1"),
+                                          ("64", "128", "1")])
 @pytest.mark.parametrize("xcd", ["1", "0"])
-def test_rot90_tile_orders(gpu, oracle, rng, monkeypatch, xcd, th):
-    """The 64x64-tile rotation on its flat grid, XCD-contiguous (default for odd band counts) or x-fastest
-    round robin (MIPX_ROT_XCD=0), 64 or 128 input rows per tile
-    (MIPX_ROT_TH): a batch of 3 with ragged edge tiles, every band count."""
+def test_rot90_tile_orders(gpu, oracle, rng, monkeypatch, xcd, th, tc, order):
+    """The LDS-tile rotation on its flat grid, XCD-contiguous (default for odd band counts) or x-fastest
+    round robin (MIPX_ROT_XCD=0), 64 or 128 input rows per tile (MIPX_ROT_TH), 64 or 128
+    input columns per tile (MIPX_ROT_T), tiles x- or y-fastest (MIPX_ROT_ORDER): a batch of
+    3 with ragged edge tiles, every band count."""
     monkeypatch.setenv("MIPX_ROT_XCD", xcd)
     monkeypatch.setenv("MIPX_ROT_TH", th)
+    monkeypatch.setenv("MIPX_ROT_T", tc)
+    monkeypatch.setenv("MIPX_ROT_ORDER", order)
     for h, w, b in ((130, 197, 3), (65, 300, 4), (200, 129, 1), (67, 131, 2), (261, 70, 4)):
         imgs = np.stack([rand_img(rng, h, w, b) for _ in range(3)])
         for a in (90, 270):

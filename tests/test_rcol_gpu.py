@@ -12,6 +12,14 @@ from test_parity_gpu import assert_same, rand_img, smooth_img
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True, params=["rcol", "default"])
+def route(request, monkeypatch):
+    """k_rcol is opt-in (MIPX_RCOL=1) while it measures slower than k_rmf2; every case
+    runs through it and through the default route."""
+    monkeypatch.setenv("MIPX_RCOL", "1" if request.param == "rcol" else "")
+    yield request.param
+
 SHRINKS = [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9), (2.7, 1.5),
            (1.46484375, 1.46484375), (1.1, 1.05), (1.6, 1.5976331360946747), (2.0, 1.25), (1.25, 2.0)]
 SHAPES = [(301, 1100, 3), (97, 640, 3), (13, 200, 3), (40, 36, 3), (270, 480, 3), (37, 1028, 3), (150, 96, 3),
@@ -80,3 +88,36 @@ def test_unaligned_rows_probe_fallback(gpu, oracle, rng, monkeypatch, probe):
         got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=hs)
         for i in range(2):
             assert_same(got[i], oracle.reduce(imgs[i], hs, hs), f"probe={probe} {h}x{w}x3 /{hs} img{i}")
+
+
+@pytest.fixture
+def centre(oracle, monkeypatch):
+    """PARITY_ASSUMPTIONS.md row 1 flipped: libvips' centre sampling convention
+    (X = (o + 0.5) * shrink - 0.5) in the engine (MIPX_REDUCE_CENTRE=1) and the oracle."""
+    monkeypatch.setenv("MIPX_REDUCE_CENTRE", "1")
+    oracle.set_switch("reduce_centre", 1)
+    yield
+    oracle.set_switch("reduce_centre", 0)
+
+
+def test_reduce_centre_c2_c1_shapes(gpu, oracle, rng, centre):
+    """C2 (4K RGB -> 1080p, shrink 2: the fused 2x2 kernel steps aside, every output sits
+    at phase 64) and C1's 480x270 -> 300x169, plus the kernels behind k_rcol (unaligned
+    rows: k_rmf2; one axis: the separable passes) and a windowed plan."""
+    for h, w, b, hs, vs in ((2160, 3840, 3, 2.0, 2.0), (270, 480, 3, 1.6, 1.5976331360946747),
+                            (375, 500, 3, 1.46484375, 1.46484375), (301, 1333, 3, 1.6666666666666667, 1.6666666666666667),
+                            (200, 300, 4, 1.3333333333333333, 1.3333333333333333), (97, 640, 3, 2.4, 1.0),
+                            (33, 17, 3, 1.0, 2.5)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+        for i in range(2):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"centre {h}x{w}x{b} {hs}x{vs} img{i}")
+    for (iw, ih, b, opts) in ((1500, 1000, 3, dict(width=333, height=171, crop=1)),
+                              (2048, 2048, 4, dict(width=1024)), (1920, 1080, 3, dict(width=300))):
+        p = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(iw, ih, b, "png"))
+        e, rp = oracle.plan(opts, dict(w=iw, h=ih, bands=b, type=3))
+        assert e == 0
+        imgs = rng.integers(0, 256, (2, ih, iw, b), dtype=np.uint8)
+        got = gpu.execute(p, imgs)
+        for i in range(2):
+            assert_same(got[i], oracle.execute(rp, imgs[i]), f"centre plan {iw}x{ih}x{b} {opts}")
