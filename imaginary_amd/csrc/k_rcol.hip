@@ -1,28 +1,32 @@
 // k_rcol.hip — the generic Lanczos3 reduce (libvips vips_reduce: reducev then
-// reduceh, both shrinks in (1, 2.75), <= 16 taps each way) as a column walker on
+// reduceh, both shrinks in (1, ~2.5], <= 16 taps each way) as a column walker on
 // the i8 matrix cores.
 //
-// A block owns one strip of XW output pixels of one image and walks a segment of
-// its output rows down the image, 16 rows per step:
-//   * the input rows a step needs live in an LDS ring; each input row is loaded
-//     once per segment (the vertical halo of a step is the previous step's rows),
-//     by buffer loads into registers issued one step ahead and written to the ring
-//     at the top of the next step, so the row loads overlap the block's own work;
-//   * the vertical pass is k_rmf2's: per 16-byte column tile D[byte][row] =
-//     A[byte][staged row] x B[staged row][row] on v_mfma_i32_16x16x64_i8, A from
-//     two ds_read_b64_tr_b8, the 12-bit taps split c = 64 hi + lo, pixels as
-//     p - 128 with the offset returned in the seed; the uchar intermediate goes to
-//     LDS row-major (interleaved channels, still - 128);
-//   * the horizontal pass runs on the interleaved bytes (no channel planes): a
-//     unit is 16 consecutive output bytes x 16 rows, output byte o = B x + c takes
-//     tap k at intermediate byte B (start(x) + k - org) + c, so its operand row is
-//     a 16-byte window of the stride-B tap table (device_reduce_i8s).  These
-//     operands depend on the column only, so they are loaded once per segment
-//     and held in registers for every step; each step costs two ds_read_b64 and
-//     two MFMAs per unit and K step, and the result is one output dword per lane.
-// The COPY edge: rows clamp at the load; columns outside the image are gathered
-// from the edge pixel at the load (only the chunks that hold them), so the
-// vertical pass already produces the edge-extended intermediate.
+// A block (4 waves) owns one strip of 64 output pixels of one image and walks a
+// segment of its output rows down the image, 16 rows per step.  Steps sit on
+// absolute 16-row groups of the op output (rows outside the window are computed and
+// not stored), so every per-row quantity of the vertical pass comes from one
+// per-shrink table (device_rcol_vplan): the step's first and end input rows, and per
+// output row its vertical taps already placed at their K positions relative to the
+// step's first row, split c = 64 hi + lo, plus the accumulator seed.  The loop does
+// no position arithmetic.
+//   * ring: the input rows a step reads live in an LDS ring of 32 / 64 rows (slot =
+//     row & (ring - 1)).  Each input row is loaded once per segment: 16-byte chunks
+//     dealt over the block's 256 lanes (the same lane -> (row, column) map every
+//     step), loaded to registers two steps ahead (buffer loads, compiler-counted
+//     vmcnt), flipped to pixel - 128 and written to the ring at the top of their step;
+//   * vertical: per 16-byte column tile D[byte][row] = A[byte][ring row] x
+//     B[ring row][row] on v_mfma_i32_16x16x64_i8, A from two ds_read_b64_tr_b8, B the
+//     table's tap fragments (registers, loaded with the ring chunks); the result is
+//     the uchar intermediate - 128 (v_ashr_pk_i8_i32), row-major in LDS;
+//   * horizontal: on the interleaved bytes, a unit is 16 consecutive output bytes x
+//     16 rows, output byte o = B x + c takes tap k at intermediate byte
+//     B (start(x) + k - org) + c; those operands depend on the column only and are
+//     held in registers for the whole segment (the COPY edge folded in at the image
+//     edges), as are the per-byte seeds.  Two ds_read_b64 and two MFMAs per unit and
+//     K step, one output dword per lane, stored straight from registers.
+// Loads past the image read zeros (buffer range check); rows clamp at the load (COPY
+// edge); columns past the image carry zero weight after the fold.
 //
 // Results are bit-identical to reducev -> reduceh (oracle/vips_ref.c): the same
 // integer sums in int32, the same rounding (>> 12 with 2048 folded into the seed)
@@ -44,8 +48,10 @@ using namespace dev;
 typedef int rc_v4i __attribute__((ext_vector_type(4)));
 typedef int rc_v2i __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void rc_lds_void;
+typedef const __attribute__((address_space(4))) int rc_cint;
 
 constexpr int kRcRows = 16;   // output rows per step (the MFMA N)
+constexpr int kRcNT = 256;    // threads per block (4 waves, 64-pixel strips)
 
 struct RcArgs {
     const u8 *in;
@@ -54,20 +60,19 @@ struct RcArgs {
     int ox0, oy0, ow, oh;     // output window (op-output coordinates) and its size
     long long in_img, out_img;
     int strips, segs, seg_steps;
-    int ring;                 // ring rows: a multiple of 16, >= the rows one step reads
-    int rs;                   // ring row stride in dwords ((rs mod 64) / 4 odd)
+    int k0, ksteps;           // the window's first 16-row group (oy0 / 16) and group count
+    int rmask;                // ring rows - 1 (31 or 63)
+    int rs;                   // ring row stride in bytes ((rs / 4 mod 64) / 4 odd)
     int iw;                   // intermediate row stride in bytes
-    int vtaps, vpad, htaps, hpad;
-    double vs, hs;
-    const signed char *tabv;  // device_reduce_i8(vs): [129][hi, lo][kHmTabW]
-    const int *sumv;          // its per-phase tap sums
+    int htaps, hpad;
+    double hs;
+    const u8 *plan;           // device_rcol_vplan(vs): [plan_rows][kRcolPlanRow], then [plan_rows / 16][2] ints
+    int plan_rows;
     const signed char *tabh;  // device_reduce_i8s(hs, B): [129][hi, lo][kRsTabW]
-    const int *sumh;
+    const int *sumh;          // device_reduce_i8(hs) per-phase tap sums
     const float *tabf;        // device_reduce_table(hs): [129][htaps] (edge operands, narrow images)
     const signed char *tabhf; // device_reduce_i8s_fold(hs, B): the COPY edge folded in
-    int out_aligned;          // every output row starts on a dword
     int centre;               // MIPX_REDUCE_CENTRE: centre sampling convention
-    unsigned long long *stamps;  // diagnostic (MIPX_RCOL_STAMPS=1): per block, cycles per step phase
 };
 
 // libvips reduce position (reducev.cpp / reduceh.cpp): X = reduce_x (o * shrink, or
@@ -80,20 +85,9 @@ __device__ __forceinline__ void rc_pos(int o, double s, int pad, int *start, int
 
 // Workgroup barrier for LDS data: this wave's LDS reads and writes complete, then
 // s_barrier; the "memory" clobber keeps the compiler from moving memory accesses across
-// it.  Not the fence builtins: with direct-to-LDS loads in flight, an LDS release fence
-// makes the compiler drain vmcnt(0) — every load of the next steps (their ring rows go to
-// slots nobody reads before a later counted wait).
+// it.  Not __syncthreads(): its workgroup release fence would drain vmcnt(0), i.e. wait
+// for the ring loads of the next two steps, which are in flight on purpose.
 __device__ __forceinline__ void rc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// 8 bytes of a kHmTabW tap row from byte o (taps at kHmTabPad ..; zeros around)
-__device__ __forceinline__ rc_v2i rc_taps8(const signed char *row, int o) {
-    o = clampi(o, kHmTabPad - 8, kHmTabPad + 16);
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(row + (o & ~3));
-    const int sh = o & 3;
-    const uint32_t a = p[0], b = p[1], c = p[2];
-    return rc_v2i{static_cast<int>(__builtin_amdgcn_alignbyte(b, a, sh)),
-                  static_cast<int>(__builtin_amdgcn_alignbyte(c, b, sh))};
-}
 
 // 16 bytes of a kRsTabW stride-B tap row from byte o (any alignment)
 __device__ __forceinline__ rc_v4i rc_frag16(const signed char *row, int o) {
@@ -108,11 +102,19 @@ __device__ __forceinline__ rc_v4i rc_frag16(const signed char *row, int o) {
 }
 
 // (a0..3 + 2048) >> 12 clamped to 0..255 and packed (accumulators seeded with the
-// rounding); v_ashr_pk_u8_i32 writes 16 bits, so the halves are joined by a perm
+// rounding); v_ashr_pk_u8_i32 writes 16 bits, so the halves are joined by a perm.
+// rc_round4s: the same minus 128 as signed bytes (seeds carry - 128 << 12): the
+// intermediate in the pixel - 128 form the next pass multiplies
 __device__ __forceinline__ uint32_t rc_round4(int a0, int a1, int a2, int a3) {
     uint32_t lo, hi;
     asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(a0), "v"(a1));
     asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(a2), "v"(a3));
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+__device__ __forceinline__ uint32_t rc_round4s(int a0, int a1, int a2, int a3) {
+    uint32_t lo, hi;
+    asm("v_ashr_pk_i8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(a0), "v"(a1));
+    asm("v_ashr_pk_i8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(a2), "v"(a3));
     return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
@@ -140,10 +142,8 @@ __device__ __forceinline__ void rc_edge_frag(const float *tabf, int taps, int pp
     *fl = rc_v4i{static_cast<int>(lw[0]), static_cast<int>(lw[1]), static_cast<int>(lw[2]), static_cast<int>(lw[3])};
 }
 
-// LDS accesses of the step loop as inline asm.  The compiler cannot tell these from
-// the direct-to-LDS loads in flight (the ring rows and taps of later steps, which go
-// to slots nothing reads before their own counted wait) and would put vmcnt(0) before
-// each one; as asm it does not, and the loop waits on lgkmcnt itself.
+// LDS accesses of the step loop as inline asm: the loop counts its own lgkmcnt waits
+// (two tiles in flight per wait) and the compiler's waits stay on the global loads.
 typedef uint32_t rc_u2 __attribute__((ext_vector_type(2)));
 typedef uint32_t rc_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t rc_lds(const void *p) {
@@ -170,6 +170,7 @@ __device__ __forceinline__ rc_v2i lds_tr8(uint32_t a) {
     return v;
 }
 __device__ __forceinline__ void lds_wr32(uint32_t a, uint32_t v) { asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory"); }
+__device__ __forceinline__ void lds_wr128(uint32_t a, rc_u4 v) { asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory"); }
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // The wait must also be a data dependence of the values it waits for: an asm read's
 // result is an ordinary register to the compiler, which could otherwise schedule its
@@ -183,60 +184,16 @@ __device__ __forceinline__ void lgkm_wait_for(T &...v) {
     (rc_pin(v), ...);  // every later use reads the copy made after the wait
 }
 
-// 8 bytes of a kHmTabW tap row in LDS from byte o: the three dwords, then the shift.
-// The rows are sliced [dword / 4][16 rows][dword % 4] (row = this lane's base, dword
-// d at + (d >> 2) * 256 + (d & 3) * 4 bytes); dw0 = 0 for the hi row, 16 for the lo row.
-struct RcTap8 { uint32_t a, b, c; int sh; };
-__device__ __forceinline__ RcTap8 rc_taps8_issue(uint32_t row, int dw0, int o) {
-    o = clampi(o, kHmTabPad - 8, kHmTabPad + 16);
-    const int d = dw0 + (o >> 2);
-    auto at = [&](int k) { return row + (((d + k) >> 2) << 8) + (((d + k) & 3) << 2); };
-    return RcTap8{lds_rd32(at(0)), lds_rd32(at(1)), lds_rd32(at(2)), o & 3};
-}
-__device__ __forceinline__ rc_v2i rc_taps8_done(const RcTap8 &t) {
-    return rc_v2i{static_cast<int>(__builtin_amdgcn_alignbyte(t.b, t.a, t.sh)),
-                  static_cast<int>(__builtin_amdgcn_alignbyte(t.c, t.b, t.sh))};
-}
-
-__device__ __forceinline__ unsigned long long rc_now() {
-    unsigned long long t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform n (the instruction takes an immediate).
-// Buffer loads, stores and LDS-DMA retire in issue order on the VM counter, so
-// "all but the n youngest" is exact for them (MI355X_MICROARCH.md, vmcnt).
-__device__ __forceinline__ void rc_wait_vm(int n) {
-    switch (__builtin_amdgcn_readfirstlane(min(max(n, 0), 63))) {
-#define RC_W(k) \
-    case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-#define RC_W8(k) RC_W(k) RC_W(k + 1) RC_W(k + 2) RC_W(k + 3) RC_W(k + 4) RC_W(k + 5) RC_W(k + 6) RC_W(k + 7)
-        RC_W8(0) RC_W8(8) RC_W8(16) RC_W8(24) RC_W8(32) RC_W8(40) RC_W8(48) RC_W8(56)
-#undef RC_W8
-#undef RC_W
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-
-constexpr int kRcD = 2;  // steps whose loads are in flight ahead of the step being computed
-
-// WV waves per block, XW = 16 WV output pixels per strip: 3 (RGB) / 4 (RGBA) units per wave.
-// A step's global traffic (its new ring rows, its 16 output rows' vertical tap rows and
-// tap sums) is direct-to-LDS DMA issued kRcD steps ahead; the step waits for it with a
-// counted vmcnt (every younger DMA of this wave stays in flight) and a barrier.
-template <int B, int WV, int NKS>
-__global__ void __launch_bounds__(512) k_rcol(RcArgs a) {
-    constexpr int XW = 16 * WV;
-    constexpr int NT = 64 * WV;       // threads
-    constexpr int UPW = B;            // units per wave: XW B / 16 / WV
-    constexpr int NSL = kRcD + 1;     // tap slots
+// KMAX ring chunks per lane per step (16 bytes each), NKS horizontal K steps (64 bytes
+// each), ALN: every output row starts on a dword (one b32 store per unit, else 4 b8).
+template <int B, int NKS, int KMAX, bool ALN>
+__global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
+    constexpr int WV = kRcNT / 64, XW = 16 * WV;
+    constexpr int UPW = B;  // horizontal units per wave: XW B / 16 / WV
+    constexpr int SB = ALN ? 1 : 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t rcs[];
-    uint32_t *ring = rcs;                                                   // [ring][rs]
-    u8 *inter = reinterpret_cast<u8 *>(ring + a.ring * a.rs);              // [16][iw] (pixel - 128)
-    int *pbias = reinterpret_cast<int *>(inter + kRcRows * a.iw);          // [XW * B] 128 * tap sum + 2048
-    uint32_t *vtap = reinterpret_cast<uint32_t *>(pbias + XW * B);         // [NSL][16 rows][hi 16 | lo 16 dwords]
-    int *vsum = reinterpret_cast<int *>(vtap + NSL * kRcRows * 32);        // [NSL][16] tap sums
+    const uint32_t ring_l = rc_lds(rcs);                                            // [rmask + 1][rs]
+    const uint32_t inter_l = ring_l + static_cast<uint32_t>((a.rmask + 1) * a.rs);  // [16][iw]
 
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = static_cast<int>(t % static_cast<uint32_t>(a.strips));
@@ -246,7 +203,6 @@ __global__ void __launch_bounds__(512) k_rcol(RcArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n = lane & 15, kg = lane >> 4;
-    const unsigned long long t_k0 = a.stamps ? rc_now() : 0;
 
     const int x0 = strip * XW, x_last = min(x0 + XW - 1, a.ow - 1);
     const int vbytes = B * (x_last - x0 + 1);  // output bytes of this strip row
@@ -254,98 +210,23 @@ __global__ void __launch_bounds__(512) k_rcol(RcArgs a) {
     rc_pos(a.ox0 + x0, a.hs, a.hpad, &lo, &ph, a.centre);
     rc_pos(a.ox0 + x_last, a.hs, a.hpad, &hi, &ph, a.centre);
     hi += a.htaps - 1;
-    const int org = lo & ~3;                 // first staged pixel (B org stays dword aligned)
-    const int span = B * (hi - org + 1);     // staged bytes per row
-    const int nt = (span + 15) >> 4;         // 16-byte column tiles
-    const int ndw = (span + 3) >> 2;         // staged dwords per row
-    const int cpr = (ndw + 63) >> 6;         // DMA instructions per row
+    // first staged pixel: B org dword aligned; at the left edge (lo < 0) a multiple of 16
+    // bytes, so no 16-byte chunk straddles the image start (a load at a negative offset
+    // reads 0 whole, image bytes included)
+    const int org = lo & (lo < 0 && B == 3 ? ~15 : ~3);
+    const int span = B * (hi - org + 1);   // staged bytes per row
+    const int cpr = (span + 15) >> 4;      // 16-byte chunks per row = vertical column tiles
     const int pitch = a.w * B;
 
-    const int y_begin = seg * a.seg_steps * kRcRows;
-    const int y_end = min(a.oh, y_begin + a.seg_steps * kRcRows);
-    const int steps = (y_end - y_begin + kRcRows - 1) / kRcRows;
+    const int ka = a.k0 + seg * a.seg_steps;  // this segment's 16-row groups [ka, ka + steps)
+    const int steps = min(a.k0 + a.ksteps, ka + a.seg_steps) - ka;
 
     const __amdgpu_buffer_rsrc_t src = image_rsrc(a.in + img * a.in_img, a.in_img);
-    const __amdgpu_buffer_rsrc_t tsrc = image_rsrc(reinterpret_cast<const u8 *>(a.tabv),
-                                                   (kTransformScale + 1) * (2 * kHmTabW + 4));
-    u8 *ob = a.out + img * a.out_img;
-    const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
+    const __amdgpu_buffer_rsrc_t prs = image_rsrc(a.plan, static_cast<long long>(a.plan_rows) * kRcolPlanRow);
+    rc_cint *srow = (rc_cint *)(a.plan + static_cast<size_t>(a.plan_rows) * kRcolPlanRow);  // [group][first, end]
+    const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
 
-    // step geometry: first ring row and end of the rows read (uniform)
-    auto step_rows = [&](int st, int *r_lo, int *r_end) {
-        const int y = y_begin + st * kRcRows, nr = min(kRcRows, y_end - y);
-        int p;
-        rc_pos(a.oy0 + y, a.vs, a.vpad, r_lo, &p, a.centre);
-        rc_pos(a.oy0 + y + nr - 1, a.vs, a.vpad, r_end, &p, a.centre);
-        *r_end += a.vtaps;
-    };
-    int r_lo0, r_end0;
-    step_rows(0, &r_lo0, &r_end0);
-    const int vbase = r_lo0;
-    u8 *ringb = reinterpret_cast<u8 *>(ring);
-    const int rsb = a.rs * 4;
-    // DMA for step st: ring rows [v0, v1) and the step's vertical tap rows + sums, dealt to
-    // the waves; returns this wave's instruction count.  Image row offsets ride in the
-    // VGPR offset (range-checked per image); rows clamp (COPY edge).
-    int slot_ld = 0;  // ring slot of row `loaded` ((loaded - vbase) mod ring, tracked without divisions)
-    auto issue = [&](int st, int v0, int v1) -> int {
-        // whole rows dealt to the waves (row l -> wave l mod WV), cpr instructions per row
-        const int nrows = v1 - v0;
-        int slot = slot_ld + wave;
-        slot = slot >= a.ring ? slot - a.ring : slot;
-        int cnt = 0;
-        for (int l = wave; l < nrows; l += WV) {
-            const int ro = clampi(v0 + l, 0, a.h - 1) * pitch + B * org + 4 * lane;
-            u8 *drow = ringb + slot * rsb;
-            for (int c = 0; c < cpr; ++c)
-                if (64 * c + lane < ndw)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (rc_lds_void *)(drow + 256 * c), 4, ro + 256 * c, 0, 0, 0);
-            cnt += cpr;
-            slot += WV;
-            slot = slot >= a.ring ? slot - a.ring : slot;
-        }
-        slot_ld += nrows;
-        slot_ld = slot_ld >= a.ring ? slot_ld - a.ring : slot_ld;
-        const int sl = st % NSL;
-        const int y = y_begin + st * kRcRows, nr = min(kRcRows, y_end - y);
-        // 16 rows x 32 dwords (the hi and lo 64-byte tap rows of each output row's phase),
-        // stored as 8 slices of [16 rows][4 dwords] so the 16 rows' reads of one dword
-        // spread over 16 bank quads (instruction i, lane l: row l >> 2, dword 4 i + (l & 3))
-        for (int i = wave; i < kRcRows * 32 / 64; i += WV) {
-            const int r = lane >> 2, dw = 4 * i + (lane & 3);
-            int sv, pv;
-            rc_pos(a.oy0 + y + min(r, nr - 1), a.vs, a.vpad, &sv, &pv, a.centre);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(tsrc, (rc_lds_void *)(vtap + (sl * kRcRows * 32 + 64 * i)), 4,
-                                                     (pv * 2 + (dw >> 4)) * kHmTabW + 4 * (dw & 15), 0, 0, 0);
-            ++cnt;
-        }
-        if (wave == (kRcRows * 32 / 64) % WV) {  // the 16 tap sums (after the 129 x 2 rows)
-            int sv, pv;
-            rc_pos(a.oy0 + y + min(lane & 15, nr - 1), a.vs, a.vpad, &sv, &pv, a.centre);
-            if (lane < kRcRows)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(tsrc, (rc_lds_void *)(vsum + sl * kRcRows), 4,
-                                                         (kTransformScale + 1) * 2 * kHmTabW + 4 * pv, 0, 0, 0);
-            ++cnt;
-        }
-        return cnt;
-    };
-
-    // ---- prime: steps 0 .. kRcD - 1 ----
-    int loaded = vbase, cnt_next = 0;
-    for (int st = 0; st < kRcD && st < steps; ++st) {
-        int rl, re;
-        step_rows(st, &rl, &re);
-        const int c = issue(st, loaded, re);
-        loaded = re;
-        if (st == 1) cnt_next = c;
-    }
-
-    // ---- per-segment set-up: horizontal operands (registers, COPY edge folded) and biases ----
-    for (int j = tid; j < XW * B; j += NT) {
-        int sp, pp;
-        rc_pos(a.ox0 + min(x0 + j / B, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
-        pbias[j] = 128 * a.sumh[pp] + 2048;
-    }
+    // ---- per-segment set-up: horizontal operands (registers, COPY edge folded) ----
     // every operand load issued before the first is used (one memory round trip)
     rc_v4i th[UPW][NKS], tl[UPW][NKS];
     uint4 qh[UPW][NKS], ql[UPW][NKS];
@@ -385,6 +266,51 @@ __global__ void __launch_bounds__(512) k_rcol(RcArgs a) {
             }
         }
     }
+    // per output byte seeds of the horizontal pass (lane: bytes 16 u + 4 kg + j of row n)
+    // and store offsets (past the strip's last byte: beyond any image, so dropped)
+    rc_v4i hb[UPW];
+    uint32_t sto[UPW][SB];
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) {
+        const int e = 16 * (wave + WV * i) + 4 * kg;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            int sp, pp;
+            rc_pos(a.ox0 + min(x0 + (e + j) / B, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
+            hb[i][j] = 128 * a.sumh[pp] + 2048;
+        }
+#pragma unroll
+        for (int j = 0; j < SB; ++j) sto[i][j] = e + j < vbytes ? static_cast<uint32_t>(B * x0 + e + j) : 0x20000000u;
+    }
+
+    // ring chunks: chunk c = tid + 256 j of a step's rows is (row rr, column col); the
+    // same map every step.  A lane's chunks past the step's rows load rows below it:
+    // harmless (host-checked: their slots hold rows no longer read).
+    int rr[KMAX], cof[KMAX];
+    uint32_t lcol[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) {
+        const int c = tid + kRcNT * j;
+        rr[j] = c / cpr;
+        const int col = c - rr[j] * cpr;
+        cof[j] = B * org + 16 * col;
+        lcol[j] = ring_l + static_cast<uint32_t>(16 * col);
+    }
+    const int lkf = (kRcNT * KMAX) / cpr;  // rows one load batch covers completely
+
+    // ---- prime: group ka's rows straight into the ring (exact rows only) ----
+    const int bka = srow[2 * ka], eka = srow[2 * ka + 1];
+    for (int r = bka; r < eka; r += lkf) {
+        rc_u4 tv[KMAX];
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  src, clampi(r + rr[j], 0, a.h - 1) * pitch + cof[j], 0, 0));
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if (rr[j] < lkf && r + rr[j] < eka)
+                lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j], tv[j] ^ 0x80808080u);
+    }
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
         if (both[i]) continue;
@@ -403,185 +329,146 @@ __global__ void __launch_bounds__(512) k_rcol(RcArgs a) {
         }
     }
 
-    uint32_t res[UPW];
-    int y_prev = 0, nr_prev = 0;
-    int ring_lo = 0, r_lo_prev = vbase;
-    const bool stamp = a.stamps != nullptr;  // uniform
-    unsigned long long ph_t[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t_prev = t_k0;
-    auto mark = [&](int k) {
-        if (stamp) {
-            const unsigned long long t1 = rc_now();
-            ph_t[k] += t1 - t_prev;
-            t_prev = t1;
+    // ---- the step pipeline: register set P = (step - ka) & 1 holds step k + 2's ring
+    // chunks and vertical operands from the middle of step k to the top of step k + 2.
+    // Every step issues the same global loads and stores (out-of-range offsets where
+    // there is nothing to do), so the compiler's vmcnt waits are the exact two-step
+    // counts and never drain the loads of the next step.
+    rc_u4 rv[2][KMAX];
+    rc_v4i vh[2], vl[2];
+    int vsd[2];
+    const int toff = n * kRcolPlanRow + 16 * kg;  // this lane's tap fragment: output row n, K 16 kg ..
+    auto issue_taps = [&](auto pc, int k) {
+        constexpr int P = decltype(pc)::value;
+        const int o = k * (kRcRows * kRcolPlanRow);
+        vh[P] = __builtin_bit_cast(rc_v4i, __builtin_amdgcn_raw_buffer_load_b128(prs, toff + o, 0, 0));
+        vl[P] = __builtin_bit_cast(rc_v4i, __builtin_amdgcn_raw_buffer_load_b128(prs, toff + o + 64, 0, 0));
+        vsd[P] = __builtin_amdgcn_raw_buffer_load_b32(prs, n * kRcolPlanRow + 128 + o, 0, 0);
+    };
+    auto issue_ring = [&](auto pc, int r0) {
+        constexpr int P = decltype(pc)::value;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            rv[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     src, clampi(r0 + rr[j], 0, a.h - 1) * pitch + cof[j], 0, 0));
+    };
+    auto write_ring = [&](auto pc, int r0) {
+        constexpr int P = decltype(pc)::value;
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            lds_wr128(static_cast<uint32_t>(((r0 + rr[j]) & a.rmask) * a.rs) + lcol[j], rv[P][j] ^ 0x80808080u);
+    };
+    auto store = [&](int k, bool live, const uint32_t *res) {
+        const int o = k * kRcRows + n - a.oy0;  // window row of the lane's output row
+        const uint32_t rb = live && o >= 0 && o < a.oh ? static_cast<uint32_t>(o * a.ow * B) : 0x80000000u;
+#pragma unroll
+        for (int i = 0; i < UPW; ++i) {
+            if constexpr (ALN) {
+                __builtin_amdgcn_raw_buffer_store_b32(res[i], dst, static_cast<int>(rb + sto[i][0]), 0, 0);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(res[i] >> (8 * j)), dst,
+                                                         static_cast<int>(rb + sto[i][j]), 0, 0);
+            }
         }
     };
-    mark(8); asm volatile(";@@MARK 8");  // prime + set-up
-    for (int s = 0; s < steps; ++s) {
-        const int y = y_begin + s * kRcRows;
-        const int nr = min(kRcRows, y_end - y);
-        int r_lo, r_end;
-        step_rows(s, &r_lo, &r_end);
-        // (C) this step's DMA has landed (this wave: all but the next step's loads; the
-        // barrier: every wave), the intermediate is free (previous horizontal pass done)
-        mark(0); asm volatile(";@@MARK 0");
-        rc_wait_vm(s + 1 < steps ? cnt_next : 0);
-        mark(1); asm volatile(";@@MARK 1");
-        rc_barrier();
-        mark(2); asm volatile(";@@MARK 2");
-        // (D) the previous step's outputs
-        if (s > 0) {
+    // vertical pass: 16-byte column tiles dealt to the waves, two in flight per wait.  K
+    // index 16 kg + e holds relative row 8 kg + e (e < 8) or 32 + 8 kg + e - 8, so the 16
+    // rows one 32-lane half reads per transposed load sit in consecutive ring slots
+    auto vertical = [&](auto pc, int bk) {
+        constexpr int P = decltype(pc)::value;
+        const rc_v4i bh = vh[P], bl = vl[P];
+        const int sd = vsd[P];
+        const int r1 = bk + 8 * kg + (n >> 1);
+        const uint32_t a1 = ring_l + static_cast<uint32_t>((r1 & a.rmask) * a.rs + 8 * (n & 1));
+        const uint32_t a2 = ring_l + static_cast<uint32_t>(((r1 + 32) & a.rmask) * a.rs + 8 * (n & 1));
+        const uint32_t iq = inter_l + static_cast<uint32_t>(n * a.iw + 4 * kg);
+        auto tile = [&](int ct, rc_v2i t1, rc_v2i t2) {
+            const rc_v4i av = rc_v4i{t1.x, t1.y, t2.x, t2.y};
+            rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
+            dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
+            dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
+            lds_wr32(iq + 16 * ct,
+                     rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
+        };
+        for (int ct = wave; ct < cpr; ct += 2 * WV) {
+            const bool two = ct + WV < cpr;  // uniform
+            rc_v2i t1a = lds_tr8(a1 + 16 * ct), t2a = lds_tr8(a2 + 16 * ct);
+            rc_v2i t1b = t1a, t2b = t2a;
+            if (two) {
+                t1b = lds_tr8(a1 + 16 * (ct + WV));
+                t2b = lds_tr8(a2 + 16 * (ct + WV));
+            }
+            lgkm_wait_for<0>(t1a, t2a, t1b, t2b);
+            tile(ct, t1a, t2a);
+            if (two) tile(ct + WV, t1b, t2b);
+        }
+    };
+    // horizontal pass: units wave + WV i, operands from registers, every unit's LDS
+    // reads in flight together
+    auto horizontal = [&](uint32_t *res) {
+        rc_u2 q[UPW][NKS][2];
 #pragma unroll
-            for (int i = 0; i < UPW; ++i) {
-                const int u = wave + WV * i;
-                const int e = 16 * u + 4 * kg;  // strip byte of the lane's dword
-                if (n >= nr_prev || e >= vbytes) continue;
-                const int qo = (y_prev + n) * a.ow * B + B * x0 + e;
-                if (a.out_aligned) {
-                    __builtin_amdgcn_raw_buffer_store_b32(res[i], dst, qo, 0, 0);
-                } else {
+        for (int i = 0; i < UPW; ++i) {
+            const uint32_t ir = inter_l + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg);
 #pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (e + k < vbytes)
-                            __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(res[i] >> (8 * k)), dst, qo + k, 0, 0);
-                }
+            for (int ks = 0; ks < NKS; ++ks) {
+                q[i][ks][0] = lds_rd64(ir + 64 * ks);
+                q[i][ks][1] = lds_rd64(ir + 64 * ks + 8);
             }
         }
-        // (B) step s + kRcD's loads: its new rows go to slots of rows below this step's
-        // first (ring >= rows from this step's first to that step's last, host-checked)
-        mark(3); asm volatile(";@@MARK 3");  // stores
-        cnt_next = 0;
-        if (s + kRcD < steps) {
-            int rl, re;
-            step_rows(s + kRcD, &rl, &re);
-            cnt_next = issue(s + kRcD, loaded, re);
-            loaded = re;
-        }
-        mark(4); asm volatile(";@@MARK 4");  // DMA issue
-        // (E) vertical pass: 16-byte column tiles dealt to the waves.  K index 16 kg + e
-        // holds relative row 8 kg + e (e < 8) or 32 + 8 kg + e - 8, so the 16 rows one
-        // 32-lane half reads per transposed load sit in consecutive ring slots
-        {
-            const int sl = s % NSL;
-            int sv, pv;
-            rc_pos(a.oy0 + y + min(n, nr - 1), a.vs, a.vpad, &sv, &pv, a.centre);
-            const uint32_t rv = rc_lds(vtap + sl * kRcRows * 32 + 4 * n);
-            const int d = sv - r_lo - kHmTabPad;
-            const RcTap8 qh0 = rc_taps8_issue(rv, 0, 8 * kg - d), qh1 = rc_taps8_issue(rv, 0, 32 + 8 * kg - d);
-            const RcTap8 ql0 = rc_taps8_issue(rv, 16, 8 * kg - d), ql1 = rc_taps8_issue(rv, 16, 32 + 8 * kg - d);
-            const uint32_t vsr = lds_rd32(rc_lds(vsum + sl * kRcRows + n));
-            ring_lo += r_lo - r_lo_prev;  // ring slot of this step's first row
-            ring_lo = ring_lo >= a.ring ? ring_lo - a.ring : ring_lo;
-            r_lo_prev = r_lo;
-            const int base = ring_lo;
-            int s1 = base + 8 * kg + (n >> 1), s2 = s1 + 32;
-            s1 = s1 >= a.ring ? s1 - a.ring : s1;
-            s1 = s1 >= a.ring ? s1 - a.ring : s1;
-            s2 = s2 >= a.ring ? s2 - a.ring : s2;
-            s2 = s2 >= a.ring ? s2 - a.ring : s2;
-            s2 = s2 >= a.ring ? s2 - a.ring : s2;
-            const uint32_t a1 = rc_lds(ringb + s1 * rsb + 8 * (n & 1));
-            const uint32_t a2 = rc_lds(ringb + s2 * rsb + 8 * (n & 1));
-            const uint32_t iq = rc_lds(inter + n * a.iw + 4 * kg);
-            RcTap8 th0 = qh0, th1 = qh1, tl0 = ql0, tl1 = ql1;
-            uint32_t vsv = vsr;
-            lgkm_wait_for<0>(th0.a, th0.b, th0.c, th1.a, th1.b, th1.c, tl0.a, tl0.b, tl0.c, tl1.a, tl1.b, tl1.c, vsv);
-            const rc_v2i h0 = rc_taps8_done(th0), h1 = rc_taps8_done(th1);
-            const rc_v2i l0 = rc_taps8_done(tl0), l1 = rc_taps8_done(tl1);
-            const rc_v4i bh = rc_v4i{h0.x, h0.y, h1.x, h1.y};
-            const rc_v4i bl = rc_v4i{l0.x, l0.y, l1.x, l1.y};
-            const int vb = 128 * static_cast<int>(vsv) + 2048;
-            auto tile = [&](int ct, rc_v2i t1, rc_v2i t2) {
-                const rc_v4i av = rc_v4i{t1.x ^ static_cast<int>(0x80808080u), t1.y ^ static_cast<int>(0x80808080u),
-                                         t2.x ^ static_cast<int>(0x80808080u), t2.y ^ static_cast<int>(0x80808080u)};
-                rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{vb, vb, vb, vb};
-                dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
-                dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
-                const uint32_t wv = rc_round4((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
-                                              (dh[3] << 6) + dl[3]);
-                lds_wr32(iq + 16 * ct, wv ^ 0x80808080u);
-            };
-            // two tiles in flight per wait
-            for (int ct = wave; ct < nt; ct += 2 * WV) {
-                const bool two = ct + WV < nt;  // uniform
-                rc_v2i t1a = lds_tr8(a1 + 16 * ct), t2a = lds_tr8(a2 + 16 * ct);
-                rc_v2i t1b = t1a, t2b = t2a;
-                if (two) {
-                    t1b = lds_tr8(a1 + 16 * (ct + WV));
-                    t2b = lds_tr8(a2 + 16 * (ct + WV));
-                }
-                lgkm_wait_for<0>(t1a, t2a, t1b, t2b);
-                tile(ct, t1a, t2a);
-                if (two) tile(ct + WV, t1b, t2b);
+#pragma unroll
+        for (int i = 0; i < UPW; ++i)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) rc_pin(q[i][ks][0]), rc_pin(q[i][ks][1]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < UPW; ++i) {
+            rc_v4i ah = rc_v4i{0, 0, 0, 0}, al = hb[i];
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                rc_pin(q[i][ks][0]);
+                rc_pin(q[i][ks][1]);
+                const rc_v4i bz = rc_v4i{static_cast<int>(q[i][ks][0].x), static_cast<int>(q[i][ks][0].y),
+                                         static_cast<int>(q[i][ks][1].x), static_cast<int>(q[i][ks][1].y)};
+                ah = __builtin_amdgcn_mfma_i32_16x16x64_i8(th[i][ks], bz, ah, 0, 0, 0);
+                al = __builtin_amdgcn_mfma_i32_16x16x64_i8(tl[i][ks], bz, al, 0, 0, 0);
             }
+            res[i] = rc_round4((ah[0] << 6) + al[0], (ah[1] << 6) + al[1], (ah[2] << 6) + al[2], (ah[3] << 6) + al[3]);
         }
-        mark(5); asm volatile(";@@MARK 5");  // vertical
-        // (F) the intermediate is complete
-        rc_barrier();
-        mark(6); asm volatile(";@@MARK 6");
-        // (H) horizontal pass: units wave + WV i, operands from registers; unit i + 1's
-        // LDS reads are in flight while unit i computes
-        {
-            constexpr int RPU = 1 + 2 * NKS;  // LDS reads per unit
-            rc_u4 bias[UPW];
-            rc_u2 q[UPW][NKS][2];
-            auto rd = [&](int i) {
-                const int u = wave + WV * i;
-                bias[i] = lds_rd128(rc_lds(pbias + 16 * u + 4 * kg));
-                const uint32_t ir = rc_lds(inter + n * a.iw + kb[i] + 16 * kg);
+    };
+    // one step (16-row group k): ring rows of k (loaded two steps ago) -> barrier ->
+    // vertical -> loads of k + 2 -> barrier -> horizontal -> stores.  A phantom step
+    // (live = false, the odd tail of a pair) issues the same loads and stores, all idle.
+    auto body = [&](auto pc, int k, bool live, bool first) {
+        uint32_t res[UPW];
 #pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) {
-                    q[i][ks][0] = lds_rd64(ir + 64 * ks);
-                    q[i][ks][1] = lds_rd64(ir + 64 * ks + 8);
-                }
-            };
-            // units past the strip's last output byte read in-range LDS and are not stored
-            rd(0);
-#pragma unroll
-            for (int i = 0; i < UPW; ++i) {
-                if (i + 1 < UPW) {
-                    rd(i + 1);
-                    if constexpr (NKS == 1) lgkm_wait_for<RPU>(bias[i], q[i][0][0], q[i][0][1]);
-                    else lgkm_wait_for<RPU>(bias[i], q[i][0][0], q[i][0][1], q[i][NKS - 1][0], q[i][NKS - 1][1]);
-                } else {
-                    if constexpr (NKS == 1) lgkm_wait_for<0>(bias[i], q[i][0][0], q[i][0][1]);
-                    else lgkm_wait_for<0>(bias[i], q[i][0][0], q[i][0][1], q[i][NKS - 1][0], q[i][NKS - 1][1]);
-                }
-                rc_v4i ah = rc_v4i{0, 0, 0, 0};
-                rc_v4i al = rc_v4i{static_cast<int>(bias[i].x), static_cast<int>(bias[i].y), static_cast<int>(bias[i].z),
-                                   static_cast<int>(bias[i].w)};
-#pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) {
-                    const rc_v4i bz = rc_v4i{static_cast<int>(q[i][ks][0].x), static_cast<int>(q[i][ks][0].y),
-                                             static_cast<int>(q[i][ks][1].x), static_cast<int>(q[i][ks][1].y)};
-                    ah = __builtin_amdgcn_mfma_i32_16x16x64_i8(th[i][ks], bz, ah, 0, 0, 0);
-                    al = __builtin_amdgcn_mfma_i32_16x16x64_i8(tl[i][ks], bz, al, 0, 0, 0);
-                }
-                res[i] = rc_round4((ah[0] << 6) + al[0], (ah[1] << 6) + al[1], (ah[2] << 6) + al[2], (ah[3] << 6) + al[3]);
-            }
+        for (int i = 0; i < UPW; ++i) res[i] = 0u;
+        if (live) {
+            if (!first) write_ring(pc, srow[2 * (k - 1) + 1]);
+            rc_barrier();
+            vertical(pc, srow[2 * k]);
         }
-        mark(7); asm volatile(";@@MARK 7");  // horizontal
-        y_prev = y;
-        nr_prev = nr;
-    }
-    if (stamp && tid == 0) {
-        for (int k = 0; k < 9; ++k) a.stamps[blockIdx.x * 10 + k] = ph_t[k];
-        a.stamps[blockIdx.x * 10 + 9] = static_cast<unsigned long long>(steps);
-    }
-    // the last step's outputs
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) {
-        const int u = wave + WV * i;
-        const int e = 16 * u + 4 * kg;
-        if (n >= nr_prev || e >= vbytes) continue;
-        const int qo = (y_prev + n) * a.ow * B + B * x0 + e;
-        if (a.out_aligned) {
-            __builtin_amdgcn_raw_buffer_store_b32(res[i], dst, qo, 0, 0);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (e + k < vbytes)
-                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(res[i] >> (8 * k)), dst, qo + k, 0, 0);
+        issue_ring(pc, srow[2 * (k + 1) + 1]);
+        issue_taps(pc, k + 2);
+        if (live) {
+            rc_barrier();
+            horizontal(res);
         }
+        store(k, live, res);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    const uint32_t zero[UPW] = {};
+    issue_taps(I0{}, ka);
+    store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
+    issue_ring(I1{}, eka);
+    issue_taps(I1{}, ka + 1);
+    store(ka, false, zero);
+    for (int s = 0; s < steps; s += 2) {
+        body(I0{}, ka + s, true, s == 0);
+        body(I1{}, ka + s + 1, s + 1 < steps, false);
     }
 }
 
@@ -589,17 +476,20 @@ int rc_start(int o, double s, int pad, bool centre) { return static_cast<int>(re
 
 }  // namespace
 
-// The column walker for both shrinks in (1, 2.75) on 3- / 4-band images whose
-// input rows start on a dword; MIPX_EUNSUPPORTED otherwise (the caller runs
+// The column walker for both shrinks in (1, ~2.5] (<= 16 taps) on 3- / 4-band images
+// whose input rows start on a dword; MIPX_EUNSUPPORTED otherwise (the caller runs
 // another kernel).  Output window [ox0, ox0 + ow) x [oy0, oy0 + oh).
 int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
                       int ow, int oh, hipStream_t st) {
     if ((b != 3 && b != 4) || !(hs > 1.0) || !(vs > 1.0)) return MIPX_EUNSUPPORTED;
     const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
-    if (in_img >= 0x7fffffffLL || out_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
+    // out-of-range store offsets are built from 2^29 and 2^31 (k_rcol store)
+    if (in_img >= 0x7fffffffLL || out_img >= (1LL << 29)) return MIPX_EUNSUPPORTED;
     if ((w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0) return MIPX_EUNSUPPORTED;
     const int vtaps = reduce_points(vs), htaps = reduce_points(hs);
     if (vtaps > 16 || htaps > 16) return MIPX_EUNSUPPORTED;
+    const bool centre = reduce_centre();
+    const int vpad = vtaps / 2 - 1;
     RcArgs a{};
     a.in = in;
     a.out = out;
@@ -611,124 +501,120 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     a.oh = oh;
     a.in_img = in_img;
     a.out_img = out_img;
-    a.vtaps = vtaps;
-    a.vpad = vtaps / 2 - 1;
     a.htaps = htaps;
     a.hpad = htaps / 2 - 1;
-    a.vs = vs;
     a.hs = hs;
-    a.out_aligned = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
-    const bool centre = reduce_centre();
     a.centre = centre;
-    // ring rows: from a step's first row to the last row of the step kRcD ahead (whose
-    // loads are issued before the step's vertical pass), exact over the window's steps;
-    // the MFMA K is 64 rows
-    const int nsteps = (oh + kRcRows - 1) / kRcRows;
-    int lmax = 0, ring = 0;
-    auto first_row = [&](int st) { return rc_start(oy0 + st * kRcRows, vs, a.vpad, centre); };
-    auto end_row = [&](int st) { return rc_start(oy0 + std::min(oh, (st + 1) * kRcRows) - 1, vs, a.vpad, centre) + vtaps; };
-    for (int st = 0; st < nsteps; ++st) {
-        lmax = std::max(lmax, end_row(st) - first_row(st));
-        ring = std::max(ring, end_row(std::min(nsteps - 1, st + kRcD)) - first_row(st));
+    a.k0 = oy0 / kRcRows;
+    const int k1 = (oy0 + oh - 1) / kRcRows;  // last group
+    a.ksteps = k1 - a.k0 + 1;
+    // the plan's group rows (host copy of the same formula)
+    auto gb = [&](int k) { return rc_start(kRcRows * k, vs, vpad, centre); };
+    auto ge = [&](int k) { return rc_start(kRcRows * k + kRcRows - 1, vs, vpad, centre) + vtaps; };
+    int lmax = 0, maxnew = 0;
+    for (int k = a.k0; k <= k1; ++k) {
+        lmax = std::max(lmax, ge(k) - gb(k));
+        if (k > a.k0) maxnew = std::max(maxnew, ge(k) - ge(k - 1));
     }
-    if (lmax > 64) return MIPX_EUNSUPPORTED;
-    a.ring = (ring + 15) & ~15;
-    int ntv = 0, nth = 0, ntf = 0;
-    a.tabv = device_reduce_i8(vs, &ntv, &a.sumv);
+    if (lmax > 64) return MIPX_EUNSUPPORTED;  // the MFMA K
+
+    // strip geometry: staged chunks per row, K steps of the horizontal units
+    int cpr_min = 1 << 30, cpr_max = 0, nks = 0, kbmax = 0;
+    for (int x0 = 0; x0 < ow; x0 += 64) {
+        const int xl = std::min(x0 + 63, ow - 1);
+        const int lo = rc_start(ox0 + x0, hs, a.hpad, centre), hi = rc_start(ox0 + xl, hs, a.hpad, centre) + htaps - 1;
+        const int org = lo & (lo < 0 && b == 3 ? ~15 : ~3);  // as k_rcol
+        const int cpr = (b * (hi - org + 1) + 15) >> 4;
+        cpr_min = std::min(cpr_min, cpr);
+        cpr_max = std::max(cpr_max, cpr);
+        for (int u = 0; u < 64 * b / 16; ++u) {
+            const int o0 = 16 * u, o1 = 16 * u + 15;
+            if (x0 + o0 / b > xl) break;
+            const int xf = x0 + o0 / b, xe = std::min(x0 + o1 / b, xl);
+            const int kbu = (b * (rc_start(ox0 + xf, hs, a.hpad, centre) - org) + o0 % b) & ~7;
+            const int need = b * (rc_start(ox0 + xe, hs, a.hpad, centre) + htaps - 1 - org) + b;
+            nks = std::max(nks, (need - kbu + 63) / 64);
+            kbmax = std::max(kbmax, kbu);
+        }
+    }
+    if (nks > 2) return MIPX_EUNSUPPORTED;
+    // chunks per lane: the widest strip's rows of the largest step fit one batch; ring:
+    // the rows of a step, and a batch's over-reach past the step's end must only land on
+    // slots of rows above the step's first
+    int kmax = 0, ring = 0;
+    for (int km : {3, 6}) {
+        if ((kRcNT * km) / cpr_max < maxnew) continue;
+        const int reach = (kRcNT * km + cpr_min - 1) / cpr_min;
+        for (int r : {32, 64}) {
+            bool ok = lmax <= r;
+            for (int k = a.k0 + 1; ok && k <= k1; ++k) ok = ge(k - 1) + reach <= gb(k) + r;
+            if (ok) { ring = r; break; }
+        }
+        if (ring) { kmax = km; break; }
+    }
+    if (!kmax) return MIPX_EUNSUPPORTED;
+    a.rmask = ring - 1;
+    int rs = 4 * cpr_max;  // dwords
+    while (((rs & 63) >> 2) % 2 == 0) rs += 4;  // 16 consecutive rows on distinct bank quads
+    a.rs = 4 * rs;
+    int iw = (std::max(16 * cpr_max, kbmax + 64 * nks) + 16 + 15) & ~15;
+    while ((iw / 4) % 8 != 4) iw += 16;  // 4 mod 8 dwords: the intermediate writes hit distinct banks
+    a.iw = iw;
+    const size_t lds = static_cast<size_t>(ring) * a.rs + static_cast<size_t>(kRcRows) * iw;
+    if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
+
+    int plan_rows = 0;
+    a.plan = device_rcol_vplan(vs, centre, kRcRows * (k1 + 3), &plan_rows);
+    a.plan_rows = plan_rows;
+    int nth = 0, ntf = 0, nfh = 0;
     const int *sumh = nullptr;
-    if (!device_reduce_i8(hs, &nth, &sumh)) return MIPX_EDEVICE;
+    if (!a.plan || !device_reduce_i8(hs, &nth, &sumh)) return MIPX_EDEVICE;
     a.sumh = sumh;
     a.tabh = device_reduce_i8s(hs, b, &nth);
     a.tabf = device_reduce_table(hs, &ntf);
-    int nfh = 0;
     a.tabhf = device_reduce_i8s_fold(hs, b, &nfh);
-    if (!a.tabv || !a.tabh || !a.tabf || !a.tabhf || ntv != vtaps || nth != htaps || ntf != htaps || nfh != htaps)
-        return MIPX_EDEVICE;
+    if (!a.tabh || !a.tabf || !a.tabhf || nth != htaps || ntf != htaps || nfh != htaps) return MIPX_EDEVICE;
 
-    // per strip width (16 output pixels per wave): staged bytes, K steps of the
-    // horizontal units, LDS
-    struct Geo { int wv, nt, nks, rs, iw; size_t lds; };
-    auto geo_for = [&](int wv) {
-        const int xw = 16 * wv;
-        Geo g{wv, 0, 0, 0, 0, 0};
-        int kbmax = 0;
-        for (int x0 = 0; x0 < ow; x0 += xw) {
-            const int xl = std::min(x0 + xw - 1, ow - 1);
-            const int lo = rc_start(ox0 + x0, hs, a.hpad, centre), hi = rc_start(ox0 + xl, hs, a.hpad, centre) + htaps - 1;
-            const int org = lo & ~3;
-            g.nt = std::max(g.nt, (b * (hi - org + 1) + 15) >> 4);
-            for (int u = 0; u < xw * b / 16; ++u) {
-                const int o0 = 16 * u, o1 = 16 * u + 15;
-                if (x0 + o0 / b > xl) break;
-                const int xf = x0 + o0 / b, xe = std::min(x0 + o1 / b, xl);
-                const int kbu = (b * (rc_start(ox0 + xf, hs, a.hpad, centre) - org) + o0 % b) & ~7;
-                const int need = b * (rc_start(ox0 + xe, hs, a.hpad, centre) + htaps - 1 - org) + b;
-                g.nks = std::max(g.nks, (need - kbu + 63) / 64);
-                kbmax = std::max(kbmax, kbu);
-            }
-        }
-        g.rs = 4 * g.nt;
-        while (((g.rs & 63) >> 2) % 2 == 0) g.rs += 4;  // 16 consecutive rows on distinct bank quads
-        g.iw = (std::max(16 * g.nt, kbmax + 64 * g.nks) + 16 + 15) & ~15;
-        while ((g.iw / 4) % 8 != 4) g.iw += 16;  // 4 mod 8 dwords: the intermediate writes hit distinct banks
-        g.lds = static_cast<size_t>(a.ring) * g.rs * 4 + static_cast<size_t>(kRcRows) * g.iw +
-                static_cast<size_t>(xw) * b * 4 + static_cast<size_t>(kRcD + 1) * kRcRows * 33 * 4;
-        return g;
-    };
-    Geo g = geo_for(8);  // 128-pixel strips, 512 threads: 2 workgroups per CU
-    if (g.nks > 2 || g.lds > 72 * 1024) g = geo_for(4);
-    if (g.nks > 2 || g.lds > 64 * 1024) return MIPX_EUNSUPPORTED;
-    a.rs = g.rs;
-    a.iw = g.iw;
-    a.strips = (ow + 16 * g.wv - 1) / (16 * g.wv);
-    // segments: enough blocks to fill the chip a few times over, >= 2 steps each
-    const int steps = (oh + kRcRows - 1) / kRcRows;
-    const long long cols = static_cast<long long>(a.strips) * n;
-    // ~3 blocks per resident slot (LDS-limited workgroups per CU x 256 CUs): long segments
-    // amortise the per-block set-up, several per slot keep the tail short
-    const int wg_per_cu = std::max<int>(1, static_cast<int>((160 * 1024) / std::max<size_t>(g.lds, 1)));
-    const long long target = 3LL * 256 * std::min(wg_per_cu, g.wv == 8 ? 2 : 8);
-    int segs = static_cast<int>(std::min<long long>(steps, std::max<long long>(1, (target + cols - 1) / cols)));
-    int seg_steps = (steps + segs - 1) / segs;
-    if (seg_steps < 2 && steps >= 2) seg_steps = 2;
-    segs = (steps + seg_steps - 1) / seg_steps;
-    a.segs = segs;
-    a.seg_steps = seg_steps;
-    const long long blocks = cols * segs;
-    if (!grid_ok(blocks)) return MIPX_EINVAL;
-    const dim3 grid(static_cast<unsigned>(blocks)), blk(64 * g.wv);
-    // diagnostic: MIPX_RCOL_STAMPS=1 records s_memtime cycles per step phase of every
-    // block's first wave and prints the means to stderr (synchronises; timing runs only)
-    const char *est = tune_env("MIPX_RCOL_STAMPS");
-    unsigned long long *dstamps = nullptr;
-    if (est && *est == '1' && hipMalloc(&dstamps, static_cast<size_t>(blocks) * 10 * 8) == hipSuccess) a.stamps = dstamps;
-#define MIPX_RC(B_, WV_)                                                                                     \
-    if (g.nks == 1) hipLaunchKernelGGL((k_rcol<B_, WV_, 1>), grid, blk, g.lds, st, a);                      \
-    else hipLaunchKernelGGL((k_rcol<B_, WV_, 2>), grid, blk, g.lds, st, a);
+    const bool aligned = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
+    const void *fn = nullptr;
+#define MIPX_RC_K(B_, NKS_, KM_)                                                                           \
+    fn = aligned ? reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, true>)                            \
+                 : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, false>);
+#define MIPX_RC_KM(B_, NKS_) \
+    if (kmax == 3) { MIPX_RC_K(B_, NKS_, 3) } else { MIPX_RC_K(B_, NKS_, 6) }
     if (b == 3) {
-        if (g.wv == 8) { MIPX_RC(3, 8) } else { MIPX_RC(3, 4) }
+        if (nks == 1) { MIPX_RC_KM(3, 1) } else { MIPX_RC_KM(3, 2) }
     } else {
-        if (g.wv == 8) { MIPX_RC(4, 8) } else { MIPX_RC(4, 4) }
+        if (nks == 1) { MIPX_RC_KM(4, 1) } else { MIPX_RC_KM(4, 2) }
     }
-#undef MIPX_RC
-    if (dstamps) {
-        std::vector<unsigned long long> h(static_cast<size_t>(blocks) * 10);
-        if (hipStreamSynchronize(st) == hipSuccess &&
-            hipMemcpy(h.data(), dstamps, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-            double tot[9] = {0}, nst = 0;
-            for (long long bi = 0; bi < blocks; ++bi) {
-                for (int k = 0; k < 9; ++k) tot[k] += static_cast<double>(h[bi * 10 + k]);
-                nst += static_cast<double>(h[bi * 10 + 9]);
-            }
-            static const char *names[9] = {"top", "vm_wait", "barrier_c", "stores", "dma_issue", "vertical",
-                                           "barrier_f", "horizontal", "setup_per_block"};
-            std::fprintf(stderr, "{\"k_rcol_stamps\": {\"wv\": %d, \"blocks\": %lld, \"steps\": %.0f", g.wv, blocks, nst);
-            for (int k = 0; k < 9; ++k)
-                std::fprintf(stderr, ", \"%s\": %.1f", names[k], k == 8 ? tot[k] / blocks : tot[k] / nst);
-            std::fprintf(stderr, "}}\n");
+#undef MIPX_RC_KM
+#undef MIPX_RC_K
+
+    // segments: a block's set-up (operand loads, the first group's rows) costs about two
+    // steps; pick the split that minimises (rounds of resident blocks) x (steps + 2)
+    a.strips = (ow + 63) / 64;
+    const long long cols = static_cast<long long>(a.strips) * n;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kRcNT, lds) != hipSuccess || per_cu < 1) per_cu = 2;
+    const long long slots = 256LL * per_cu;
+    int best_segs = 1;
+    double best = 1e300;
+    for (int segs = 1; segs <= a.ksteps; ++segs) {
+        const int ss = (a.ksteps + segs - 1) / segs;
+        if (segs > 1 && ss < 4) break;
+        const long long blocks = cols * ((a.ksteps + ss - 1) / ss);
+        const double cost = static_cast<double>((blocks + slots - 1) / slots) * (ss + 2);
+        if (cost < best - 1e-9) {
+            best = cost;
+            best_segs = segs;
         }
-        (void)hipFree(dstamps);
     }
+    a.seg_steps = (a.ksteps + best_segs - 1) / best_segs;
+    a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
+    const long long blocks = cols * a.segs;
+    if (!grid_ok(blocks)) return MIPX_EINVAL;
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(RcArgs)>(const_cast<void *>(fn)), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kRcNT), lds, st, a);
     return launch_check("k_rcol");
 }
 

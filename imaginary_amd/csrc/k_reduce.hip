@@ -405,12 +405,11 @@ int reduceh_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hsh
 }
 
 // Both shrinks > 1 in one launch, output window [ox0, ox0 + ow) x [oy0, oy0 + oh):
-// k_rmf2 (matrix cores, rows of any alignment) first, then the small-image strip
-// walker and fused kernel (> 16 taps); MIPX_EUNSUPPORTED leaves it to the two
-// separable passes.  MIPX_RCOL=1 tries the column walker k_rcol (LDS row ring,
-// dword-aligned rows, <= 16 taps) before k_rmf2 -- opt-in while it measures slower
-// (DESIGN.md §4.1); MIPX_RMFMA=0 turns k_rmf2 off; MIPX_RSTRIP=1 puts the strip
-// walker first.
+// the column walker k_rcol (matrix cores, LDS row ring; dword-aligned input rows,
+// <= 16 taps) first, then k_rmf2 (matrix cores, rows of any alignment), then the
+// small-image strip walker and fused kernel (> 16 taps); MIPX_EUNSUPPORTED leaves it
+// to the two separable passes.  MIPX_RCOL=0 / MIPX_RMFMA=0 turn the first two off
+// (A/B); MIPX_RSTRIP=1 puts the strip walker first.
 int reduce_one_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
                       int ow, int oh, hipStream_t st) {
     const char *ef = tune_env("MIPX_RSTRIP");
@@ -420,7 +419,7 @@ int reduce_one_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
         if (se != MIPX_EUNSUPPORTED) return se;
     }
     const char *ec = tune_env("MIPX_RCOL");
-    if (ec && *ec == '1') {
+    if (!(ec && *ec == '0')) {
         const int ce = reduce_col_launch(in, out, n, w, h, b, hs, vs, ox0, oy0, ow, oh, st);
         if (ce != MIPX_EUNSUPPORTED) return ce;
     }

@@ -78,6 +78,10 @@ const signed char *device_reduce_i8(double shrink, int *n_taps, const int **sums
 const signed char *device_reduce_i8s(double shrink, int bands, int *n_taps);  // taps at a byte stride of bands
 // the same with the COPY edge folded in: [2 sides][taps - 1][129][hi, lo][kRsTabW] (k_rcol)
 const signed char *device_reduce_i8s_fold(double shrink, int bands, int *n_taps);
+// k_rcol's vertical plan (per output row: K-placed split taps + seed; per 16-row group:
+// first / end input rows) over at least `rows` op-output rows; *cap_rows = rows it holds
+constexpr int kRcolPlanRow = 144;
+const uint8_t *device_rcol_vplan(double shrink, bool centre, int rows, int *cap_rows);
 // k_bmf's i8 MFMA operands for a blur mask (cached per device): [nks][64][16]
 // horizontal taps at byte stride `bands` shifted by delta, then [64][16] vertical taps
 const signed char *device_blur_ops(const std::vector<int> &mask, int bands, int delta, int nks);

@@ -13,11 +13,11 @@ from test_parity_gpu import assert_same, rand_img, smooth_img
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["rcol", "default"])
+@pytest.fixture(autouse=True, params=["rcol", "norcol"])
 def route(request, monkeypatch):
-    """k_rcol is opt-in (MIPX_RCOL=1) while it measures slower than k_rmf2; every case
-    runs through it and through the default route."""
-    monkeypatch.setenv("MIPX_RCOL", "1" if request.param == "rcol" else "")
+    """Every case through k_rcol (the default) and through the kernels behind it
+    (MIPX_RCOL=0: k_rmf2 and the strip walker)."""
+    monkeypatch.setenv("MIPX_RCOL", "" if request.param == "rcol" else "0")
     yield request.param
 
 SHRINKS = [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9), (2.7, 1.5),
