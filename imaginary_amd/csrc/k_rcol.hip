@@ -62,6 +62,7 @@ struct RcArgs {
     int strips, segs, seg_steps;
     int k0, ksteps;           // the window's first 16-row group (oy0 / 16) and group count
     int rmask;                // ring rows - 1 (31 or 63)
+    int rcap;                 // ring chunks of rows rcap and below (in a load batch) idle
     int rs;                   // ring row stride in bytes ((rs / 4 mod 64) / 4 odd)
     int iw;                   // intermediate row stride in bytes
     int htaps, hpad;
@@ -186,7 +187,9 @@ __device__ __forceinline__ void lgkm_wait_for(T &...v) {
 
 // KMAX ring chunks per lane per step (16 bytes each), NKS horizontal K steps (64 bytes
 // each), ALN: every output row starts on a dword (one b32 store per unit, else 4 b8).
-template <int B, int NKS, int KMAX, bool ALN>
+// VP: the vertical pass software-pipelined (next pair's transposed reads and this
+// pair's products in flight while the previous pair is rounded and written)
+template <int B, int NKS, int KMAX, bool ALN, bool VP>
 __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
     constexpr int WV = kRcNT / 64, XW = 16 * WV;
     constexpr int UPW = B;  // horizontal units per wave: XW B / 16 / WV
@@ -194,6 +197,7 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rcs[];
     const uint32_t ring_l = rc_lds(rcs);                                            // [rmask + 1][rs]
     const uint32_t inter_l = ring_l + static_cast<uint32_t>((a.rmask + 1) * a.rs);  // [16][iw]
+    const uint32_t dummy_l = inter_l + static_cast<uint32_t>(kRcRows * a.iw);       // [64] dwords (VP)
 
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = static_cast<int>(t % static_cast<uint32_t>(a.strips));
@@ -345,18 +349,24 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
         vl[P] = __builtin_bit_cast(rc_v4i, __builtin_amdgcn_raw_buffer_load_b128(prs, toff + o + 64, 0, 0));
         vsd[P] = __builtin_amdgcn_raw_buffer_load_b32(prs, n * kRcolPlanRow + 128 + o, 0, 0);
     };
+    // chunks of rows rcap and below are idle: their loads take an offset past the image
+    // (no memory access) and they write nothing, so a narrow strip's lanes do not reach
+    // past a step's new rows into ring slots still in use (r03: admits narrow last
+    // strips and shrinks to ~2.5)
     auto issue_ring = [&](auto pc, int r0) {
         constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
-            rv[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     src, clampi(r0 + rr[j], 0, a.h - 1) * pitch + cof[j], 0, 0));
+            rv[P][j] = __builtin_bit_cast(
+                rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
+                           src, rr[j] < a.rcap ? clampi(r0 + rr[j], 0, a.h - 1) * pitch + cof[j] : 0x7ffffff0, 0, 0));
     };
     auto write_ring = [&](auto pc, int r0) {
         constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
-            lds_wr128(static_cast<uint32_t>(((r0 + rr[j]) & a.rmask) * a.rs) + lcol[j], rv[P][j] ^ 0x80808080u);
+            if (rr[j] < a.rcap)
+                lds_wr128(static_cast<uint32_t>(((r0 + rr[j]) & a.rmask) * a.rs) + lcol[j], rv[P][j] ^ 0x80808080u);
     };
     auto store = [&](int k, bool live, const uint32_t *res) {
         const int o = k * kRcRows + n - a.oy0;  // window row of the lane's output row
@@ -392,17 +402,65 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
             lds_wr32(iq + 16 * ct,
                      rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
         };
-        for (int ct = wave; ct < cpr; ct += 2 * WV) {
-            const bool two = ct + WV < cpr;  // uniform
-            rc_v2i t1a = lds_tr8(a1 + 16 * ct), t2a = lds_tr8(a2 + 16 * ct);
-            rc_v2i t1b = t1a, t2b = t2a;
-            if (two) {
-                t1b = lds_tr8(a1 + 16 * (ct + WV));
-                t2b = lds_tr8(a2 + 16 * (ct + WV));
+        if constexpr (VP) {
+            // pair p = tiles ct = wave + 2 WV p and ct + WV.  Iteration p: the 4 reads of
+            // pair p + 1 (clamped to a valid tile past the end), wait for pair p's (6 LDS
+            // ops after them: 2 writes + these 4 reads, dummies included so the count is
+            // static), pair p's 4 products, then pair p - 1's rounding and 2 writes (to
+            // the dummy slot where that pair has no tile)
+            const int np = (cpr - wave + 2 * WV - 1) / (2 * WV);  // uniform
+            if (np <= 0) return;
+            const uint32_t dmy = dummy_l + static_cast<uint32_t>(4 * lane);
+            auto rd = [&](int p, rc_v2i *t) {
+                const int c0 = min(wave + 2 * WV * p, cpr - 1), c1 = min(c0 + WV, cpr - 1);
+                t[0] = lds_tr8(a1 + 16 * c0);
+                t[1] = lds_tr8(a2 + 16 * c0);
+                t[2] = lds_tr8(a1 + 16 * c1);
+                t[3] = lds_tr8(a2 + 16 * c1);
+            };
+            auto fin = [&](uint32_t addr, const rc_v4i &dh, const rc_v4i &dl) {
+                lds_wr32(addr, rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
+                                          (dh[3] << 6) + dl[3]));
+            };
+            rc_v2i cur[4], nxt[4];
+            rd(0, cur);
+            lds_wr32(dmy, 0u);
+            lds_wr32(dmy, 0u);
+            rc_v4i ph0 = rc_v4i{0, 0, 0, 0}, pl0 = ph0, ph1 = ph0, pl1 = ph0;
+            uint32_t pa0 = dmy, pa1 = dmy;
+            for (int p = 0; p < np; ++p) {
+                rd(p + 1, nxt);
+                lgkm_wait_for<6>(cur[0], cur[1], cur[2], cur[3]);
+                const int ct = wave + 2 * WV * p;
+                const rc_v4i av0 = rc_v4i{cur[0].x, cur[0].y, cur[1].x, cur[1].y};
+                const rc_v4i av1 = rc_v4i{cur[2].x, cur[2].y, cur[3].x, cur[3].y};
+                const rc_v4i dh0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av0, bh, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
+                const rc_v4i dl0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av0, bl, rc_v4i{sd, sd, sd, sd}, 0, 0, 0);
+                const rc_v4i dh1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av1, bh, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
+                const rc_v4i dl1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av1, bl, rc_v4i{sd, sd, sd, sd}, 0, 0, 0);
+                fin(pa0, ph0, pl0);
+                fin(pa1, ph1, pl1);
+                ph0 = dh0, pl0 = dl0, ph1 = dh1, pl1 = dl1;
+                pa0 = iq + 16 * ct;
+                pa1 = ct + WV < cpr ? iq + 16 * (ct + WV) : dmy;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
             }
-            lgkm_wait_for<0>(t1a, t2a, t1b, t2b);
-            tile(ct, t1a, t2a);
-            if (two) tile(ct + WV, t1b, t2b);
+            fin(pa0, ph0, pl0);
+            fin(pa1, ph1, pl1);
+        } else {
+            for (int ct = wave; ct < cpr; ct += 2 * WV) {
+                const bool two = ct + WV < cpr;  // uniform
+                rc_v2i t1a = lds_tr8(a1 + 16 * ct), t2a = lds_tr8(a2 + 16 * ct);
+                rc_v2i t1b = t1a, t2b = t2a;
+                if (two) {
+                    t1b = lds_tr8(a1 + 16 * (ct + WV));
+                    t2b = lds_tr8(a2 + 16 * (ct + WV));
+                }
+                lgkm_wait_for<0>(t1a, t2a, t1b, t2b);
+                tile(ct, t1a, t2a);
+                if (two) tile(ct + WV, t1b, t2b);
+            }
         }
     };
     // horizontal pass: units wave + WV i, operands from registers, every unit's LDS
@@ -539,12 +597,13 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     }
     if (nks > 2) return MIPX_EUNSUPPORTED;
     // chunks per lane: the widest strip's rows of the largest step fit one batch; ring:
-    // the rows of a step, and a batch's over-reach past the step's end must only land on
-    // slots of rows above the step's first
+    // the rows of a step, and a batch's rows (at most the rows one step adds) must only
+    // land on slots of rows above the step's first
     int kmax = 0, ring = 0;
+    const int rcap = std::max(maxnew, 1);
     for (int km : {3, 6}) {
-        if ((kRcNT * km) / cpr_max < maxnew) continue;
-        const int reach = (kRcNT * km + cpr_min - 1) / cpr_min;
+        if ((kRcNT * km) / cpr_max < rcap) continue;
+        const int reach = std::min((kRcNT * km + cpr_min - 1) / cpr_min, rcap);
         for (int r : {32, 64}) {
             bool ok = lmax <= r;
             for (int k = a.k0 + 1; ok && k <= k1; ++k) ok = ge(k - 1) + reach <= gb(k) + r;
@@ -554,13 +613,14 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     }
     if (!kmax) return MIPX_EUNSUPPORTED;
     a.rmask = ring - 1;
+    a.rcap = rcap;
     int rs = 4 * cpr_max;  // dwords
     while (((rs & 63) >> 2) % 2 == 0) rs += 4;  // 16 consecutive rows on distinct bank quads
     a.rs = 4 * rs;
     int iw = (std::max(16 * cpr_max, kbmax + 64 * nks) + 16 + 15) & ~15;
     while ((iw / 4) % 8 != 4) iw += 16;  // 4 mod 8 dwords: the intermediate writes hit distinct banks
     a.iw = iw;
-    const size_t lds = static_cast<size_t>(ring) * a.rs + static_cast<size_t>(kRcRows) * iw;
+    const size_t lds = static_cast<size_t>(ring) * a.rs + static_cast<size_t>(kRcRows) * iw + 256;  // + dummy slots
     if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
 
     int plan_rows = 0;
@@ -577,9 +637,13 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
 
     const bool aligned = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
     const void *fn = nullptr;
-#define MIPX_RC_K(B_, NKS_, KM_)                                                                           \
-    fn = aligned ? reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, true>)                            \
-                 : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, false>);
+    const char *evp = tune_env("MIPX_RCOL_VP");  // 1: the software-pipelined vertical pass (A/B)
+    const bool vp = evp && *evp == '1';
+#define MIPX_RC_K(B_, NKS_, KM_)                                                                              \
+    fn = aligned ? (vp ? reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, true, true>)                    \
+                       : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, true, false>))                  \
+                 : (vp ? reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, false, true>)                   \
+                       : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, false, false>));
 #define MIPX_RC_KM(B_, NKS_) \
     if (kmax == 3) { MIPX_RC_K(B_, NKS_, 3) } else { MIPX_RC_K(B_, NKS_, 6) }
     if (b == 3) {

@@ -235,6 +235,8 @@ def engine() -> Engine:
     """The process-wide request engine (mipx_init is idempotent, so this also
     re-initialises after an mipx_shutdown)."""
     global _ENGINE
+    if _ENGINE is not None and _abi.lib.mipx_queue_count() > 0:
+        return _ENGINE  # still up (possibly started by another Engine with its own config)
     _ENGINE = Engine()
     return _ENGINE
 

@@ -28,6 +28,7 @@ SHAPES = [  # w, h, b, n, hs, vs  (op_survey rows)
     (1024, 1024, 4, 512, 1.3333333333333333, 1.3333333333333333),
     (1920, 1080, 4, 64, 1.6, 1.6),
     (1000, 750, 3, 64, 1.5625, 1.5625),
+    (1333, 1000, 3, 48, 1.6666666666666667, 1.6666666666666667),
 ]
 if os.environ.get("SHAPES"):
     SHAPES = [tuple(float(v) if "." in v else int(v) for v in s.split(",")) for s in os.environ["SHAPES"].split(";")]

@@ -211,7 +211,7 @@ def test_rot90_tile_orders(gpu, oracle, rng, monkeypatch, xcd, th, tc, order):
     monkeypatch.setenv("MIPX_ROT_TH", th)
     monkeypatch.setenv("MIPX_ROT_T", tc)
     monkeypatch.setenv("MIPX_ROT_ORDER", order)
-    for h, w, b in ((130, 197, 3), (65, 300, 4), (200, 129, 1), (67, 131, 2), (261, 70, 4)):
+    for h, w, b in ((130, 197, 3), (65, 300, 4), (200, 129, 1), (67, 131, 2), (261, 70, 4), (128, 160, 3), (96, 64, 3)):
         imgs = np.stack([rand_img(rng, h, w, b) for _ in range(3)])
         for a in (90, 270):
             got = gpu.run_op("rot", imgs, angle=a)
@@ -642,6 +642,7 @@ def test_watermark_plan(gpu, oracle, rng):
 
 def test_request_path_batches_and_matches(gpu, oracle, rng):
     """mipx_submit/mipx_wait: pinned staging, queue, cross-request batching."""
+    gpu.lib.mipx_shutdown()  # mipx_init refuses another configuration while one runs
     eng = gpu.Engine(max_batch=8)
     try:
         p = gpu.plan_make(gpu.make_opts(width=160, height=120, embed=1), gpu.make_input(320, 240, 3, "png"))
@@ -660,6 +661,7 @@ def test_request_path_concurrent_mixed_plans(gpu, oracle, rng):
     result matches the oracle, batches fuse requests, the three-stream pipeline
     retires everything."""
     from concurrent.futures import ThreadPoolExecutor
+    gpu.lib.mipx_shutdown()  # mipx_init refuses another configuration while one runs
     eng = gpu.Engine(max_batch=16, batch_wait_us=2000)
     try:
         specs = [(dict(width=160, height=120, embed=1), (320, 240, 3)),
