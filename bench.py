@@ -32,6 +32,10 @@ W_OUT, H_OUT = 1920, 1080
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+# MIPX_REDUCE_CENTRE=1: libvips' centre sampling convention (PARITY_ASSUMPTIONS.md row 1), checked
+# against the oracle under the same switch
+CENTRE = os.environ.get("MIPX_REDUCE_CENTRE") == "1"
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -243,6 +247,8 @@ def main():
     verify = None
     if not args.no_verify and rank == 0:
         from oracle import oracle as o
+        if CENTRE:
+            o.set_switch("reduce_centre", 1)
         idx = [0, n - 1]
         got = d_out[idx].cpu().numpy().reshape(len(idx), H_OUT, W_OUT, BANDS)
         src = d_in[idx].cpu().numpy().reshape(len(idx), H_IN, W_IN, BANDS)
@@ -270,7 +276,9 @@ def main():
             "dtype": "u8",
             "data": "synthetic uniform-random uchar, device-resident (seed 20241220+rank)",
             "config": {"workload": "C2: batched 3840x2160x3 -> 1920x1080x3 Lanczos3 reduce (bimg "
-                                   "/resize?width=1920&height=1080), fused k_reduce2x2",
+                                   "/resize?width=1920&height=1080), " +
+                                   ("centre sampling convention (PARITY_ASSUMPTIONS row 1 flipped), k_rcol"
+                                    if CENTRE else "fused k_reduce2x2"),
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world} (independent shards)"},
             "achieved_hbm_gbs": round(achieved, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

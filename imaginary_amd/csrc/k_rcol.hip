@@ -24,7 +24,9 @@
 //     B (start(x) + k - org) + c; those operands depend on the column only and are
 //     held in registers for the whole segment (the COPY edge folded in at the image
 //     edges), as are the per-byte seeds.  Two ds_read_b64 and two MFMAs per unit and
-//     K step, one output dword per lane, stored straight from registers.
+//     K step; a wave's units are consecutive, and its 16 rows x 16 B dwords go through a
+//     wave-private LDS tile to 16-byte row pieces (r03: the 4-byte stores of 16 rows per
+//     instruction had capped the kernel; the memory-only pattern, scripts/strip_probe.hip).
 // Loads past the image read zeros (buffer range check); rows clamp at the load (COPY
 // edge); columns past the image carry zero weight after the fold.
 //
@@ -74,6 +76,7 @@ struct RcArgs {
     const float *tabf;        // device_reduce_table(hs): [129][htaps] (edge operands, narrow images)
     const signed char *tabhf; // device_reduce_i8s_fold(hs, B): the COPY edge folded in
     int centre;               // MIPX_REDUCE_CENTRE: centre sampling convention
+    int wst;                  // each wave's 16 rows x 16 UPW bytes go out as 16-byte row pieces
 };
 
 // libvips reduce position (reducev.cpp / reduceh.cpp): X = reduce_x (o * shrink, or
@@ -186,18 +189,14 @@ __device__ __forceinline__ void lgkm_wait_for(T &...v) {
 }
 
 // KMAX ring chunks per lane per step (16 bytes each), NKS horizontal K steps (64 bytes
-// each), ALN: every output row starts on a dword (one b32 store per unit, else 4 b8).
-// VP: the vertical pass software-pipelined (next pair's transposed reads and this
-// pair's products in flight while the previous pair is rounded and written)
-template <int B, int NKS, int KMAX, bool ALN, bool VP>
+// each).  Output rows start on a dword (host-checked).
+template <int B, int NKS, int KMAX>
 __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
     constexpr int WV = kRcNT / 64, XW = 16 * WV;
     constexpr int UPW = B;  // horizontal units per wave: XW B / 16 / WV
-    constexpr int SB = ALN ? 1 : 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t rcs[];
     const uint32_t ring_l = rc_lds(rcs);                                            // [rmask + 1][rs]
     const uint32_t inter_l = ring_l + static_cast<uint32_t>((a.rmask + 1) * a.rs);  // [16][iw]
-    const uint32_t dummy_l = inter_l + static_cast<uint32_t>(kRcRows * a.iw);       // [64] dwords (VP)
 
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = static_cast<int>(t % static_cast<uint32_t>(a.strips));
@@ -240,7 +239,7 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
     int kb[UPW];
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
-        const int u = wave + WV * i;
+        const int u = a.wst ? UPW * wave + i : wave + WV * i;
         int sf, pf;
         rc_pos(a.ox0 + min(x0 + (16 * u) / B, x_last), a.hs, a.hpad, &sf, &pf, a.centre);
         kb[i] = __builtin_amdgcn_readfirstlane((B * (sf - org) + (16 * u) % B) & ~7);  // K origin (8-byte aligned)
@@ -273,18 +272,17 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
     // per output byte seeds of the horizontal pass (lane: bytes 16 u + 4 kg + j of row n)
     // and store offsets (past the strip's last byte: beyond any image, so dropped)
     rc_v4i hb[UPW];
-    uint32_t sto[UPW][SB];
+    uint32_t sto[UPW];
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
-        const int e = 16 * (wave + WV * i) + 4 * kg;
+        const int e = 16 * (a.wst ? UPW * wave + i : wave + WV * i) + 4 * kg;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             int sp, pp;
             rc_pos(a.ox0 + min(x0 + (e + j) / B, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
             hb[i][j] = 128 * a.sumh[pp] + 2048;
         }
-#pragma unroll
-        for (int j = 0; j < SB; ++j) sto[i][j] = e + j < vbytes ? static_cast<uint32_t>(B * x0 + e + j) : 0x20000000u;
+        sto[i] = e < vbytes ? static_cast<uint32_t>(B * x0 + e) : 0x20000000u;
     }
 
     // ring chunks: chunk c = tid + 256 j of a step's rows is (row rr, column col); the
@@ -368,20 +366,36 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
             if (rr[j] < a.rcap)
                 lds_wr128(static_cast<uint32_t>(((r0 + rr[j]) & a.rmask) * a.rs) + lcol[j], rv[P][j] ^ 0x80808080u);
     };
+    // wst: the wave's units are consecutive (bytes 16 UPW wave ..), staged through a
+    // wave-private LDS tile [16 rows][16 UPW (+ 16 for RGBA: bank spread) bytes] and
+    // stored as 16-byte pieces: 16 UPW contiguous bytes per row instead of 16
+    constexpr int WSR = 16 * UPW + (UPW == 4 ? 16 : 0);
+    const uint32_t wst_l = inter_l + static_cast<uint32_t>(kRcRows * a.iw + wave * kRcRows * WSR);
+    const int wrow = min(lane / UPW, kRcRows - 1), wch = lane - UPW * (lane / UPW);  // read-back: row, 16-byte chunk
+    const int we = 16 * (UPW * wave + wch);                          // its first byte in the strip row
     auto store = [&](int k, bool live, const uint32_t *res) {
+        if (a.wst) {
+#pragma unroll
+            for (int i = 0; i < UPW; ++i) lds_wr32(wst_l + static_cast<uint32_t>(n * WSR + 16 * i + 4 * kg), res[i]);
+            rc_u4 q = lds_rd128(wst_l + static_cast<uint32_t>(wrow * WSR + 16 * wch));
+            lgkm_wait_for<0>(q);
+            const int o = k * kRcRows + wrow - a.oy0;
+            const bool ok = live && lane < 16 * UPW && o >= 0 && o < a.oh;
+            const int base = o * a.ow * B + B * x0 + we;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, q), dst,
+                                                   ok && we + 16 <= vbytes ? base : 0x7ffffff0, 0, 0);
+            if (a.wst > 1) {  // rows whose byte count is not a multiple of 16: the piece at the image edge in dwords
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    __builtin_amdgcn_raw_buffer_store_b32(
+                        q[j], dst, ok && we + 16 > vbytes && we + 4 * j < vbytes ? base + 4 * j : 0x7ffffff0, 0, 0);
+            }
+            return;
+        }
         const int o = k * kRcRows + n - a.oy0;  // window row of the lane's output row
         const uint32_t rb = live && o >= 0 && o < a.oh ? static_cast<uint32_t>(o * a.ow * B) : 0x80000000u;
 #pragma unroll
-        for (int i = 0; i < UPW; ++i) {
-            if constexpr (ALN) {
-                __builtin_amdgcn_raw_buffer_store_b32(res[i], dst, static_cast<int>(rb + sto[i][0]), 0, 0);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(res[i] >> (8 * j)), dst,
-                                                         static_cast<int>(rb + sto[i][j]), 0, 0);
-            }
-        }
+        for (int i = 0; i < UPW; ++i) __builtin_amdgcn_raw_buffer_store_b32(res[i], dst, static_cast<int>(rb + sto[i]), 0, 0);
     };
     // vertical pass: 16-byte column tiles dealt to the waves, two in flight per wait.  K
     // index 16 kg + e holds relative row 8 kg + e (e < 8) or 32 + 8 kg + e - 8, so the 16
@@ -402,53 +416,6 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
             lds_wr32(iq + 16 * ct,
                      rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
         };
-        if constexpr (VP) {
-            // pair p = tiles ct = wave + 2 WV p and ct + WV.  Iteration p: the 4 reads of
-            // pair p + 1 (clamped to a valid tile past the end), wait for pair p's (6 LDS
-            // ops after them: 2 writes + these 4 reads, dummies included so the count is
-            // static), pair p's 4 products, then pair p - 1's rounding and 2 writes (to
-            // the dummy slot where that pair has no tile)
-            const int np = (cpr - wave + 2 * WV - 1) / (2 * WV);  // uniform
-            if (np <= 0) return;
-            const uint32_t dmy = dummy_l + static_cast<uint32_t>(4 * lane);
-            auto rd = [&](int p, rc_v2i *t) {
-                const int c0 = min(wave + 2 * WV * p, cpr - 1), c1 = min(c0 + WV, cpr - 1);
-                t[0] = lds_tr8(a1 + 16 * c0);
-                t[1] = lds_tr8(a2 + 16 * c0);
-                t[2] = lds_tr8(a1 + 16 * c1);
-                t[3] = lds_tr8(a2 + 16 * c1);
-            };
-            auto fin = [&](uint32_t addr, const rc_v4i &dh, const rc_v4i &dl) {
-                lds_wr32(addr, rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
-                                          (dh[3] << 6) + dl[3]));
-            };
-            rc_v2i cur[4], nxt[4];
-            rd(0, cur);
-            lds_wr32(dmy, 0u);
-            lds_wr32(dmy, 0u);
-            rc_v4i ph0 = rc_v4i{0, 0, 0, 0}, pl0 = ph0, ph1 = ph0, pl1 = ph0;
-            uint32_t pa0 = dmy, pa1 = dmy;
-            for (int p = 0; p < np; ++p) {
-                rd(p + 1, nxt);
-                lgkm_wait_for<6>(cur[0], cur[1], cur[2], cur[3]);
-                const int ct = wave + 2 * WV * p;
-                const rc_v4i av0 = rc_v4i{cur[0].x, cur[0].y, cur[1].x, cur[1].y};
-                const rc_v4i av1 = rc_v4i{cur[2].x, cur[2].y, cur[3].x, cur[3].y};
-                const rc_v4i dh0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av0, bh, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
-                const rc_v4i dl0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av0, bl, rc_v4i{sd, sd, sd, sd}, 0, 0, 0);
-                const rc_v4i dh1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av1, bh, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
-                const rc_v4i dl1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(av1, bl, rc_v4i{sd, sd, sd, sd}, 0, 0, 0);
-                fin(pa0, ph0, pl0);
-                fin(pa1, ph1, pl1);
-                ph0 = dh0, pl0 = dl0, ph1 = dh1, pl1 = dl1;
-                pa0 = iq + 16 * ct;
-                pa1 = ct + WV < cpr ? iq + 16 * (ct + WV) : dmy;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
-            }
-            fin(pa0, ph0, pl0);
-            fin(pa1, ph1, pl1);
-        } else {
             for (int ct = wave; ct < cpr; ct += 2 * WV) {
                 const bool two = ct + WV < cpr;  // uniform
                 rc_v2i t1a = lds_tr8(a1 + 16 * ct), t2a = lds_tr8(a2 + 16 * ct);
@@ -461,7 +428,6 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
                 tile(ct, t1a, t2a);
                 if (two) tile(ct + WV, t1b, t2b);
             }
-        }
     };
     // horizontal pass: units wave + WV i, operands from registers, every unit's LDS
     // reads in flight together
@@ -544,6 +510,8 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // out-of-range store offsets are built from 2^29 and 2^31 (k_rcol store)
     if (in_img >= 0x7fffffffLL || out_img >= (1LL << 29)) return MIPX_EUNSUPPORTED;
     if ((w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0) return MIPX_EUNSUPPORTED;
+    // output rows on a dword (else k_rmf2: byte stores here ran 1.2x slower there, r03)
+    if ((ow * b) % 4 != 0 || reinterpret_cast<uintptr_t>(out) % 4 != 0) return MIPX_EUNSUPPORTED;
     const int vtaps = reduce_points(vs), htaps = reduce_points(hs);
     if (vtaps > 16 || htaps > 16) return MIPX_EUNSUPPORTED;
     const bool centre = reduce_centre();
@@ -620,7 +588,9 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     int iw = (std::max(16 * cpr_max, kbmax + 64 * nks) + 16 + 15) & ~15;
     while ((iw / 4) % 8 != 4) iw += 16;  // 4 mod 8 dwords: the intermediate writes hit distinct banks
     a.iw = iw;
-    const size_t lds = static_cast<size_t>(ring) * a.rs + static_cast<size_t>(kRcRows) * iw + 256;  // + dummy slots
+    // + the wave store tiles (4 x 16 rows x (16 B + 16 for RGBA))
+    const size_t lds = static_cast<size_t>(ring) * a.rs + static_cast<size_t>(kRcRows) * iw +
+                       static_cast<size_t>(4 * kRcRows * (16 * b + (b == 4 ? 16 : 0)));
     if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
 
     int plan_rows = 0;
@@ -635,15 +605,12 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     a.tabhf = device_reduce_i8s_fold(hs, b, &nfh);
     if (!a.tabh || !a.tabf || !a.tabhf || nth != htaps || ntf != htaps || nfh != htaps) return MIPX_EDEVICE;
 
-    const bool aligned = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
+    // r03: 16-byte row pieces through a wave tile (1080p RGB / 1.6 -16 %, 1024^2 RGBA / 1.333
+    // -31 %, profiles/r03/rcol_wst_ab.jsonl); MIPX_RCOL_WST=0 keeps the 4-byte stores (A/B)
+    const char *ews = tune_env("MIPX_RCOL_WST");
+    a.wst = !(ews && *ews == '0') ? ((ow * b) % 16 == 0 ? 1 : 2) : 0;
     const void *fn = nullptr;
-    const char *evp = tune_env("MIPX_RCOL_VP");  // 1: the software-pipelined vertical pass (A/B)
-    const bool vp = evp && *evp == '1';
-#define MIPX_RC_K(B_, NKS_, KM_)                                                                              \
-    fn = aligned ? (vp ? reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, true, true>)                    \
-                       : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, true, false>))                  \
-                 : (vp ? reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, false, true>)                   \
-                       : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, false, false>));
+#define MIPX_RC_K(B_, NKS_, KM_) fn = reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_>);
 #define MIPX_RC_KM(B_, NKS_) \
     if (kmax == 3) { MIPX_RC_K(B_, NKS_, 3) } else { MIPX_RC_K(B_, NKS_, 6) }
     if (b == 3) {

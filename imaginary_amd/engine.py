@@ -128,12 +128,19 @@ class Engine:
         sync_tuning()
         check(lib.mipx_init(C.byref(cfg)), "mipx_init")
 
-    def submit(self, plan: MipxPlan, img: np.ndarray, wm: Optional[np.ndarray] = None, device: int = -1):
+    def submit(self, plan: MipxPlan, img: np.ndarray, wm: Optional[np.ndarray] = None, device: int = -1,
+               out: Optional[np.ndarray] = None):
+        """Queue one request; returns (ticket, out).  `out` (optional) receives the
+        result: contiguous uint8 of the plan's output shape."""
         sync_tuning()
         if not (img.dtype == np.uint8 and img.ndim == 3 and img.strides[2] == 1
                 and img.strides[1] == img.shape[2]):
             img = np.ascontiguousarray(img, dtype=np.uint8)  # rows may keep a wider stride
-        out = np.empty((plan.out_h, plan.out_w, plan.out_bands), np.uint8)
+        shape = (plan.out_h, plan.out_w, plan.out_bands)
+        if out is None:
+            out = np.empty(shape, np.uint8)
+        elif out.shape != shape or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            raise ValueError(f"out must be contiguous uint8 {shape}")
         ti = C.c_uint64()
         wmi = C.byref(_img(np.ascontiguousarray(wm, dtype=np.uint8))) if wm is not None else None
         check(lib.mipx_submit(device, C.byref(plan), C.byref(_img(img)), wmi, C.byref(_img(out)),

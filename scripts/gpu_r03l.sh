@@ -1,0 +1,8 @@
+# r03 checkpoint: k_rcol 16-byte row-piece stores default; full GPU suite, A/B, op survey, configs
+set -u; cd $GRAFT_REPO_ROOT; O=gpurun_out/r03l; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 800 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?; tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+VARIANTS='MIPX_RCOL_WST=1;MIPX_RCOL_WST=0;MIPX_RCOL=0' timeout -k 10 400 python3 -u scripts/ab_rcol.py > $O/ab_rcol.jsonl 2> $O/ab_rcol.err || { tail $O/ab_rcol.err; exit 1; }
+cat $O/ab_rcol.jsonl
+timeout -k 10 300 python3 -u bench_configs.py --configs C3,C4,C5 --steps 10 --warmup 2 > $O/configs.jsonl 2> $O/configs.err || { tail $O/configs.err; exit 1; }
+cut -c1-260 $O/configs.jsonl
+bash scripts/op_survey.sh > $O/op_survey.txt 2>&1; rc=$?; cp gpurun_out/op_survey.jsonl $O/; cat $O/op_survey.txt; exit $rc

@@ -7,7 +7,7 @@ i=0
 while read -r ctrs; do
   [ -z "$ctrs" ] && continue
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $ctrs --output-format csv -d "$OUT/p$i" -o run -- python3 "$R/scripts/op_bench.py" $OP_ARGS --iters 3 > "$OUT/p$i.log" 2>&1
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $ctrs --output-format csv -d "$OUT/p$i" -o run -- python3 "$R/scripts/op_bench.py" $OP_ARGS --iters 3 --warm-ms 0 > "$OUT/p$i.log" 2>&1
   rc=$?; if [ $rc -ne 0 ]; then echo "pass $i rc=$rc"; tail -5 "$OUT/p$i.log"; exit $rc; fi
 done <<LIST
 ${PMC_LIST:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES

@@ -1,0 +1,154 @@
+// Memory-only ceilings for the generic reduce's access pattern (k_rcol without the
+// arithmetic): 64 x 1920x1080x3 images in, 1200x675x3 out (shrink 1.6).
+//   strip  a block walks a vertical strip of SPX output pixels (span SPX * 1.6 + 11 input
+//          pixels) down a segment of 16-row steps; each step loads the ~26 input rows it
+//          adds with 16-byte buffer loads (the lane -> (row, chunk) map of k_rcol, two
+//          steps in flight) and stores 16 output rows of the strip as dwords
+//   band   the same rows, but a block owns a band of whole rows (every strip of the
+//          image side by side): the row-major order of the two-pass kernels
+// One JSON line per (pattern, strip width, steps per block).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+struct P {
+    const uint8_t *in;
+    uint8_t *out;
+    int w, h, ow, oh, strips, segs, seg_steps, ksteps, cpr, spx;
+    long long in_img, out_img;
+    float s;
+};
+
+__device__ __forceinline__ int grow(int k, float s) { return static_cast<int>(16 * k * s); }  // first input row of step k
+
+// XCD-contiguous block order (as the engine's xcd_remap): XCD x walks t in its own range
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
+    const uint32_t xcd = b & 7u, q = nb >> 3, r = nb & 7u;
+    const uint32_t base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (b >> 3);
+}
+
+// MODE bit 0: XCD-contiguous order; bit 1: no loads; bit 2: no stores
+template <int KM, int MODE>
+__global__ void __launch_bounds__(256) strip(P a) {
+    const int t = (MODE & 1) ? static_cast<int>(xcd_remap(blockIdx.x, gridDim.x)) : static_cast<int>(blockIdx.x);
+    const int st = t % a.strips, rest = t / a.strips, seg = rest % a.segs, img = rest / a.segs;
+    const int tid = threadIdx.x;
+    const int pitch = a.w * 3;
+    const int x0 = st * a.spx;
+    const int b0 = (static_cast<int>(x0 * a.s) * 3 - 15) & ~15;
+    const __amdgpu_buffer_rsrc_t src =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.in + img * a.in_img), 0, static_cast<int>(a.in_img), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dst =
+        __builtin_amdgcn_make_buffer_rsrc(a.out + img * a.out_img, 0, static_cast<int>(a.out_img), 0x00020000);
+    int rr[KM], cof[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        const int c = tid + 256 * j;
+        rr[j] = c / a.cpr;
+        cof[j] = b0 + 16 * (c - rr[j] * a.cpr);
+    }
+    const int ka = seg * a.seg_steps, kz = min(a.ksteps, ka + a.seg_steps);
+    u4v v0[KM], v1[KM];
+    uint32_t acc = 0;
+    auto issue = [&](u4v *v, int k) {
+        const int r0 = grow(k, a.s), r1 = grow(k + 1, a.s);
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+            v[j] = (MODE & 2) ? u4v{0u, 0u, 0u, static_cast<uint32_t>(k)} : __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                               src, rr[j] < r1 - r0 ? min(r0 + rr[j], a.h - 1) * pitch + cof[j] : 0x7ffffff0, 0, 0));
+    };
+    const int obw = a.spx * 3, nd = obw / 4;  // output dwords per strip row
+    auto store = [&](int k) {
+        if (MODE & 4) {
+            if (acc == 0x9e3779b9u) __builtin_amdgcn_raw_buffer_store_b32(acc, dst, 0, 0, 0);
+            return;
+        }
+        for (int i = tid; i < 16 * nd; i += 256) {
+            const int r = i / nd, d = i - r * nd, y = 16 * k + r;
+            const int off = y < a.oh && x0 + (4 * d) / 3 < a.ow ? (y * a.ow + x0) * 3 + 4 * d : 0x7ffffff0;
+            __builtin_amdgcn_raw_buffer_store_b32(acc + i, dst, off, 0, 0);
+        }
+    };
+    issue(v0, ka);
+    issue(v1, ka + 1);
+    for (int k = ka; k < kz; k += 2) {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) acc ^= v0[j].x ^ v0[j].w;
+        issue(v0, k + 2);
+        store(k);
+        if (k + 1 < kz) {
+#pragma unroll
+            for (int j = 0; j < KM; ++j) acc ^= v1[j].y ^ v1[j].z;
+            issue(v1, k + 3);
+            store(k + 1);
+        }
+    }
+}
+
+template <class F>
+static float time_it(F launch) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    for (int i = 0; i < 3; ++i) launch();
+    std::vector<float> v;
+    for (int g = 0; g < 5; ++g) {
+        hipEventRecord(a);
+        for (int i = 0; i < 10; ++i) launch();
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        v.push_back(ms / 10);
+    }
+    std::sort(v.begin(), v.end());
+    return v[2];
+}
+
+int main() {
+    const int n = 64, W = 1920, H = 1080, OW = 1200, OH = 675;
+    const float s = 1.6f;
+    const long long in_img = 1LL * W * H * 3, out_img = 1LL * OW * OH * 3;
+    uint8_t *in, *out;
+    CK(hipMalloc(&in, n * in_img + 4096));
+    CK(hipMalloc(&out, n * out_img + 4096));
+    CK(hipMemset(in, 1, n * in_img));
+    CK(hipDeviceSynchronize());
+    const double bytes = static_cast<double>(n) * (in_img + out_img);
+    const int ksteps = (OH + 15) / 16;
+    auto run = [&](const char *name, int spx, int ss, int mode) {
+        const int span = static_cast<int>(spx * s) * 3 + 11 * 3 + 16;
+        const int cpr = (span + 15) / 16;
+        const int km = (26 * cpr + 255) / 256;
+        P a{};
+        a.in = in, a.out = out, a.w = W, a.h = H, a.ow = OW, a.oh = OH, a.s = s, a.spx = spx;
+        a.strips = (OW + spx - 1) / spx, a.ksteps = ksteps, a.seg_steps = ss, a.segs = (ksteps + ss - 1) / ss;
+        a.cpr = cpr, a.in_img = in_img, a.out_img = out_img;
+        const unsigned blocks = static_cast<unsigned>(a.strips) * a.segs * n;
+        float ms = -1;
+#define SP_RUN(KM_) \
+        if (mode == 0) ms = time_it([&] { strip<KM_, 0><<<blocks, 256>>>(a); }); \
+        else if (mode == 1) ms = time_it([&] { strip<KM_, 1><<<blocks, 256>>>(a); }); \
+        else if (mode == 3) ms = time_it([&] { strip<KM_, 3><<<blocks, 256>>>(a); }); \
+        else if (mode == 5) ms = time_it([&] { strip<KM_, 5><<<blocks, 256>>>(a); });
+        if (km <= 3) { SP_RUN(3) } else if (km <= 5) { SP_RUN(5) } else if (km <= 9) { SP_RUN(9) } else return;
+        printf("{\"pattern\": \"%s\", \"spx\": %d, \"span_B\": %d, \"steps\": %d, \"mode\": %d, \"blocks\": %u, \"ms\": %.4f, \"GBps\": %.1f}\n",
+               name, spx, 16 * cpr, ss, mode, blocks, ms, bytes / ms / 1e6);
+        fflush(stdout);
+    };
+    for (int spx : {64, 128, 256}) {
+        run("strip", spx, 11, 0);
+        run("strip_xcd", spx, 11, 1);
+        run("stores_only_xcd", spx, 11, 3);
+        run("loads_only_xcd", spx, 11, 5);
+    }
+    return 0;
+}

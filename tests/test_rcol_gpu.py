@@ -13,11 +13,13 @@ from test_parity_gpu import assert_same, rand_img, smooth_img
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["rcol", "norcol"])
+@pytest.fixture(autouse=True, params=["rcol", "rcol4b", "norcol"])
 def route(request, monkeypatch):
-    """Every case through k_rcol (the default) and through the kernels behind it
+    """Every case through k_rcol (the default: 16-byte row pieces through a wave
+    tile), k_rcol with 4-byte stores (MIPX_RCOL_WST=0), and the kernels behind it
     (MIPX_RCOL=0: k_rmf2 and the strip walker)."""
-    monkeypatch.setenv("MIPX_RCOL", "" if request.param == "rcol" else "0")
+    monkeypatch.setenv("MIPX_RCOL", "0" if request.param == "norcol" else "")
+    monkeypatch.setenv("MIPX_RCOL_WST", "0" if request.param == "rcol4b" else "")
     yield request.param
 
 SHRINKS = [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9), (2.7, 1.5),

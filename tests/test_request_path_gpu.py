@@ -110,8 +110,9 @@ def test_cancel_after_timeout_detaches_the_output(gpu):
         tickets = []
         outs = []
         for _ in range(6):
-            t, out = eng.submit(p, img)
-            out[:] = sentinel
+            # the sentinel goes in before the submit: the request may complete before it returns
+            out = np.full((1080, 1920, 3), sentinel, np.uint8)
+            t, out = eng.submit(p, img, out=out)
             tickets.append(t)
             outs.append(out)
         code = gpu.lib.mipx_wait(tickets[-1], 0)
