@@ -1,0 +1,379 @@
+// k_bcol.hip — libvips vips_gaussblur (convsep.c: the horizontal 1 x n integer mask,
+// then the vertical one, through convi.c: uchar intermediate, (sum + (scale + 1) / 2) /
+// scale, clipped, EXTEND_COPY edges) as a column walker on the i8 matrix cores, r03.
+//
+// A block (4 waves) owns a strip of 64 output pixels of one image (or window) and walks
+// a segment of its rows, 16 output rows per step:
+//   * loads: the 16 input rows a step's horizontal pass needs (16 j + half ..) are
+//     loaded as 16-byte chunks into registers two steps ahead, flipped to p - 128 and
+//     written to one of two staging buffers in LDS (the step's parity), one barrier per
+//     step.  Strips at the window edges repeat the edge pixel into the staged halo
+//     (COPY) after a second barrier;
+//   * horizontal: a wave owns UPW consecutive 16-byte output units of the strip; per
+//     unit, D[output byte][row] = A[output byte][K] x B[K][row] on
+//     v_mfma_i32_16x16x64_i8 with A = the banded taps (tap k at K = o + delta + B k,
+//     the same for every unit: registers) and B = 16 staged rows' bytes; the rounded
+//     uchar (as T - 128) goes to a ring of intermediate rows in LDS;
+//   * vertical: per 16-byte column of the wave's own units, D[byte][output row] = A[byte]
+//     [ring row] x B[ring row][output row], A from two ds_read_b64_tr_b8, B the banded
+//     taps (registers).  A wave reads only the ring columns it wrote, so the vertical
+//     pass needs no barrier;
+//   * stores: 16 rows x 16 UPW bytes through a wave-private LDS tile as 16-byte row pieces.
+// Every input row is loaded and filtered once per segment; the first steps of a segment
+// filter the rows above it (taps - 1 of them).  Bit-identical to the two convi passes
+// (oracle/vips_ref.c convi_pass): the same integer sums, the same rounding (magic
+// multiply exact for sums below 2^32 / scale) and the same clamped edges.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "device_common.h"
+#include "lds_ops.h"
+
+namespace mipx {
+namespace {
+
+using namespace dev;
+
+constexpr int kBcRows = 16;  // rows per step (the MFMA N)
+constexpr int kBcNT = 256;   // threads per block
+
+struct BcArgs {
+    const u8 *in;
+    u8 *out;
+    long long in_base;  // byte offset of the window origin in an image
+    int in_pitch;
+    long long in_img, out_img;
+    int w, h;           // window = output size (COPY clamp range)
+    int strips, segs, seg_steps, ksteps;
+    int half;           // taps / 2
+    int sx0;            // staged rows start at window pixel x0 - sx0 (B sx0 a multiple of 16)
+    int spx;            // staged pixels per strip row
+    int kb0;            // the H operand's first staged byte (e & ~3, e = B (sx0 - half))
+    int cpr;            // 16-byte chunks per staged row
+    int rsd;            // staging row stride (bytes)
+    int rmask, tw;      // ring rows - 1, ring row stride (bytes)
+    int pre;            // filter-only steps before a segment's first output step
+    uint32_t mag;       // floor(x / scale) == mulhi(x, mag) for the sums here
+    int seed;           // 128 scale + (scale + 1) / 2
+    int wst2;           // output rows not a multiple of 16 bytes: the edge piece as dwords
+    const signed char *ops;  // device_blur_ops: [NKS][64 lanes][16] horizontal, then [64][16] vertical
+};
+
+__device__ __forceinline__ uint32_t bc_pack(const rc_v4i &d, uint32_t mag) {
+    const int t0 = __umulhi(static_cast<uint32_t>(d[0]), mag), t1 = __umulhi(static_cast<uint32_t>(d[1]), mag);
+    const int t2 = __umulhi(static_cast<uint32_t>(d[2]), mag), t3 = __umulhi(static_cast<uint32_t>(d[3]), mag);
+    uint32_t lo, hi;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 0" : "=v"(lo) : "v"(t0), "v"(t1));
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 0" : "=v"(hi) : "v"(t2), "v"(t3));
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
+// 8 bytes at a 4-byte-aligned LDS address (two adjacent dwords, one instruction)
+__device__ __forceinline__ rc_u2 lds_rd2x32(uint32_t a) {
+    rc_u2 v;
+    asm volatile("ds_read2_b32 %0, %1 offset1:1" : "=v"(v) : "v"(a));
+    return v;
+}
+
+// B: bands, NKS: horizontal K steps of 64 bytes, KMAX: staging chunks per lane per step,
+// PX: output pixels per strip (64 / 128)
+template <int B, int NKS, int KMAX, int PX>
+__global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
+    constexpr int UPW = B * PX / 64;  // 16-byte units per wave: PX B / 16 over the 4 waves
+    constexpr int WSR = 16 * UPW + (UPW % 2 == 0 ? 16 : 0);  // dwords = 4 mod 8: the tile writes on distinct banks
+    constexpr int NPC = (16 * UPW + 63) / 64;                  // 16-byte row pieces per lane
+    extern __shared__ __attribute__((aligned(16))) uint32_t bcs[];
+    const uint32_t stg_l = rc_lds(bcs);                                                  // [2][16][rsd]
+    const uint32_t ring_l = stg_l + static_cast<uint32_t>(2 * kBcRows * a.rsd);          // [rmask + 1][tw]
+    const uint32_t wst_l0 = ring_l + static_cast<uint32_t>((a.rmask + 1) * a.tw);        // [WV][16][WSR]
+    u8 *stgb = reinterpret_cast<u8 *>(bcs);
+
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int strip = static_cast<int>(t % static_cast<uint32_t>(a.strips));
+    const int rest = static_cast<int>(t / static_cast<uint32_t>(a.strips));
+    const int seg = rest % a.segs;
+    const int img = __builtin_amdgcn_readfirstlane(rest / a.segs);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n = lane & 15, kg = lane >> 4;
+
+    const int x0 = strip * PX, xw = min(PX, a.w - x0);
+    const int vbytes = B * xw;
+    const int sx = x0 - a.sx0;                              // window pixel of staged pixel 0
+    const bool edge = sx < 0 || sx + a.spx > a.w;           // block-uniform
+    const int ka = seg * a.seg_steps, kz = min(a.ksteps, ka + a.seg_steps);
+    const int j0 = ka - a.pre;                              // first (filter-only) step
+
+    const __amdgpu_buffer_rsrc_t src = image_rsrc(a.in + img * a.in_img, a.in_img);
+    const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
+
+    // operands: horizontal taps per K step and the vertical banded taps (registers)
+    rc_v4i ta[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) ta[ks] = *reinterpret_cast<const rc_v4i *>(a.ops + (ks * 64 + lane) * 16);
+    const rc_v4i tb = *reinterpret_cast<const rc_v4i *>(a.ops + (NKS * 64 + lane) * 16);
+
+    // staging chunks: chunk c = tid + 256 k of a step is (row rr, column col)
+    int rr[KMAX], cof[KMAX];
+    uint32_t lsl[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        const int c = tid + kBcNT * k;
+        rr[k] = c / a.cpr;
+        const int col = c - rr[k] * a.cpr;
+        cof[k] = static_cast<int>(a.in_base) + B * sx + 16 * col;
+        lsl[k] = static_cast<uint32_t>(rr[k] * a.rsd + 16 * col);
+    }
+    rc_u4 rv[2][KMAX];
+    auto issue = [&](auto pc, int j) {  // the input rows of step j: 16 j + half + rr
+        constexpr int P = decltype(pc)::value;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int r = clampi(kBcRows * j + a.half + rr[k], 0, a.h - 1);
+            rv[P][k] = __builtin_bit_cast(
+                rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, rr[k] < kBcRows ? r * a.in_pitch + cof[k] : 0x7ffffff0, 0, 0));
+        }
+    };
+    auto stage = [&](auto pc) {
+        constexpr int P = decltype(pc)::value;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k)
+            if (rr[k] < kBcRows) lds_wr128(stg_l + static_cast<uint32_t>(P * kBcRows * a.rsd) + lsl[k], rv[P][k] ^ 0x80808080u);
+    };
+    // COPY edge: staged pixels outside the window repeat its edge pixel
+    auto fixup = [&](auto pc) {
+        constexpr int P = decltype(pc)::value;
+        u8 *sb = stgb + P * kBcRows * a.rsd;
+        for (int i = tid; i < kBcRows * a.spx; i += kBcNT) {
+            const int l = i / a.spx, pq = i - l * a.spx, p = sx + pq;
+            if (p >= 0 && p < a.w) continue;
+            const int sp = clampi(p, 0, a.w - 1) - sx;
+#pragma unroll
+            for (int z = 0; z < B; ++z) sb[l * a.rsd + pq * B + z] = sb[l * a.rsd + sp * B + z];
+        }
+    };
+    // horizontal pass of step j: this wave's units, 16 staged rows -> ring rows 16 j + half + n
+    auto horizontal = [&](auto pc, int j) {
+        constexpr int P = decltype(pc)::value;
+        const uint32_t sr = stg_l + static_cast<uint32_t>(P * kBcRows * a.rsd + n * a.rsd + a.kb0 + 16 * kg);
+        const uint32_t rw = ring_l + static_cast<uint32_t>(((kBcRows * j + a.half + n) & a.rmask) * a.tw + 4 * kg);
+        rc_u2 q[UPW][NKS][2];
+#pragma unroll
+        for (int i = 0; i < UPW; ++i)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const uint32_t ad = sr + static_cast<uint32_t>(16 * (UPW * wave + i) + 64 * ks);
+                q[i][ks][0] = lds_rd2x32(ad);
+                q[i][ks][1] = lds_rd2x32(ad + 8);
+            }
+#pragma unroll
+        for (int i = 0; i < UPW; ++i)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) rc_pin(q[i][ks][0]), rc_pin(q[i][ks][1]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < UPW; ++i) {
+            rc_v4i acc = rc_v4i{a.seed, a.seed, a.seed, a.seed};
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                rc_pin(q[i][ks][0]);
+                rc_pin(q[i][ks][1]);
+                const rc_v4i bv = rc_v4i{static_cast<int>(q[i][ks][0].x), static_cast<int>(q[i][ks][0].y),
+                                         static_cast<int>(q[i][ks][1].x), static_cast<int>(q[i][ks][1].y)};
+                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[ks], bv, acc, 0, 0, 0);
+            }
+            lds_wr32(rw + static_cast<uint32_t>(16 * (UPW * wave + i)), bc_pack(acc, a.mag) ^ 0x80808080u);
+        }
+    };
+    // vertical pass of step j: ring rows 16 j - half + K, K = 16 kg + (0..7 | 8..15)
+    const uint32_t wst_l = wst_l0 + static_cast<uint32_t>(wave * kBcRows * WSR);
+    auto vertical_store = [&](int j, bool live) {
+        const int r1 = kBcRows * j - a.half + 16 * kg + (n >> 1);
+        const uint32_t a1 = ring_l + static_cast<uint32_t>((r1 & a.rmask) * a.tw + 8 * (n & 1));
+        const uint32_t a2 = ring_l + static_cast<uint32_t>(((r1 + 8) & a.rmask) * a.tw + 8 * (n & 1));
+        rc_v2i t1[UPW], t2[UPW];
+#pragma unroll
+        for (int i = 0; i < UPW; ++i) {
+            const uint32_t cb = static_cast<uint32_t>(16 * (UPW * wave + i));
+            t1[i] = lds_tr8(a1 + cb);
+            t2[i] = lds_tr8(a2 + cb);
+        }
+#pragma unroll
+        for (int i = 0; i < UPW; ++i) rc_pin(t1[i]), rc_pin(t2[i]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        uint32_t res[UPW];
+#pragma unroll
+        for (int i = 0; i < UPW; ++i) {
+            rc_pin(t1[i]);
+            rc_pin(t2[i]);
+            const rc_v4i av = rc_v4i{t1[i].x, t1[i].y, t2[i].x, t2[i].y};
+            res[i] = bc_pack(__builtin_amdgcn_mfma_i32_16x16x64_i8(av, tb, rc_v4i{a.seed, a.seed, a.seed, a.seed}, 0, 0, 0),
+                             a.mag);
+        }
+#pragma unroll
+        for (int i = 0; i < UPW; ++i) lds_wr32(wst_l + static_cast<uint32_t>(n * WSR + 16 * i + 4 * kg), res[i]);
+        rc_u4 qv[NPC];
+#pragma unroll
+        for (int r = 0; r < NPC; ++r) {  // piece lane + 64 r = (row, 16-byte chunk)
+            const int pc = min(lane + 64 * r, 16 * UPW - 1), wrow = pc / UPW, wch = pc - UPW * wrow;
+            qv[r] = lds_rd128(wst_l + static_cast<uint32_t>(wrow * WSR + 16 * wch));
+        }
+#pragma unroll
+        for (int r = 0; r < NPC; ++r) rc_pin(qv[r]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < NPC; ++r) {
+            rc_pin(qv[r]);
+            const int pc = lane + 64 * r, wrow = pc / UPW, wch = pc - UPW * wrow;
+            const int we = 16 * (UPW * wave + wch);  // the piece's first byte in the strip row
+            const int y = kBcRows * j + wrow;
+            const bool ok = live && pc < 16 * UPW && y < a.h;
+            const int base = (y * a.w + x0) * B + we;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, qv[r]), dst,
+                                                   ok && we + 16 <= vbytes ? base : 0x7ffffff0, 0, 0);
+            if (a.wst2) {  // rows whose byte count is not a multiple of 16: the piece at the window edge in dwords
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    __builtin_amdgcn_raw_buffer_store_b32(
+                        qv[r][k], dst, ok && we + 16 > vbytes && we + 4 * k < vbytes ? base + 4 * k : 0x7ffffff0, 0, 0);
+            }
+        }
+    };
+    // one step: stage rows of j (loaded two steps ago, set P) -> barrier [-> COPY fix-up ->
+    // barrier] -> loads of j + 2 -> horizontal(j) -> vertical(j) + stores (idle before ka).
+    // Two staging buffers: a wave writing step j + 1's rows has passed the barrier of step
+    // j, so every wave is done with step j - 1's buffer.
+    auto body = [&](auto pc, int j) {
+        stage(pc);
+        rc_barrier();
+        if (edge) {
+            fixup(pc);
+            rc_barrier();
+        }
+        issue(pc, j + 2);
+        horizontal(pc, j);
+        vertical_store(j, j >= ka);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    issue(I0{}, j0);
+    issue(I1{}, j0 + 1);
+    for (int j = j0; j < kz; j += 2) {
+        body(I0{}, j);
+        if (j + 1 < kz) body(I1{}, j + 1);
+    }
+}
+
+}  // namespace
+
+// The column-walking blur of the (left, top, ow x oh) window: RGB / RGBA, dword-aligned
+// rows, window start and output, masks of <= 33 non-negative taps below 128, scale below
+// 4096; MIPX_EUNSUPPORTED otherwise (the caller runs k_bmf / k_blur2d).
+int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, int top, int ow, int oh,
+                    const std::vector<int> &mask, int scale, hipStream_t st) {
+    const char *ec = tune_env("MIPX_BCOL");  // 0: k_bmf / k_blur2d (A/B)
+    if (ec && *ec == '0') return MIPX_EUNSUPPORTED;
+    const int taps = static_cast<int>(mask.size());
+    if ((b != 3 && b != 4) || taps < 1 || taps > 33 || (taps & 1) == 0 || scale <= 0 || scale >= 4096)
+        return MIPX_EUNSUPPORTED;
+    for (int m : mask)
+        if (m < 0 || m > 127) return MIPX_EUNSUPPORTED;
+    if ((w * b) % 4 || (left * b) % 4 || reinterpret_cast<uintptr_t>(in) % 4 || (ow * b) % 4 ||
+        reinterpret_cast<uintptr_t>(out) % 4)
+        return MIPX_EUNSUPPORTED;
+    BcArgs a{};
+    a.in = in;
+    a.out = out;
+    a.in_pitch = w * b;
+    a.in_base = (static_cast<long long>(top) * w + left) * b;
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = img_bytes(ow, oh, b);
+    if (a.in_img >= 0x7fffffffLL - 4096 || a.out_img >= 0x7fffffffLL - 4096) return MIPX_EUNSUPPORTED;
+    a.w = ow;
+    a.h = oh;
+    a.half = taps / 2;
+    // the staged origin B (x0 - sx0) sits on 16 bytes at the window's left edge, so no chunk
+    // straddles a row start (a load at a negative offset reads 0 whole)
+    const int al = b == 3 ? 16 : 4;
+    a.sx0 = (a.half + al - 1) / al * al;
+    const char *epx = tune_env("MIPX_BCOL_PX");  // output pixels per strip: 64 / 128 (A/B)
+    const int px = epx && *epx ? (std::atoi(epx) == 128 ? 128 : 64) : 64;
+    a.spx = px + a.sx0 + a.half;
+    const int e = b * (a.sx0 - a.half), delta = e & 3;
+    a.kb0 = e & ~3;
+    const int nks = (16 + delta + b * (taps - 1) + 63) / 64;
+    if (nks > 3) return MIPX_EUNSUPPORTED;
+    a.cpr = (b * a.spx + 15) / 16;
+    const int kmax = (kBcRows * a.cpr + kBcNT - 1) / kBcNT;
+    if (kmax > (px == 64 ? 3 : 5)) return MIPX_EUNSUPPORTED;
+    // staging stride: every horizontal read in the row (+ 4 units of slack), dwords = 4 mod 8
+    int rsd = std::max(16 * a.cpr, a.kb0 + px * b + 64 * nks) + 16;
+    rsd = (rsd + 15) & ~15;
+    while ((rsd / 4) % 8 != 4) rsd += 16;
+    a.rsd = rsd;
+    const int ring = kBcRows + taps - 1 <= 32 ? 32 : 64;
+    a.rmask = ring - 1;
+    int twd = (px * b) / 4;  // the transposed reads: (dwords mod 64) / 4 odd
+    twd = (twd + 3) & ~3;
+    while (((twd & 63) >> 2) % 2 == 0) twd += 4;
+    a.tw = 4 * twd;
+    a.pre = (2 * a.half + kBcRows - 1) / kBcRows;
+    a.mag = static_cast<uint32_t>(((1ULL << 32) + scale - 1) / scale);
+    a.seed = 128 * scale + (scale + 1) / 2;
+    a.wst2 = (ow * b) % 16 != 0;
+    a.ops = device_blur_ops(mask, b, delta, nks);
+    if (!a.ops) return MIPX_EDEVICE;
+    const size_t lds = static_cast<size_t>(2 * kBcRows) * rsd + static_cast<size_t>(ring) * a.tw +
+                       static_cast<size_t>(4 * kBcRows) * (16 * (b * px / 64) + ((b * px / 64) % 2 == 0 ? 16 : 0));
+    if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
+
+    const void *fn = nullptr;
+#define MIPX_BC_KP(B_, NKS_, PX_)                                                                    \
+    fn = kmax == 1   ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 1, PX_>)                     \
+         : kmax == 2 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 2, PX_>)                     \
+         : kmax == 3 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 3, PX_>)                     \
+         : kmax == 4 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 4, PX_>)                     \
+                     : reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 5, PX_>);
+#define MIPX_BC_K(B_, NKS_) \
+    if (px == 64) { MIPX_BC_KP(B_, NKS_, 64) } else { MIPX_BC_KP(B_, NKS_, 128) }
+    if (b == 3) {
+        if (nks == 1) { MIPX_BC_K(3, 1) } else if (nks == 2) { MIPX_BC_K(3, 2) } else { MIPX_BC_K(3, 3) }
+    } else {
+        if (nks == 1) { MIPX_BC_K(4, 1) } else if (nks == 2) { MIPX_BC_K(4, 2) } else { MIPX_BC_K(4, 3) }
+    }
+#undef MIPX_BC_K
+#undef MIPX_BC_KP
+
+    // segments: a segment's first pre steps only filter; pick the split that minimises
+    // (rounds of resident blocks) x (steps + pre)
+    a.strips = (ow + px - 1) / px;
+    a.ksteps = (oh + kBcRows - 1) / kBcRows;
+    const long long cols = static_cast<long long>(a.strips) * n;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBcNT, lds) != hipSuccess || per_cu < 1) per_cu = 2;
+    const long long slots = 256LL * per_cu;
+    int best_segs = 1;
+    double best = 1e300;
+    for (int segs = 1; segs <= a.ksteps; ++segs) {
+        const int ss = (a.ksteps + segs - 1) / segs;
+        if (segs > 1 && ss < 4) break;
+        const long long blocks = cols * ((a.ksteps + ss - 1) / ss);
+        const double cost = static_cast<double>((blocks + slots - 1) / slots) * (ss + a.pre);
+        if (cost < best - 1e-9) {
+            best = cost;
+            best_segs = segs;
+        }
+    }
+    a.seg_steps = (a.ksteps + best_segs - 1) / best_segs;
+    a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
+    const long long blocks = cols * a.segs;
+    if (!grid_ok(blocks)) return MIPX_EINVAL;
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(BcArgs)>(const_cast<void *>(fn)), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBcNT), lds, st, a);
+    return launch_check("k_bcol");
+}
+
+}  // namespace mipx

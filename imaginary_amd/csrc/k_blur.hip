@@ -666,6 +666,8 @@ int blur_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int le
     std::vector<int> mask;
     int scale = 0;
     if (gaussmat(sigma, min_ampl, mask, scale) < 0) return MIPX_EINVAL;
+    const int ec = blur_col_launch(in, out, n, w, h, b, left, top, ow, oh, mask, scale, st);
+    if (ec != MIPX_EUNSUPPORTED) return ec;
     const int em = blur_mfma_launch(in, out, n, w, h, b, left, top, ow, oh, mask, scale, st);
     if (em != MIPX_EUNSUPPORTED) return em;
     const int ef = blur2d_launch(in, out, n, w, h, b, left, top, ow, oh, mask, scale, st);

@@ -41,15 +41,13 @@
 #include <vector>
 
 #include "device_common.h"
+#include "lds_ops.h"
 
 namespace mipx {
 namespace {
 
 using namespace dev;
 
-typedef int rc_v4i __attribute__((ext_vector_type(4)));
-typedef int rc_v2i __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) void rc_lds_void;
 typedef const __attribute__((address_space(4))) int rc_cint;
 
 constexpr int kRcRows = 16;   // output rows per step (the MFMA N)
@@ -86,12 +84,6 @@ __device__ __forceinline__ void rc_pos(int o, double s, int pad, int *start, int
     *start = static_cast<int>(X) - pad;
     *phase = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
 }
-
-// Workgroup barrier for LDS data: this wave's LDS reads and writes complete, then
-// s_barrier; the "memory" clobber keeps the compiler from moving memory accesses across
-// it.  Not __syncthreads(): its workgroup release fence would drain vmcnt(0), i.e. wait
-// for the ring loads of the next two steps, which are in flight on purpose.
-__device__ __forceinline__ void rc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // 16 bytes of a kRsTabW stride-B tap row from byte o (any alignment)
 __device__ __forceinline__ rc_v4i rc_frag16(const signed char *row, int o) {
@@ -144,48 +136,6 @@ __device__ __forceinline__ void rc_edge_frag(const float *tabf, int taps, int pp
     }
     *fh = rc_v4i{static_cast<int>(hw[0]), static_cast<int>(hw[1]), static_cast<int>(hw[2]), static_cast<int>(hw[3])};
     *fl = rc_v4i{static_cast<int>(lw[0]), static_cast<int>(lw[1]), static_cast<int>(lw[2]), static_cast<int>(lw[3])};
-}
-
-// LDS accesses of the step loop as inline asm: the loop counts its own lgkmcnt waits
-// (two tiles in flight per wait) and the compiler's waits stay on the global loads.
-typedef uint32_t rc_u2 __attribute__((ext_vector_type(2)));
-typedef uint32_t rc_u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t rc_lds(const void *p) {
-    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((rc_lds_void *)(const_cast<void *>(p))));
-}
-__device__ __forceinline__ uint32_t lds_rd32(uint32_t a) {
-    uint32_t v;
-    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a));
-    return v;
-}
-__device__ __forceinline__ rc_u2 lds_rd64(uint32_t a) {
-    rc_u2 v;
-    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
-    return v;
-}
-__device__ __forceinline__ rc_u4 lds_rd128(uint32_t a) {
-    rc_u4 v;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
-    return v;
-}
-__device__ __forceinline__ rc_v2i lds_tr8(uint32_t a) {
-    rc_v2i v;
-    asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(v) : "v"(a));
-    return v;
-}
-__device__ __forceinline__ void lds_wr32(uint32_t a, uint32_t v) { asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory"); }
-__device__ __forceinline__ void lds_wr128(uint32_t a, rc_u4 v) { asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory"); }
-__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// The wait must also be a data dependence of the values it waits for: an asm read's
-// result is an ordinary register to the compiler, which could otherwise schedule its
-// first use between the read and a separate wait (no hardware interlock on LDS returns)
-template <typename T>
-__device__ __forceinline__ void rc_pin(T &v) { asm volatile("" : "+v"(v)); }
-template <int N, typename... T>
-__device__ __forceinline__ void lgkm_wait_for(T &...v) {
-    (rc_pin(v), ...);  // the values are live into the wait
-    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
-    (rc_pin(v), ...);  // every later use reads the copy made after the wait
 }
 
 // KMAX ring chunks per lane per step (16 bytes each), NKS horizontal K steps (64 bytes
@@ -432,30 +382,27 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
     // horizontal pass: units wave + WV i, operands from registers, every unit's LDS
     // reads in flight together
     auto horizontal = [&](uint32_t *res) {
-        rc_u2 q[UPW][NKS][2];
+        rc_u4 q[UPW][NKS];
 #pragma unroll
         for (int i = 0; i < UPW; ++i) {
             const uint32_t ir = inter_l + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg);
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                q[i][ks][0] = lds_rd64(ir + 64 * ks);
-                q[i][ks][1] = lds_rd64(ir + 64 * ks + 8);
+                q[i][ks] = lds_rd2x64(ir + 64 * ks);  // one 16-byte read: 4 lanes per bank quad, not 2 x (4 per pair)
             }
         }
 #pragma unroll
         for (int i = 0; i < UPW; ++i)
 #pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) rc_pin(q[i][ks][0]), rc_pin(q[i][ks][1]);
+            for (int ks = 0; ks < NKS; ++ks) rc_pin(q[i][ks]);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int i = 0; i < UPW; ++i) {
             rc_v4i ah = rc_v4i{0, 0, 0, 0}, al = hb[i];
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                rc_pin(q[i][ks][0]);
-                rc_pin(q[i][ks][1]);
-                const rc_v4i bz = rc_v4i{static_cast<int>(q[i][ks][0].x), static_cast<int>(q[i][ks][0].y),
-                                         static_cast<int>(q[i][ks][1].x), static_cast<int>(q[i][ks][1].y)};
+                rc_pin(q[i][ks]);
+                const rc_v4i bz = __builtin_bit_cast(rc_v4i, q[i][ks]);
                 ah = __builtin_amdgcn_mfma_i32_16x16x64_i8(th[i][ks], bz, ah, 0, 0, 0);
                 al = __builtin_amdgcn_mfma_i32_16x16x64_i8(tl[i][ks], bz, al, 0, 0, 0);
             }

@@ -945,7 +945,6 @@ __global__ void __launch_bounds__(256) k_hreduce(HPassArgs a) {
 // the i8 table (row ph, bytes from kHmTabPad + k - start), B = 16 staged bytes
 // of image row l & 15, so each lane ends with 4 consecutive output pixels of one
 // row per channel: 12 / 16 contiguous bytes to store.
-constexpr int kHmRows = 16;  // image rows per block (the MFMA N)
 typedef int hm_v4i __attribute__((ext_vector_type(4)));
 
 // The 16-byte fragment of an i8 tap row at window offset o (tap o + j in byte j,
@@ -969,7 +968,6 @@ __device__ __forceinline__ hm_v4i load_taps16(const signed char *row, int o) {
 // fused reduce on the matrix cores (k_rmf2): both passes on v_mfma_i32_16x16x64_i8
 // ===========================================================================
 constexpr int kRmRows = 16;
-constexpr int kRmXW = 128;
 constexpr int kRmMaxCt = 16;  // k_rmf2: 16-byte column tiles per wave (staged span <= 1024 bytes)
 
 struct RmArgs {

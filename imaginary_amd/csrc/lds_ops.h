@@ -1,0 +1,66 @@
+// lds_ops.h — LDS accesses as inline asm with explicit lgkmcnt waits, shared by the
+// column walkers (k_rcol.hip, k_bcol.hip): the loops count their own waits so that the
+// compiler's waits stay on the global loads that are in flight on purpose.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mipx {
+namespace dev {
+
+typedef int rc_v4i __attribute__((ext_vector_type(4)));
+typedef int rc_v2i __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void rc_lds_void;
+
+// Workgroup barrier for LDS data: this wave's LDS reads and writes complete, then
+// s_barrier; the "memory" clobber keeps the compiler from moving memory accesses across
+// it.  Not __syncthreads(): its workgroup release fence would drain vmcnt(0), i.e. wait
+// for the ring loads of the next two steps, which are in flight on purpose.
+__device__ __forceinline__ void rc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS accesses of the step loop as inline asm: the loop counts its own lgkmcnt waits
+// (two tiles in flight per wait) and the compiler's waits stay on the global loads.
+typedef uint32_t rc_u2 __attribute__((ext_vector_type(2)));
+typedef uint32_t rc_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t rc_lds(const void *p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((rc_lds_void *)(const_cast<void *>(p))));
+}
+__device__ __forceinline__ uint32_t lds_rd32(uint32_t a) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+// 16 bytes at an 8-byte-aligned address in one instruction (2 x 8 bytes, adjacent)
+__device__ __forceinline__ rc_u4 lds_rd2x64(uint32_t a) {
+    rc_u4 v;
+    asm volatile("ds_read2_b64 %0, %1 offset1:1" : "=v"(v) : "v"(a));
+    return v;
+}
+__device__ __forceinline__ rc_u4 lds_rd128(uint32_t a) {
+    rc_u4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+__device__ __forceinline__ rc_v2i lds_tr8(uint32_t a) {
+    rc_v2i v;
+    asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+__device__ __forceinline__ void lds_wr32(uint32_t a, uint32_t v) { asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory"); }
+__device__ __forceinline__ void lds_wr128(uint32_t a, rc_u4 v) { asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory"); }
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// The wait must also be a data dependence of the values it waits for: an asm read's
+// result is an ordinary register to the compiler, which could otherwise schedule its
+// first use between the read and a separate wait (no hardware interlock on LDS returns)
+template <typename T>
+__device__ __forceinline__ void rc_pin(T &v) { asm volatile("" : "+v"(v)); }
+template <int N, typename... T>
+__device__ __forceinline__ void lgkm_wait_for(T &...v) {
+    (rc_pin(v), ...);  // the values are live into the wait
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+    (rc_pin(v), ...);  // every later use reads the copy made after the wait
+}
+
+}  // namespace dev
+}  // namespace mipx

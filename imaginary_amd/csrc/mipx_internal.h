@@ -120,6 +120,9 @@ int reduce_fused_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, in
 // small-image fused kernel); MIPX_EUNSUPPORTED = run the two separable passes
 int reduce_one_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                       int oy0, int ow, int oh, hipStream_t st);
+// k_bcol.hip: the column-walking gaussblur (both convsep passes on the matrix cores)
+int blur_col_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int left, int top, int ow, int oh,
+                    const std::vector<int> &mask, int scale, hipStream_t st);
 // k_rcol.hip: the column walker (LDS row ring, both passes on the matrix cores)
 int reduce_col_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
                       int oy0, int ow, int oh, hipStream_t st);

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
@@ -93,6 +94,44 @@ __global__ void __launch_bounds__(256) strip(P a) {
     }
 }
 
+// k_bmf's access pattern, memory only: a block owns TW output pixels x TR output rows of
+// one image (same-size output: the blur), loads its TR + HALO input rows of
+// (TW + HALO) pixels with 16-byte loads (all issued, then used), stores its TR rows
+struct T {
+    const uint8_t *in;
+    uint8_t *out;
+    int w, h, tw, tr, halo, xb, yb;
+    long long img;
+};
+template <int KM>
+__global__ void __launch_bounds__(256) tile(T a) {
+    const int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+    const int xb = t % a.xb, rest = t / a.xb, yb = rest % a.yb, img = rest / a.yb;
+    const int tid = threadIdx.x, pitch = a.w * 3;
+    const int x0 = xb * a.tw, y0 = yb * a.tr;
+    const int b0 = max(0, (x0 - a.halo / 2) * 3) & ~15;
+    const int span = (a.tw + a.halo) * 3 + 16, cpr = (span + 15) / 16, L = a.tr + a.halo;
+    const __amdgpu_buffer_rsrc_t src =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.in + img * a.img), 0, static_cast<int>(a.img), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(a.out + img * a.img, 0, static_cast<int>(a.img), 0x00020000);
+    uint32_t acc = 0;
+    u4v v[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        const int c = tid + 256 * j, r = c / cpr, col = c - r * cpr;
+        const int row = min(max(y0 - a.halo / 2 + r, 0), a.h - 1);
+        v[j] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(src, r < L ? row * pitch + b0 + 16 * col : 0x7ffffff0, 0, 0));
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j) acc ^= v[j].x ^ v[j].w;
+    const int nq = a.tw * 3 / 16;
+    for (int i = tid; i < a.tr * nq; i += 256) {
+        const int r = i / nq, q = i - r * nq, y = y0 + r;
+        const int off = y < a.h && x0 * 3 + 16 * q + 16 <= pitch ? y * pitch + x0 * 3 + 16 * q : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, u4v{acc, acc + 1, acc + 2, acc + i}), dst, off, 0, 0);
+    }
+}
+
 template <class F>
 static float time_it(F launch) {
     hipEvent_t a, b;
@@ -119,7 +158,7 @@ int main() {
     const long long in_img = 1LL * W * H * 3, out_img = 1LL * OW * OH * 3;
     uint8_t *in, *out;
     CK(hipMalloc(&in, n * in_img + 4096));
-    CK(hipMalloc(&out, n * out_img + 4096));
+    CK(hipMalloc(&out, n * in_img + 4096));  // the tile pattern writes full-size images
     CK(hipMemset(in, 1, n * in_img));
     CK(hipDeviceSynchronize());
     const double bytes = static_cast<double>(n) * (in_img + out_img);
@@ -144,11 +183,34 @@ int main() {
                name, spx, 16 * cpr, ss, mode, blocks, ms, bytes / ms / 1e6);
         fflush(stdout);
     };
-    for (int spx : {64, 128, 256}) {
-        run("strip", spx, 11, 0);
-        run("strip_xcd", spx, 11, 1);
-        run("stores_only_xcd", spx, 11, 3);
-        run("loads_only_xcd", spx, 11, 5);
+    if (getenv("PROBE_STRIP")) {
+        for (int spx : {64, 128, 256}) {
+            run("strip", spx, 11, 0);
+            run("strip_xcd", spx, 11, 1);
+            run("stores_only_xcd", spx, 11, 3);
+            run("loads_only_xcd", spx, 11, 5);
+        }
+    }
+    // k_bmf tiles on 64 x 1080p RGB in = out (blur): 128 px x 16 / 32 / 48 rows, halo 0 / 12 / 16
+    {
+        const long long img = 1LL * W * H * 3;
+        const double tb = 2.0 * n * img;
+        for (int tr : {16, 32, 48})
+            for (int halo : {0, 12, 16}) {
+                T a{};
+                a.in = in, a.out = out, a.w = W, a.h = H, a.tw = 128, a.tr = tr, a.halo = halo, a.img = img;
+                a.xb = (W + 127) / 128, a.yb = (H + tr - 1) / tr;
+                const unsigned blocks = static_cast<unsigned>(a.xb) * a.yb * n;
+                const int cpr = ((128 + halo) * 3 + 16 + 15) / 16, km = ((tr + halo) * cpr + 255) / 256;
+                float ms = -1;
+                if (km <= 4) ms = time_it([&] { tile<4><<<blocks, 256>>>(a); });
+                else if (km <= 8) ms = time_it([&] { tile<8><<<blocks, 256>>>(a); });
+                else if (km <= 12) ms = time_it([&] { tile<12><<<blocks, 256>>>(a); });
+                else continue;
+                printf("{\"pattern\": \"bmf_tile\", \"tw\": 128, \"tr\": %d, \"halo\": %d, \"km\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n",
+                       tr, halo, km, ms, tb / ms / 1e6);
+                fflush(stdout);
+            }
     }
     return 0;
 }

@@ -305,7 +305,8 @@ def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma,
     mul-hi (default) and fp32 rounding (MIPX_BLUR2D_FROUND=1)."""
     monkeypatch.setenv("MIPX_BLUR2D_ROWS", rows)
     monkeypatch.setenv("MIPX_BLUR2D_FROUND", fround)
-    monkeypatch.setenv("MIPX_BMF", "0")  # k_blur2d, not the matrix-core kernel
+    monkeypatch.setenv("MIPX_BCOL", "0")
+    monkeypatch.setenv("MIPX_BMF", "0")  # k_blur2d, not the matrix-core kernels
     for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3), (9, 600, 4), (130, 513, 3),
                     (3, 5, 4), (70, 257, 2)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
@@ -325,6 +326,7 @@ def test_blur_mfma_matches_oracle(gpu, oracle, rng, monkeypatch, on, sigma):
     cases it leaves to k_blur2d (unaligned rows, 1-2 bands, > 33 taps).  "0" runs
     k_blur2d on the same cases; "1" uses 32-row blocks where the image has 32 rows,
     "1r" the 16-row blocks, "1t" 48-row blocks."""
+    monkeypatch.setenv("MIPX_BCOL", "0")  # k_bmf / k_blur2d (the column walker: tests/test_bcol_gpu.py)
     monkeypatch.setenv("MIPX_BMF", on[:1])
     monkeypatch.setenv("MIPX_BMF_RG", {"1r": "1", "1t": "3"}.get(on, ""))
     for h, w, b in ((64, 76, 3), (130, 516, 3), (9, 600, 4), (50, 260, 4), (3, 8, 4), (33, 20, 3), (17, 132, 3),
