@@ -288,8 +288,11 @@ def smartcrop_origins(imgs: np.ndarray, cw: int, ch: int) -> np.ndarray:
     return org.download((n, 2), np.int32)
 
 
-def execute(plan: MipxPlan, imgs: np.ndarray, wm: Optional[np.ndarray] = None) -> np.ndarray:
-    """mipx_execute_dev on a batch of host images (uploads, runs the plan, downloads)."""
+def execute(plan: MipxPlan, imgs: np.ndarray, wm: Optional[np.ndarray] = None,
+            junk: Optional[int] = None) -> np.ndarray:
+    """mipx_execute_dev on a batch of host images (uploads, runs the plan, downloads).
+    junk: fill the workspace (the ping-pong intermediates) and the output with this byte
+    first, so a step that reads outside what the steps before it wrote shows up."""
     sync_tuning()
     x = _batch(imgs)
     n = x.shape[0]
@@ -297,6 +300,10 @@ def execute(plan: MipxPlan, imgs: np.ndarray, wm: Optional[np.ndarray] = None) -
     dout = DeviceBuffer(n * plan.out_w * plan.out_h * plan.out_bands)
     wsb = lib.mipx_workspace_bytes(C.byref(plan), n)
     ws = DeviceBuffer(wsb) if wsb else None
+    if junk is not None:
+        check(lib.mipx_memset_dev(dout.ptr, junk, dout.nbytes), "mipx_memset_dev")
+        if ws:
+            check(lib.mipx_memset_dev(ws.ptr, junk, ws.nbytes), "mipx_memset_dev")
     dwm = DeviceBuffer.from_array(wm) if wm is not None else None
     check(lib.mipx_execute_dev(C.byref(plan), n, din.ptr, dout.ptr, dwm.ptr if dwm else None,
                                ws.ptr if ws else None, wsb, None), "mipx_execute_dev")

@@ -191,6 +191,23 @@ int main() {
             run("loads_only_xcd", spx, 11, 5);
         }
     }
+    // the strip walk in k_bcol's geometry: in = out (shrink 1), 64 / 128-pixel strips
+    if (getenv("PROBE_BLUR")) {
+        for (int spx : {64, 128}) {
+            const int span = spx * 3 + 24 * 3 + 16, cpr = (span + 15) / 16, km = (16 * cpr + 255) / 256;
+            P a{};
+            a.in = in, a.out = out, a.w = W, a.h = H, a.ow = W, a.oh = H, a.s = 1.0f, a.spx = spx;
+            a.strips = (W + spx - 1) / spx, a.ksteps = (H + 15) / 16, a.seg_steps = 17, a.segs = (a.ksteps + 16) / 17;
+            a.cpr = cpr, a.in_img = 1LL * W * H * 3, a.out_img = 1LL * W * H * 3;
+            const unsigned blocks = static_cast<unsigned>(a.strips) * a.segs * n;
+            float ms = -1;
+            if (km <= 3) ms = time_it([&] { strip<3, 1><<<blocks, 256>>>(a); });
+            else if (km <= 5) ms = time_it([&] { strip<5, 1><<<blocks, 256>>>(a); });
+            printf("{\"pattern\": \"blur_strip_xcd\", \"spx\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n", spx, ms,
+                   2.0 * n * a.in_img / ms / 1e6);
+            fflush(stdout);
+        }
+    }
     // k_bmf tiles on 64 x 1080p RGB in = out (blur): 128 px x 16 / 32 / 48 rows, halo 0 / 12 / 16
     {
         const long long img = 1LL * W * H * 3;

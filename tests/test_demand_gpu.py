@@ -30,9 +30,11 @@ def _ops(p):
 
 
 def _check(gpu, oracle, monkeypatch, px, plan, refs):
-    got = gpu.execute(plan, px)
+    # the demand-driven run over a workspace full of junk: a windowed step that
+    # read past what its producer computed would pick it up; the full run over another pattern
+    got = gpu.execute(plan, px, junk=0xA5)
     monkeypatch.setenv("MIPX_DEMAND", "0")
-    full = gpu.execute(plan, px)
+    full = gpu.execute(plan, px, junk=0x3C)
     monkeypatch.delenv("MIPX_DEMAND")
     for i in range(px.shape[0]):
         want = px[i]
@@ -113,3 +115,26 @@ def test_c3_chain_full_size(gpu, oracle, monkeypatch):
                         [dict(width=1024), dict(width=768, height=512, crop=1), dict(sigma=5.0, min_ampl=0.2)])
     assert _ops(plan) == [ia._abi.OP_REDUCE, ia._abi.OP_REDUCE, ia._abi.OP_EXTRACT, ia._abi.OP_BLUR]
     _check(gpu, oracle, monkeypatch, px, plan, refs)
+
+
+def test_demand_plan_through_request_path_twice(gpu, oracle):
+    """the request path reuses a plan's device buffers across batches, so a
+    windowed step reading outside its producer's region would see the previous input's
+    values.  The same demand-driven plan, two different inputs in a row, each against
+    the oracle."""
+    gpu.lib.mipx_shutdown()  # mipx_init refuses another configuration while one runs
+    eng = gpu.Engine(devices=[0], max_batch=1)
+    try:
+        plan, refs = _chain(oracle, 640, 480, 3, [dict(width=320), dict(width=200, height=100, crop=1, gravity=3)])
+        assert _ops(plan)[0] == ia._abi.OP_REDUCE
+        r = np.random.default_rng(77)
+        for k in range(2):
+            img = r.integers(0, 256, (480, 640, 3), dtype=np.uint8) if k == 0 else np.full((480, 640, 3), 200, np.uint8)
+            t, out = eng.submit(plan, img)
+            eng.wait(t)
+            want = img
+            for rp in refs:
+                want = oracle.execute(rp, want)
+            assert np.array_equal(out, want), f"request {k}"
+    finally:
+        eng.shutdown()
