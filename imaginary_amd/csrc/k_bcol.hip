@@ -26,7 +26,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <vector>
 
 #include "device_common.h"
@@ -39,6 +38,7 @@ using namespace dev;
 
 constexpr int kBcRows = 16;  // rows per step (the MFMA N)
 constexpr int kBcNT = 256;   // threads per block
+constexpr int kBcPX = 64;    // output pixels per strip
 
 struct BcArgs {
     const u8 *in;
@@ -78,13 +78,16 @@ __device__ __forceinline__ rc_u2 lds_rd2x32(uint32_t a) {
     return v;
 }
 
-// B: bands, NKS: horizontal K steps of 64 bytes, KMAX: staging chunks per lane per step,
-// PX: output pixels per strip (64 / 128)
-template <int B, int NKS, int KMAX, int PX>
+// B: bands, NKS: horizontal K steps of 64 bytes, KMAX: staging chunks per lane per step.
+// 64-pixel strips: 128-pixel ones (UPW 6 / 8, operands in chunks of half) measured 10-40 %
+// slower at 2-3 waves per SIMD (profiles/r03/bcol_px_chunk_ab.jsonl)
+template <int B, int NKS, int KMAX>
 __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
-    constexpr int UPW = B * PX / 64;  // 16-byte units per wave: PX B / 16 over the 4 waves
+    constexpr int PX = kBcPX;
+    constexpr int UPW = B;  // 16-byte units per wave: 64 B / 16 over the 4 waves
     constexpr int WSR = 16 * UPW + (UPW % 2 == 0 ? 16 : 0);  // dwords = 4 mod 8: the tile writes on distinct banks
     constexpr int NPC = (16 * UPW + 63) / 64;                  // 16-byte row pieces per lane
+    constexpr int UC = UPW;                                    // units per operand chunk
     extern __shared__ __attribute__((aligned(16))) uint32_t bcs[];
     const uint32_t stg_l = rc_lds(bcs);                                                  // [2][16][rsd]
     const uint32_t ring_l = stg_l + static_cast<uint32_t>(2 * kBcRows * a.rsd);          // [rmask + 1][tw]
@@ -160,32 +163,36 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
         constexpr int P = decltype(pc)::value;
         const uint32_t sr = stg_l + static_cast<uint32_t>(P * kBcRows * a.rsd + n * a.rsd + a.kb0 + 16 * kg);
         const uint32_t rw = ring_l + static_cast<uint32_t>(((kBcRows * j + a.half + n) & a.rmask) * a.tw + 4 * kg);
-        rc_u2 q[UPW][NKS][2];
+        // units in chunks of UC (128-pixel strips: half the operand registers live at once)
 #pragma unroll
-        for (int i = 0; i < UPW; ++i)
+        for (int c0 = 0; c0 < UPW; c0 += UC) {
+            rc_u2 q[UC][NKS][2];
 #pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                const uint32_t ad = sr + static_cast<uint32_t>(16 * (UPW * wave + i) + 64 * ks);
-                q[i][ks][0] = lds_rd2x32(ad);
-                q[i][ks][1] = lds_rd2x32(ad + 8);
+            for (int i = 0; i < UC; ++i)
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) {
+                    const uint32_t ad = sr + static_cast<uint32_t>(16 * (UPW * wave + c0 + i) + 64 * ks);
+                    q[i][ks][0] = lds_rd2x32(ad);
+                    q[i][ks][1] = lds_rd2x32(ad + 8);
+                }
+#pragma unroll
+            for (int i = 0; i < UC; ++i)
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) rc_pin(q[i][ks][0]), rc_pin(q[i][ks][1]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < UC; ++i) {
+                rc_v4i acc = rc_v4i{a.seed, a.seed, a.seed, a.seed};
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) {
+                    rc_pin(q[i][ks][0]);
+                    rc_pin(q[i][ks][1]);
+                    const rc_v4i bv = rc_v4i{static_cast<int>(q[i][ks][0].x), static_cast<int>(q[i][ks][0].y),
+                                             static_cast<int>(q[i][ks][1].x), static_cast<int>(q[i][ks][1].y)};
+                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[ks], bv, acc, 0, 0, 0);
+                }
+                lds_wr32(rw + static_cast<uint32_t>(16 * (UPW * wave + c0 + i)), bc_pack(acc, a.mag) ^ 0x80808080u);
             }
-#pragma unroll
-        for (int i = 0; i < UPW; ++i)
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) rc_pin(q[i][ks][0]), rc_pin(q[i][ks][1]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) {
-            rc_v4i acc = rc_v4i{a.seed, a.seed, a.seed, a.seed};
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                rc_pin(q[i][ks][0]);
-                rc_pin(q[i][ks][1]);
-                const rc_v4i bv = rc_v4i{static_cast<int>(q[i][ks][0].x), static_cast<int>(q[i][ks][0].y),
-                                         static_cast<int>(q[i][ks][1].x), static_cast<int>(q[i][ks][1].y)};
-                acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[ks], bv, acc, 0, 0, 0);
-            }
-            lds_wr32(rw + static_cast<uint32_t>(16 * (UPW * wave + i)), bc_pack(acc, a.mag) ^ 0x80808080u);
         }
     };
     // vertical pass of step j: ring rows 16 j - half + K, K = 16 kg + (0..7 | 8..15)
@@ -194,27 +201,28 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
         const int r1 = kBcRows * j - a.half + 16 * kg + (n >> 1);
         const uint32_t a1 = ring_l + static_cast<uint32_t>((r1 & a.rmask) * a.tw + 8 * (n & 1));
         const uint32_t a2 = ring_l + static_cast<uint32_t>(((r1 + 8) & a.rmask) * a.tw + 8 * (n & 1));
-        rc_v2i t1[UPW], t2[UPW];
 #pragma unroll
-        for (int i = 0; i < UPW; ++i) {
-            const uint32_t cb = static_cast<uint32_t>(16 * (UPW * wave + i));
-            t1[i] = lds_tr8(a1 + cb);
-            t2[i] = lds_tr8(a2 + cb);
+        for (int c0 = 0; c0 < UPW; c0 += UC) {
+            rc_v2i t1[UC], t2[UC];
+#pragma unroll
+            for (int i = 0; i < UC; ++i) {
+                const uint32_t cb = static_cast<uint32_t>(16 * (UPW * wave + c0 + i));
+                t1[i] = lds_tr8(a1 + cb);
+                t2[i] = lds_tr8(a2 + cb);
+            }
+#pragma unroll
+            for (int i = 0; i < UC; ++i) rc_pin(t1[i]), rc_pin(t2[i]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < UC; ++i) {
+                rc_pin(t1[i]);
+                rc_pin(t2[i]);
+                const rc_v4i av = rc_v4i{t1[i].x, t1[i].y, t2[i].x, t2[i].y};
+                lds_wr32(wst_l + static_cast<uint32_t>(n * WSR + 16 * (c0 + i) + 4 * kg),
+                         bc_pack(__builtin_amdgcn_mfma_i32_16x16x64_i8(av, tb, rc_v4i{a.seed, a.seed, a.seed, a.seed}, 0, 0, 0),
+                                 a.mag));
+            }
         }
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) rc_pin(t1[i]), rc_pin(t2[i]);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        uint32_t res[UPW];
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) {
-            rc_pin(t1[i]);
-            rc_pin(t2[i]);
-            const rc_v4i av = rc_v4i{t1[i].x, t1[i].y, t2[i].x, t2[i].y};
-            res[i] = bc_pack(__builtin_amdgcn_mfma_i32_16x16x64_i8(av, tb, rc_v4i{a.seed, a.seed, a.seed, a.seed}, 0, 0, 0),
-                             a.mag);
-        }
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) lds_wr32(wst_l + static_cast<uint32_t>(n * WSR + 16 * i + 4 * kg), res[i]);
         rc_u4 qv[NPC];
 #pragma unroll
         for (int r = 0; r < NPC; ++r) {  // piece lane + 64 r = (row, 16-byte chunk)
@@ -299,8 +307,7 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     // straddles a row start (a load at a negative offset reads 0 whole)
     const int al = b == 3 ? 16 : 4;
     a.sx0 = (a.half + al - 1) / al * al;
-    const char *epx = tune_env("MIPX_BCOL_PX");  // output pixels per strip: 64 / 128 (A/B)
-    const int px = epx && *epx ? (std::atoi(epx) == 128 ? 128 : 64) : 64;
+    const int px = kBcPX;
     a.spx = px + a.sx0 + a.half;
     const int e = b * (a.sx0 - a.half), delta = e & 3;
     a.kb0 = e & ~3;
@@ -308,7 +315,7 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     if (nks > 3) return MIPX_EUNSUPPORTED;
     a.cpr = (b * a.spx + 15) / 16;
     const int kmax = (kBcRows * a.cpr + kBcNT - 1) / kBcNT;
-    if (kmax > (px == 64 ? 3 : 5)) return MIPX_EUNSUPPORTED;
+    if (kmax > 3) return MIPX_EUNSUPPORTED;
     // staging stride: every horizontal read in the row (+ 4 units of slack), dwords = 4 mod 8
     int rsd = std::max(16 * a.cpr, a.kb0 + px * b + 64 * nks) + 16;
     rsd = (rsd + 15) & ~15;
@@ -331,21 +338,16 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
 
     const void *fn = nullptr;
-#define MIPX_BC_KP(B_, NKS_, PX_)                                                                    \
-    fn = kmax == 1   ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 1, PX_>)                     \
-         : kmax == 2 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 2, PX_>)                     \
-         : kmax == 3 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 3, PX_>)                     \
-         : kmax == 4 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 4, PX_>)                     \
-                     : reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 5, PX_>);
-#define MIPX_BC_K(B_, NKS_) \
-    if (px == 64) { MIPX_BC_KP(B_, NKS_, 64) } else { MIPX_BC_KP(B_, NKS_, 128) }
+#define MIPX_BC_K(B_, NKS_)                                                                        \
+    fn = kmax == 1   ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 1>)                        \
+         : kmax == 2 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 2>)                        \
+                     : reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 3>);
     if (b == 3) {
         if (nks == 1) { MIPX_BC_K(3, 1) } else if (nks == 2) { MIPX_BC_K(3, 2) } else { MIPX_BC_K(3, 3) }
     } else {
         if (nks == 1) { MIPX_BC_K(4, 1) } else if (nks == 2) { MIPX_BC_K(4, 2) } else { MIPX_BC_K(4, 3) }
     }
 #undef MIPX_BC_K
-#undef MIPX_BC_KP
 
     // segments: a segment's first pre steps only filter; pick the split that minimises
     // (rounds of resident blocks) x (steps + pre)

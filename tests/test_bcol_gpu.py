@@ -14,12 +14,10 @@ from test_parity_gpu import assert_same, rand_img, smooth_img
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["bcol", "bcol128", "nobcol"])
+@pytest.fixture(autouse=True, params=["bcol", "nobcol"])
 def route(request, monkeypatch):
-    """k_bcol with 64-pixel strips (default) and 128-pixel strips (MIPX_BCOL_PX=128),
-    and the kernels behind it (MIPX_BCOL=0)."""
-    monkeypatch.setenv("MIPX_BCOL", "0" if request.param == "nobcol" else "")
-    monkeypatch.setenv("MIPX_BCOL_PX", "128" if request.param == "bcol128" else "")
+    """k_bcol (the default) and the kernels behind it (MIPX_BCOL=0: k_bmf / k_blur2d)."""
+    monkeypatch.setenv("MIPX_BCOL", "" if request.param == "bcol" else "0")
     yield request.param
 
 
