@@ -141,16 +141,38 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
     const u8 *src = a.in + img * a.in_img;
     // ---- 1. stage the input window (extend mode at the borders) ----
     const bool interior = c0 >= 0 && c1 < a.w && r0 >= 0 && r1 < a.h;
-    if (interior) {  // dword gathers: two aligned loads + v_alignbyte per staged dword
+    if (interior) {  // r03: 16 bytes per lane (b128 + b32 loads, 4 v_alignbyte), all loads in flight
         int delta = 0;
         const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(src, a.in_img, &delta);
-        const int nd = (ncb + 3) >> 2;
-        for (int i = tid; i < nr * nd; i += 256) {
-            const int rr = i / nd, d = i - rr * nd;
-            const int off = delta + ((r0 + rr) * a.w + c0) * B + 4 * d;
-            const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, off & ~3, 0, 0);
-            const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, (off & ~3) + 4, 0, 0);
-            *reinterpret_cast<uint32_t *>(stg + rr * a.ncb + 4 * d) = __builtin_amdgcn_alignbyte(hi, lo, off & 3);
+        const int nq = (ncb + 15) >> 4;  // 16-byte items per staged row
+        for (int i0 = 0; i0 < nr * nq; i0 += 4 * 256) {
+            uint32_t v[4][4];
+            int slot[4], cnt[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + tid + 256 * k;
+                slot[k] = -1;
+                cnt[k] = 0;
+                if (i < nr * nq) {
+                    const int rr = i / nq, q = i - rr * nq;
+                    const int off = delta + ((r0 + rr) * a.w + c0) * B + 16 * q;
+                    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                    const u4v p = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, off & ~3, 0, 0));
+                    const uint32_t e = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, (off & ~3) + 16, 0, 0));
+                    const int sh = off & 3;
+                    v[k][0] = __builtin_amdgcn_alignbyte(p[1], p[0], sh);
+                    v[k][1] = __builtin_amdgcn_alignbyte(p[2], p[1], sh);
+                    v[k][2] = __builtin_amdgcn_alignbyte(p[3], p[2], sh);
+                    v[k][3] = __builtin_amdgcn_alignbyte(e, p[3], sh);
+                    slot[k] = rr * a.ncb + 16 * q;
+                    cnt[k] = min(4, (ncb - 16 * q + 3) >> 2);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    if (d < cnt[k]) *reinterpret_cast<uint32_t *>(stg + slot[k] + 4 * d) = v[k][d];
         }
     } else {
         for (int i = tid; i < nr * ncb; i += 256) {
@@ -239,31 +261,57 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
     }
 }
 
-// vips_zoom: 16 output bytes per lane, each the byte of the replicated pixel
+// vips_zoom: output row Y = source row Y / yf, output pixel x = source pixel x / xf.
+// r03: a block makes one 4 KiB chunk of the output rows of ONE source row: the source
+// bytes the chunk needs are staged in LDS with 16-byte loads (from the dword-aligned-
+// down start), each lane gathers its 16 output bytes from LDS, and the chunk is stored
+// to all yf output rows (the r02 kernel loaded every output byte from global memory,
+// once per output row: 15 % of HBM).
 template <int B>
-__global__ void __launch_bounds__(256) k_zoom(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int ow,
-                                              int xf, int yf, long long in_img, long long out_img) {
-    const int Y = blockIdx.y;
+__global__ void __launch_bounds__(256) k_zoom_rows(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int ow,
+                                                   int xf, int yf, float rxf, long long in_img, long long out_img) {
+    __shared__ __attribute__((aligned(16))) uint32_t seg[1024 + 8];
+    const int sy = blockIdx.y;
     const int img = blockIdx.z;
     const int row_out = ow * B;
-    const int j0 = (blockIdx.x * 256 + threadIdx.x) * 16;
-    if (j0 >= row_out) return;
-    const u8 *src = in + img * in_img + static_cast<long long>(Y / yf) * w * B;
-    u8 *q = out + img * out_img + static_cast<long long>(Y) * row_out + j0;
-    const int nb = min(16, row_out - j0);
+    const int j0 = blockIdx.x * 4096, j1 = min(j0 + 4096, row_out);
+    const int p0 = (j0 / B) / xf, p1 = ((j1 - 1) / B) / xf + 1;  // source pixels [p0, p1)
+    int delta = 0;
+    const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(in + img * in_img, in_img, &delta);
+    const int abs0 = delta + sy * w * B + p0 * B;
+    const int a4 = abs0 & ~3, skew = abs0 - a4;
+    const int nd = ((p1 - p0) * B + skew + 3) >> 2;  // <= 1026 (xf >= 1)
+    const int t = threadIdx.x;
+    if (4 * t < nd) {
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        const u4v v = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, a4 + 16 * t, 0, 0));
+        *reinterpret_cast<uint4 *>(seg + 4 * t) = uint4{v[0], v[1], v[2], v[3]};
+    }
+    if (t < nd - 1024) seg[1024 + t] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4096 + 4 * t, 0, 0));
+    __syncthreads();
+    const u8 *sb = reinterpret_cast<const u8 *>(seg) + skew;
+    const int jl = j0 + 16 * t;
+    if (jl >= j1) return;
+    const int nb = min(16, j1 - jl);
     uint32_t v[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         if (k < nb) {
-            const int jb = j0 + k;
+            const int jb = jl + k;
             const int px = jb / B, c = jb - px * B;
-            v[k >> 2] |= static_cast<uint32_t>(src[(px / xf) * B + c]) << (8 * (k & 3));
+            // px / xf: (px + 0.5) / xf is >= 0.5 / xf from an integer, far above the fp32 error
+            const int sp = static_cast<int>((static_cast<float>(px) + 0.5f) * rxf);
+            v[k >> 2] |= static_cast<uint32_t>(sb[(sp - p0) * B + c]) << (8 * (k & 3));
         }
     }
-    if (nb == 16 && (reinterpret_cast<uintptr_t>(q) & 15u) == 0) {
-        *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
-    } else {
-        for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
+    u8 *q = out + img * out_img + static_cast<long long>(sy) * yf * row_out + jl;
+    const bool wide = nb == 16 && (reinterpret_cast<uintptr_t>(q) & 15u) == 0 && (row_out & 15) == 0;
+    for (int r = 0; r < yf; ++r, q += row_out) {
+        if (wide) {
+            *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
+        } else {
+            for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
+        }
     }
 }
 
@@ -322,12 +370,14 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
 }
 
 int zoom_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int xf, int yf, hipStream_t st) {
-    const int ow = w * xf, oh = h * yf;
-    if (oh > 65535) return MIPX_EUNSUPPORTED;
-    const dim3 grid((ow * b + 4095) / 4096, oh, n);
-    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_zoom<B_>, grid, dim3(256), 0, st, in, out, w, ow, xf, yf,
-                                              img_bytes(w, h, b), img_bytes(ow, oh, b)));
-    return launch_check("k_zoom");
+    const int ow = w * xf;
+    if (h > 65535 || xf < 1 || yf < 1) return MIPX_EUNSUPPORTED;
+    if (img_bytes(w, h, b) >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
+    const dim3 grid((ow * b + 4095) / 4096, h, n);
+    const float rxf = 1.0f / static_cast<float>(xf);
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_zoom_rows<B_>, grid, dim3(256), 0, st, in, out, w, ow, xf, yf, rxf,
+                                              img_bytes(w, h, b), img_bytes(ow, h * yf, b)));
+    return launch_check("k_zoom_rows");
 }
 
 }  // namespace mipx

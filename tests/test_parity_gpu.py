@@ -551,6 +551,12 @@ def test_zoom_flatten_bw_match_oracle(gpu, oracle, rng, b):
         got = gpu.run_op("zoom", imgs, xfac=xf, yfac=yf)
         for i in range(2):
             assert_same(got[i], oracle.zoom(imgs[i], xf, yf), f"zoom {xf}x{yf}")
+    # r03 row-staged zoom: rows of several 4 KiB output chunks, unaligned output rows, tall factors
+    big = np.stack([rand_img(rng, 37, 1500, b), smooth_img(rng, 37, 1500, b)])
+    for xf, yf in ((2, 2), (3, 5), (7, 1), (1, 3)):
+        got = gpu.run_op("zoom", big, xfac=xf, yfac=yf)
+        for i in range(2):
+            assert_same(got[i], oracle.zoom(big[i], xf, yf), f"zoom {xf}x{yf} 37x1500x{b}")
     got = gpu.run_op("flatten", imgs, background=(200, 17, 90))
     for i in range(2):
         assert_same(got[i], oracle.flatten(imgs[i], (200, 17, 90)), "flatten")
