@@ -56,6 +56,7 @@ struct BcArgs {
     int rsd;            // staging row stride (bytes)
     int rmask, tw;      // ring rows - 1, ring row stride (bytes)
     int pre;            // filter-only steps before a segment's first output step
+    int kspan;          // horizontal K bytes the taps cover (16 + delta + B (taps - 1)): reads past it skipped
     uint32_t mag;       // floor(x / scale) == mulhi(x, mag) for the sums here
     int seed;           // 128 scale + (scale + 1) / 2
     int wst2;           // output rows not a multiple of 16 bytes: the edge piece as dwords
@@ -172,8 +173,13 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
 #pragma unroll
                 for (int ks = 0; ks < NKS; ++ks) {
                     const uint32_t ad = sr + static_cast<uint32_t>(16 * (UPW * wave + c0 + i) + 64 * ks);
-                    q[i][ks][0] = lds_rd2x32(ad);
-                    q[i][ks][1] = lds_rd2x32(ad + 8);
+                    if (64 * ks + 16 * kg < a.kspan) {  // lanes whose 16 K bytes lie past the taps read nothing
+                        q[i][ks][0] = lds_rd2x32(ad);
+                        q[i][ks][1] = lds_rd2x32(ad + 8);
+                    } else {
+                        q[i][ks][0] = rc_u2{0u, 0u};
+                        q[i][ks][1] = rc_u2{0u, 0u};
+                    }
                 }
 #pragma unroll
             for (int i = 0; i < UC; ++i)
@@ -311,7 +317,8 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     a.spx = px + a.sx0 + a.half;
     const int e = b * (a.sx0 - a.half), delta = e & 3;
     a.kb0 = e & ~3;
-    const int nks = (16 + delta + b * (taps - 1) + 63) / 64;
+    a.kspan = 16 + delta + b * (taps - 1);
+    const int nks = (a.kspan + 63) / 64;
     if (nks > 3) return MIPX_EUNSUPPORTED;
     a.cpr = (b * a.spx + 15) / 16;
     const int kmax = (kBcRows * a.cpr + kBcNT - 1) / kBcNT;
