@@ -334,11 +334,19 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
             const int base = o * a.ow * B + B * x0 + we;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, q), dst,
                                                    ok && we + 16 <= vbytes ? base : 0x7ffffff0, 0, 0);
-            if (a.wst > 1) {  // rows whose byte count is not a multiple of 16: the piece at the image edge in dwords
+            if (a.wst == 2) {  // rows whose byte count is not a multiple of 16: the piece at the image edge in dwords
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     __builtin_amdgcn_raw_buffer_store_b32(
                         q[j], dst, ok && we + 16 > vbytes && we + 4 * j < vbytes ? base + 4 * j : 0x7ffffff0, 0, 0);
+            } else if (a.wst == 3 && B * x0 + 16 * UPW * WV >= a.ow * B) {
+                // rows not on a dword (the b128 pieces above went out unaligned): the last strip's
+                // edge piece byte by byte
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(q[j >> 2] >> (8 * (j & 3))), dst,
+                                                         ok && we + 16 > vbytes && we + j < vbytes ? base + j : 0x7ffffff0,
+                                                         0, 0);
             }
             return;
         }
@@ -457,8 +465,11 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // out-of-range store offsets are built from 2^29 and 2^31 (k_rcol store)
     if (in_img >= 0x7fffffffLL || out_img >= (1LL << 29)) return MIPX_EUNSUPPORTED;
     if ((w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0) return MIPX_EUNSUPPORTED;
-    // output rows on a dword (else k_rmf2: byte stores here ran 1.2x slower there, r03)
-    if ((ow * b) % 4 != 0 || reinterpret_cast<uintptr_t>(out) % 4 != 0) return MIPX_EUNSUPPORTED;
+    // output rows off a dword go out as unaligned 16-byte pieces (wst 3); with the 4-byte
+    // stores (MIPX_RCOL_WST=0) they stay on k_rmf2
+    const bool out_al = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
+    const char *ews0 = tune_env("MIPX_RCOL_WST");
+    if (!out_al && ews0 && *ews0 == '0') return MIPX_EUNSUPPORTED;
     const int vtaps = reduce_points(vs), htaps = reduce_points(hs);
     if (vtaps > 16 || htaps > 16) return MIPX_EUNSUPPORTED;
     const bool centre = reduce_centre();
@@ -555,7 +566,7 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // r03: 16-byte row pieces through a wave tile (1080p RGB / 1.6 -16 %, 1024^2 RGBA / 1.333
     // -31 %, profiles/r03/rcol_wst_ab.jsonl); MIPX_RCOL_WST=0 keeps the 4-byte stores (A/B)
     const char *ews = tune_env("MIPX_RCOL_WST");
-    a.wst = !(ews && *ews == '0') ? ((ow * b) % 16 == 0 ? 1 : 2) : 0;
+    a.wst = !(ews && *ews == '0') ? (!out_al ? 3 : (ow * b) % 16 == 0 ? 1 : 2) : 0;
     const void *fn = nullptr;
 #define MIPX_RC_K(B_, NKS_, KM_) fn = reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_>);
 #define MIPX_RC_KM(B_, NKS_) \
