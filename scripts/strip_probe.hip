@@ -132,6 +132,61 @@ __global__ void __launch_bounds__(256) tile(T a) {
     }
 }
 
+// rot 90's access pattern, memory only: a block owns a tile of TC input columns x TH input
+// rows of one image (W x H x 3), loads its rows with 16-byte loads (LD 1: plus the b32 the
+// engine adds for the de-skew), stores TC output rows of TH pixels at the transposed place:
+// ST 0: 12 bytes per lane (the engine's 4-pixel tasks), ST 1: 16-byte pieces
+struct R {
+    const uint8_t *in;
+    uint8_t *out;
+    int w, h, tc, th, tx, ty, yfast;
+    long long img;
+};
+template <int KM, int LD, int ST>
+__global__ void __launch_bounds__(256) rot(R a) {
+    const int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+    int bx, by, img;
+    if (a.yfast) { by = t % a.ty; const int rest = t / a.ty; bx = rest % a.tx; img = rest / a.tx; }
+    else { bx = t % a.tx; const int rest = t / a.tx; by = rest % a.ty; img = rest / a.ty; }
+    const int tid = threadIdx.x, pitch = a.w * 3;
+    const int tx0 = bx * a.tc, ty0 = by * a.th;
+    const int tw = min(a.tc, a.w - tx0), th = min(a.th, a.h - ty0);
+    const __amdgpu_buffer_rsrc_t src =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.in + img * a.img), 0, static_cast<int>(a.img), 0x00020000);
+    const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(a.out + img * a.img, 0, static_cast<int>(a.img), 0x00020000);
+    const int nq = (tw * 3 + 15) / 16;
+    uint32_t acc = 0;
+    u4v v[KM];
+    uint32_t e[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        const int c = tid + 256 * j, r = c / nq, q = c - r * nq;
+        const int off = r < th ? (ty0 + r) * pitch + ((tx0 * 3) & ~3) + 16 * q : 0x7ffffff0;
+        v[j] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(src, off, 0, 0));
+        e[j] = LD ? static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, off + 16, 0, 0)) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j) acc ^= v[j].x ^ v[j].w ^ e[j];
+    __syncthreads();
+    const int ox = a.h - (ty0 + th);  // CW
+    if (ST == 0) {
+        const int quads = (th + 3) / 4;
+        for (int i = tid; i < tw * quads; i += 256) {
+            const int orr = i / quads, q = i - orr * quads;
+            const int off = ((tx0 + orr) * a.h + ox + 4 * q) * 3;
+            typedef uint32_t u3v __attribute__((ext_vector_type(3)));
+            __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u3v, u3v{acc, acc + 1, acc + i}), dst, off, 0, 0);
+        }
+    } else {
+        const int np = (th * 3 + 15) / 16;
+        for (int i = tid; i < tw * np; i += 256) {
+            const int orr = i / np, q = i - orr * np;
+            const int off = ((tx0 + orr) * a.h + ox) * 3 + 16 * q;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, u4v{acc, acc + 1, acc + 2, acc + i}), dst, off, 0, 0);
+        }
+    }
+}
+
 template <class F>
 static float time_it(F launch) {
     hipEvent_t a, b;
@@ -157,9 +212,10 @@ int main() {
     const float s = 1.6f;
     const long long in_img = 1LL * W * H * 3, out_img = 1LL * OW * OH * 3;
     uint8_t *in, *out;
-    CK(hipMalloc(&in, n * in_img + 4096));
-    CK(hipMalloc(&out, n * in_img + 4096));  // the tile pattern writes full-size images
-    CK(hipMemset(in, 1, n * in_img));
+    const long long cap = std::max(n * in_img, 32LL * 3840 * 2160 * 3);  // the rot probe's 32 x 4K RGB
+    CK(hipMalloc(&in, cap + 4096));
+    CK(hipMalloc(&out, cap + 4096));  // the tile pattern writes full-size images
+    CK(hipMemset(in, 1, cap));
     CK(hipDeviceSynchronize());
     const double bytes = static_cast<double>(n) * (in_img + out_img);
     const int ksteps = (OH + 15) / 16;
@@ -207,6 +263,37 @@ int main() {
                    2.0 * n * a.in_img / ms / 1e6);
             fflush(stdout);
         }
+    }
+    // rot 90 tiles on 32 x 4K RGB (the op survey's shape) and 16 x 12 MP RGB
+    if (getenv("PROBE_ROT")) {
+        for (int shape = 0; shape < 2; ++shape) {
+            const int RW = shape ? 4000 : 3840, RH = shape ? 3000 : 2160, rn = shape ? 16 : 32;
+            const long long img = 1LL * RW * RH * 3;
+            if (rn * img > cap) continue;
+            const double tb = 2.0 * rn * img;
+            for (int tc : {64, 128})
+                for (int thh : {32, 64, 128})
+                    for (int yf = 0; yf < 2; ++yf)
+                        for (int v = 0; v < 4; ++v) {
+                            R a{};
+                            a.in = in, a.out = out, a.w = RW, a.h = RH, a.tc = tc, a.th = thh, a.img = img, a.yfast = yf;
+                            a.tx = (RW + tc - 1) / tc, a.ty = (RH + thh - 1) / thh;
+                            const unsigned blocks = static_cast<unsigned>(a.tx) * a.ty * rn;
+                            const int km = (thh * ((tc * 3 + 15) / 16) + 255) / 256;
+                            float ms = -1;
+#define ROT_RUN(KM_) \
+                            if (v == 0) ms = time_it([&] { rot<KM_, 0, 0><<<blocks, 256>>>(a); }); \
+                            else if (v == 1) ms = time_it([&] { rot<KM_, 1, 0><<<blocks, 256>>>(a); }); \
+                            else if (v == 2) ms = time_it([&] { rot<KM_, 0, 1><<<blocks, 256>>>(a); }); \
+                            else ms = time_it([&] { rot<KM_, 1, 1><<<blocks, 256>>>(a); });
+                            if (km <= 2) { ROT_RUN(2) } else if (km <= 3) { ROT_RUN(3) } else if (km <= 6) { ROT_RUN(6) } else if (km <= 12) { ROT_RUN(12) } else continue;
+#undef ROT_RUN
+                            printf("{\"pattern\": \"rot90\", \"w\": %d, \"h\": %d, \"n\": %d, \"tc\": %d, \"th\": %d, \"yfast\": %d, \"ld_b32\": %d, \"st16\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n",
+                                   RW, RH, rn, tc, thh, yf, v & 1, v >> 1, ms, tb / ms / 1e6);
+                            fflush(stdout);
+                        }
+        }
+        return 0;
     }
     // k_bmf tiles on 64 x 1080p RGB in = out (blur): 128 px x 16 / 32 / 48 rows, halo 0 / 12 / 16
     {

@@ -219,6 +219,26 @@ def test_rot90_tile_orders(gpu, oracle, rng, monkeypatch, xcd, th, tc, order):
                 assert_same(got[i], oracle.rot(imgs[i], a), f"rot{a} {h}x{w}x{b} img{i} xcd={xcd}")
 
 
+@pytest.mark.parametrize("pxh,order", [("32", "1"), ("64", "1"), ("128", "1"), ("128", "0"), ("off", "1")])
+def test_rot90_rgb_pixel_tiles(gpu, oracle, rng, monkeypatch, pxh, order):
+    """k_rot90_px (3-band 90 / 270 through the pixel-major LDS tile): 32 / 64 / 128 input
+    rows per tile (MIPX_ROT_PXH), tiles y- or x-fastest; images whose rows are not on a
+    dword (b128 + de-skew staging) and batches of odd-size images (unaligned image bases),
+    ragged edge tiles with row counts that are not a multiple of 4, images of one row or
+    column.  "off": the same cases through k_rot90_lds (MIPX_ROT_PX=0)."""
+    if pxh == "off":
+        monkeypatch.setenv("MIPX_ROT_PX", "0")
+    else:
+        monkeypatch.setenv("MIPX_ROT_PXH", pxh)
+    monkeypatch.setenv("MIPX_ROT_ORDER", order)
+    for h, w in ((130, 197), (128, 160), (96, 64), (1, 77), (77, 1), (3, 5), (257, 63), (66, 129), (200, 300)):
+        imgs = np.stack([rand_img(rng, h, w, 3) for _ in range(3)])
+        for a in (90, 270):
+            got = gpu.run_op("rot", imgs, angle=a)
+            for i in range(3):
+                assert_same(got[i], oracle.rot(imgs[i], a), f"rot{a} {h}x{w}x3 img{i} pxh={pxh} order={order}")
+
+
 @pytest.mark.parametrize("x4", ["1", "0"])
 def test_shrink_x4_and_dword_kernels(gpu, oracle, rng, monkeypatch, x4):
     """Box shrink: the 16-byte-per-lane kernel (dword-aligned rows, vs <= 257) and
