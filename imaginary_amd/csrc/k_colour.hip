@@ -59,8 +59,7 @@ __global__ void __launch_bounds__(256) k_bw(const u8 *__restrict__ in, u8 *__res
 int flatten_launch(const u8 *in, u8 *out, int n, int w, int h, int b, const int *bg, hipStream_t st) {
     const long long npx = static_cast<long long>(n) * w * h;
     if (b != 2 && b != 4) {  // no alpha band: vips_flatten is a copy
-        MIPX_HIP(hipMemcpyAsync(out, in, static_cast<size_t>(npx) * b, hipMemcpyDeviceToDevice, st));
-        return MIPX_OK;
+        return device_copy(out, in, static_cast<size_t>(npx) * b, st);
     }
     const int c0 = clampi_host(bg[0]), c1 = clampi_host(bg[1]), c2 = clampi_host(bg[2]);
     const dim3 grid(static_cast<unsigned>((npx + 255) / 256));
@@ -72,8 +71,7 @@ int flatten_launch(const u8 *in, u8 *out, int n, int w, int h, int b, const int 
 int bw_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_t st) {
     const long long npx = static_cast<long long>(n) * w * h;
     if (b < 3) {  // 1-2 bands are already B_W
-        MIPX_HIP(hipMemcpyAsync(out, in, static_cast<size_t>(npx) * b, hipMemcpyDeviceToDevice, st));
-        return MIPX_OK;
+        return device_copy(out, in, static_cast<size_t>(npx) * b, st);
     }
     const float *t = device_colour_tables();
     if (!t) return MIPX_EDEVICE;

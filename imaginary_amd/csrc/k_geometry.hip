@@ -555,6 +555,27 @@ int remap_launch(int kind, const RemapArgs &a, int b, int n, hipStream_t st) {
 
 bool aligned4(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
 
+// Device-to-device copy of a whole batch (a plan with no steps, flatten of an image without
+// alpha, a 1.0 reduce, B_W of 1-2 bands): 4 x 16 bytes per lane in flight, consecutive
+// lanes on consecutive 16-byte chunks; the bytes past the last whole chunk by block 0.
+typedef uint32_t cp_u4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ void __launch_bounds__(256) k_copy16(const cp_u4 *__restrict__ in, cp_u4 *__restrict__ out, long long n16,
+                                                const u8 *__restrict__ tin, u8 *__restrict__ tout, int tail) {
+    const long long i0 = static_cast<long long>(blockIdx.x) * 1024 + threadIdx.x;
+    cp_u4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (i0 + 256 * k < n16) v[k] = NT ? __builtin_nontemporal_load(in + i0 + 256 * k) : in[i0 + 256 * k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (i0 + 256 * k >= n16) continue;
+        if (NT) __builtin_nontemporal_store(v[k], out + i0 + 256 * k);
+        else out[i0 + 256 * k] = v[k];
+    }
+    if (blockIdx.x == 0 && static_cast<int>(threadIdx.x) < tail) tout[threadIdx.x] = tin[threadIdx.x];
+}
+
 }  // namespace
 
 int embed_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x, int y, int ow, int oh, int extend,
@@ -633,8 +654,7 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
     angle = ((angle % 360) + 360) % 360;
     if (b == 4 && !(aligned4(in) && aligned4(out))) return MIPX_EINVAL;
     if (angle == 0) {
-        MIPX_HIP(hipMemcpyAsync(out, in, static_cast<size_t>(img_bytes(w, h, b)) * n, hipMemcpyDeviceToDevice, st));
-        return MIPX_OK;
+        return device_copy(out, in, static_cast<size_t>(img_bytes(w, h, b)) * n, st);
     }
     if (angle == 180 && img_bytes(w, h, b) < 0x7fffffffLL && h <= 65535)
         return flip_rows_launch(in, out, n, w, h, b, true, true, st);
@@ -719,6 +739,32 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
         MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_rot90t<B_, false>), grid, dim3(256), 0, st, in, out, w, h, ib));
     }
     return launch_check("k_rot90t");
+}
+
+int device_copy(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    const char *ec = tune_env("MIPX_COPY");  // 0: hipMemcpyAsync (A/B)
+    if (bytes == 0) return MIPX_OK;
+    // A/B (profiles/r03/copy_ab.jsonl): k_copy16 with non-temporal loads and stores moves 4K /
+    // 1080p / 12 MP RGB batches at 6.2-6.3 TB/s against 5.2-5.3 for hipMemcpyAsync (5.6-5.7 with
+    // plain stores); a 16 MB batch, which the caches hold, copies faster through hipMemcpyAsync
+    const bool small = bytes < (64u << 20) && !(ec && *ec);
+    if (small || (ec && *ec == '0') || ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15u) ||
+        bytes / 16 / 1024 >= 0x7fffffffULL) {
+        MIPX_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+        return MIPX_OK;
+    }
+    const long long n16 = static_cast<long long>(bytes / 16);
+    const int tail = static_cast<int>(bytes % 16);
+    const dim3 grid(static_cast<unsigned>(std::max(1LL, (n16 + 1023) / 1024)));
+    const u8 *tin = static_cast<const u8 *>(src) + 16 * n16;
+    u8 *tout = static_cast<u8 *>(dst) + 16 * n16;
+    if (ec && *ec == '2')  // plain (temporal) loads and stores (A/B)
+        hipLaunchKernelGGL(k_copy16<false>, grid, dim3(256), 0, st, static_cast<const cp_u4 *>(src), static_cast<cp_u4 *>(dst),
+                           n16, tin, tout, tail);
+    else
+        hipLaunchKernelGGL(k_copy16<true>, grid, dim3(256), 0, st, static_cast<const cp_u4 *>(src), static_cast<cp_u4 *>(dst),
+                           n16, tin, tout, tail);
+    return launch_check("k_copy16");
 }
 
 int extract_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, int top, int ow, int oh,

@@ -150,6 +150,7 @@ int embed_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, in
                  int extend, const int *bg, const int *d_origins, hipStream_t st);
 int flip_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int vertical, hipStream_t st);
 int rot_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int angle, hipStream_t st);
+int device_copy(void *dst, const void *src, size_t bytes, hipStream_t st);  // a batch, device to device
 int extract_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int left, int top, int ow, int oh,
                    hipStream_t st);
 // k_blur.hip (ws: n * w * h * b bytes for the uchar intermediate)

@@ -39,9 +39,7 @@ int mipx_op_reducev(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, i
                     double vshrink, void *stream) {
     if (!d_in || !d_out || !geom_ok(n, w, h, bands) || !(vshrink >= 1.0)) return MIPX_EINVAL;
     if (vshrink == 1.0) {
-        MIPX_HIP(hipMemcpyAsync(d_out, d_in, static_cast<size_t>(n) * w * h * bands, hipMemcpyDeviceToDevice,
-                                as_stream(stream)));
-        return MIPX_OK;
+        return device_copy(d_out, d_in, static_cast<size_t>(n) * w * h * bands, as_stream(stream));
     }
     return reducev_launch(d_in, d_out, n, w, h, bands, vshrink, as_stream(stream));
 }
@@ -50,9 +48,7 @@ int mipx_op_reduceh(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, i
                     double hshrink, void *stream) {
     if (!d_in || !d_out || !geom_ok(n, w, h, bands) || !(hshrink >= 1.0)) return MIPX_EINVAL;
     if (hshrink == 1.0) {
-        MIPX_HIP(hipMemcpyAsync(d_out, d_in, static_cast<size_t>(n) * w * h * bands, hipMemcpyDeviceToDevice,
-                                as_stream(stream)));
-        return MIPX_OK;
+        return device_copy(d_out, d_in, static_cast<size_t>(n) * w * h * bands, as_stream(stream));
     }
     return reduceh_launch(d_in, d_out, n, w, h, bands, hshrink, as_stream(stream));
 }

@@ -239,6 +239,19 @@ def test_rot90_rgb_pixel_tiles(gpu, oracle, rng, monkeypatch, pxh, order):
                 assert_same(got[i], oracle.rot(imgs[i], a), f"rot{a} {h}x{w}x3 img{i} pxh={pxh} order={order}")
 
 
+@pytest.mark.parametrize("route", ["1", "2", "0"])
+def test_batch_device_copy(gpu, rng, monkeypatch, route):
+    """The batch copy behind rot 0, flatten without alpha, a 1.0 reduce and B_W of 1-2
+    bands (k_copy16, non-temporal or plain; MIPX_COPY=0: hipMemcpyAsync): byte counts
+    below one chunk, not a multiple of 16, and past one 16 KB block."""
+    monkeypatch.setenv("MIPX_COPY", route)
+    for h, w, b, n in ((1, 1, 1, 1), (1, 5, 3, 1), (3, 7, 3, 2), (37, 53, 3, 3), (64, 64, 4, 2), (333, 251, 3, 5)):
+        imgs = rng.integers(0, 256, (n, h, w, b), dtype=np.uint8)
+        assert np.array_equal(gpu.run_op("rot", imgs, angle=0), imgs), f"rot 0 {n}x{h}x{w}x{b}"
+        if b == 3:
+            assert np.array_equal(gpu.run_op("flatten", imgs, background=(1, 2, 3)), imgs), f"flatten {h}x{w}"
+
+
 @pytest.mark.parametrize("x4", ["1", "0"])
 def test_shrink_x4_and_dword_kernels(gpu, oracle, rng, monkeypatch, x4):
     """Box shrink: the 16-byte-per-lane kernel (dword-aligned rows, vs <= 257) and
