@@ -122,8 +122,7 @@ __device__ __forceinline__ int extend_index(int v, int n, int ext) {  // -1 = fi
 template <int B>
 // fw: the fill bytes packed (byte c = fill[c]), so no per-lane index into the argument
 // struct forces it into scratch memory
-__device__ __forceinline__ void embed_chunk(const RemapArgs &a, uint32_t fw, int img, int Y, int j0) {
-    const int row_out = a.ow * B;
+__device__ __forceinline__ void embed_fetch(const RemapArgs &a, uint32_t fw, int img, int Y, int j0, uint32_t v[4]) {
     int ox = a.x, oy = a.y;
     if (a.origins) {
         ox = -a.origins[2 * img];
@@ -132,8 +131,6 @@ __device__ __forceinline__ void embed_chunk(const RemapArgs &a, uint32_t fw, int
     const int sy = extend_index(Y - oy, a.h, a.extend);
     const u8 *src = a.in + img * a.in_img;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc(src, a.in_img);
-    const int nb = min(16, row_out - j0);
-    uint32_t v[4];
     if (sy < 0) {  // fill row: the pattern, phase j mod B
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -171,15 +168,30 @@ __device__ __forceinline__ void embed_chunk(const RemapArgs &a, uint32_t fw, int
             v[d] = w;
         }
     }
+}
+
+template <int B, bool NT>
+__device__ __forceinline__ void embed_put(const RemapArgs &a, int img, int Y, int j0, const uint32_t v[4]) {
+    const int row_out = a.ow * B;
+    const int nb = min(16, row_out - j0);
     u8 *q = a.out + img * a.out_img + static_cast<long long>(Y) * row_out + j0;
     if (nb == 16 && ((reinterpret_cast<uintptr_t>(q) & 15u) == 0)) {
-        *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        if (NT) __builtin_nontemporal_store(u4v{v[0], v[1], v[2], v[3]}, reinterpret_cast<u4v *>(q));
+        else *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
     } else if (nb == 16 && ((reinterpret_cast<uintptr_t>(q) & 3u) == 0)) {
         uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
         q32[0] = v[0], q32[1] = v[1], q32[2] = v[2], q32[3] = v[3];
     } else {
         for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
     }
+}
+
+template <int B>
+__device__ __forceinline__ void embed_chunk(const RemapArgs &a, uint32_t fw, int img, int Y, int j0) {
+    uint32_t v[4];
+    embed_fetch<B>(a, fw, img, Y, j0, v);
+    embed_put<B, false>(a, img, Y, j0, v);
 }
 
 // a block: 4 KiB of a.rpb consecutive output rows (r02: 4 rows per block, so a
@@ -194,11 +206,29 @@ __global__ void __launch_bounds__(256) k_embed_rows(RemapArgs a) {
     for (int Y = y0; Y < y1; ++Y) embed_chunk<B>(a, fw, img, Y, j0);
 }
 
+// r03: the same blocks with every row's 16 bytes fetched before any is stored (RPB loads in
+// flight per lane instead of one), optionally non-temporal stores
+template <int B, int RPB, bool NT>
+__global__ void __launch_bounds__(256) k_embed_rows2(RemapArgs a) {
+    const int img = blockIdx.z;
+    const int j0 = (blockIdx.x * 256 + threadIdx.x) * 16;
+    if (j0 >= a.ow * B) return;
+    const uint32_t fw = a.fill[0] | (a.fill[1] << 8) | (a.fill[2] << 16) | (static_cast<uint32_t>(a.fill[3]) << 24);
+    const int y0 = blockIdx.y * RPB;
+    uint32_t v[RPB][4];
+#pragma unroll
+    for (int k = 0; k < RPB; ++k)
+        if (y0 + k < a.oh) embed_fetch<B>(a, fw, img, y0 + k, j0, v[k]);
+#pragma unroll
+    for (int k = 0; k < RPB; ++k)
+        if (y0 + k < a.oh) embed_put<B, NT>(a, img, y0 + k, j0, v[k]);
+}
+
 // flip H / flip V / rot 180 as row remaps: output row Y = source row sy
 // (Y or h-1-Y), pixels mirrored for H / 180.  A block stages the source bytes
 // of its 4 KiB output segment in LDS with dword loads (aligned-down start),
 // then each lane gathers its 16 output bytes from LDS and stores them at once.
-template <int B, bool MIRROR>
+template <int B, bool MIRROR, bool NT>
 __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
                                                    int vflip, long long img_bytes_, int rpb) {
     __shared__ __attribute__((aligned(16))) uint32_t seg[1024 + 8];
@@ -247,7 +277,9 @@ __global__ void __launch_bounds__(256) k_flip_rows(const u8 *__restrict__ in, u8
     }
     u8 *q = out + img * img_bytes_ + static_cast<long long>(Y) * row_bytes + jl;
     if (nb == 16 && (reinterpret_cast<uintptr_t>(q) & 15u) == 0) {
-        *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        if (NT) __builtin_nontemporal_store(u4v{v[0], v[1], v[2], v[3]}, reinterpret_cast<u4v *>(q));
+        else *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
     } else {
         for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
     }
@@ -610,7 +642,17 @@ int embed_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x, int y
     if (aligned4(in) && (a.in_img % 4) == 0 && a.in_img < 0x7fffffffLL && oh <= 65535) {
         const char *er = tune_env("MIPX_EMBED_RPB");
         a.rpb = (er && *er) ? std::max(1, std::atoi(er)) : 4;
+        const char *ev = tune_env("MIPX_EMBED_V");  // 0: k_embed_rows; 1: fetch-all; 2: + nt stores (A/B)
+        const int ver = ev && *ev ? *ev - '0' : 2;
         const dim3 grid((ow * b + 4095) / 4096, (oh + a.rpb - 1) / a.rpb, n);
+        if (ver >= 1 && a.rpb == 4) {
+            if (ver == 2) {
+                MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_embed_rows2<B_, 4, true>), grid, dim3(256), 0, st, a));
+            } else {
+                MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_embed_rows2<B_, 4, false>), grid, dim3(256), 0, st, a));
+            }
+            return launch_check("k_embed_rows2");
+        }
         MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_embed_rows<B_>, grid, dim3(256), 0, st, a));
         return launch_check("k_embed_rows");
     }
@@ -624,13 +666,17 @@ int flip_rows_launch(const u8 *in, u8 *out, int n, int w, int h, int b, bool mir
     const char *er = tune_env("MIPX_FLIP_RPB");
     const int rpb = (er && *er) ? std::max(1, std::atoi(er)) : 4;
     const dim3 grid((w * b + 4095) / 4096, (h + rpb - 1) / rpb, n);
+    const char *en = tune_env("MIPX_FLIP_NT");  // 1: non-temporal stores (A/B)
+    const bool nt = en && *en ? *en == '1' : true;
+#define MIPX_FLIP(M_, NT_)                                                                                        \
+    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_flip_rows<B_, M_, NT_>), grid, dim3(256), 0, st, in, out, w, h, \
+                                              vflip ? 1 : 0, ib, rpb))
     if (mirror) {
-        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_flip_rows<B_, true>), grid, dim3(256), 0, st, in, out, w, h,
-                                                  vflip ? 1 : 0, ib, rpb));
+        if (nt) { MIPX_FLIP(true, true); } else { MIPX_FLIP(true, false); }
     } else {
-        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_flip_rows<B_, false>), grid, dim3(256), 0, st, in, out, w, h,
-                                                  vflip ? 1 : 0, ib, rpb));
+        if (nt) { MIPX_FLIP(false, true); } else { MIPX_FLIP(false, false); }
     }
+#undef MIPX_FLIP
     return launch_check("k_flip_rows");
 }
 

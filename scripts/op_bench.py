@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--oh", type=int, default=0)
     ap.add_argument("--extend", type=int, default=1)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--ab", default="", help="KNOB=v1,v2,...: same-process A/B of a MIPX_* knob")
     ap.add_argument("--warm-ms", type=float, default=200.0, help="device-time warm-up; 0: none, one group (PMC runs)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -94,30 +95,52 @@ def main():
     # warm-up of >= 200 ms of device time first: a fresh process's first milliseconds run
     # below the sustained clock (r03: a 20-launch run of a 0.2 ms kernel read 15-20 % slow
     # against the same kernel in a long same-process A/B); then the median of 5 groups
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    check(run(), a.op)
-    torch.cuda.synchronize()
-    warm = 0.0
-    while warm < a.warm_ms:
-        e0.record(st)
-        for _ in range(10):
-            check(run(), a.op)
-        e1.record(st)
+    def measure():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        check(run(), a.op)
         torch.cuda.synchronize()
-        warm += e0.elapsed_time(e1)
-    groups = []
-    for _ in range(5 if a.warm_ms > 0 else 1):
-        e0.record(st)
-        for _ in range(a.iters):
-            check(run(), a.op)
-        e1.record(st)
-        torch.cuda.synchronize()
-        groups.append(e0.elapsed_time(e1) / a.iters)
-    ms = sorted(groups)[len(groups) // 2]
-    alg = n * (w * h * b + ow * oh * b)
-    print(json.dumps({"op": a.op, "w": w, "h": h, "b": b, "n": n, "s": a.s, "s2": s2, "out": [ow, oh],
-                      "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1)}))
+        warm = 0.0
+        while warm < a.warm_ms:
+            e0.record(st)
+            for _ in range(10):
+                check(run(), a.op)
+            e1.record(st)
+            torch.cuda.synchronize()
+            warm += e0.elapsed_time(e1)
+        groups = []
+        for _ in range(5 if a.warm_ms > 0 else 1):
+            e0.record(st)
+            for _ in range(a.iters):
+                check(run(), a.op)
+            e1.record(st)
+            torch.cuda.synchronize()
+            groups.append(e0.elapsed_time(e1) / a.iters)
+        return sorted(groups)[len(groups) // 2]
 
+    alg = n * (w * h * b + ow * oh * b)
+    line = {"op": a.op, "w": w, "h": h, "b": b, "n": n, "s": a.s, "s2": s2, "out": [ow, oh]}
+    if not a.ab:
+        ms = measure()
+        print(json.dumps({**line, "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1)}))
+        return
+    # same-process A/B: --ab KNOB=v1,v2,... interleaved over 2 rounds, output checked equal
+    knob, vals = a.ab.split("=", 1)
+    first = None
+    for rnd in range(2):
+        for v in vals.split(","):
+            os.environ[knob] = v
+            lib.mipx_tuning_reload()  # the library snapshots MIPX_* knobs
+            ms = measure()
+            same = None
+            if rnd == 0:
+                y.zero_()
+                check(run(), a.op)
+                torch.cuda.synchronize()
+                if first is None:
+                    first = y.clone()
+                same = bool(torch.equal(y, first))
+            print(json.dumps({**line, knob: v, "round": rnd, "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1),
+                              "same_as_first": same}), flush=True)
 
 if __name__ == "__main__":
     main()

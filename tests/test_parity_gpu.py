@@ -163,6 +163,29 @@ def test_embed_odd_sizes_all_bands(gpu, oracle, rng, b, extend):
         assert_same(got[0], oracle.embed(img, x, y, W, H, extend, (9, 250, 31)), f"embed {x},{y} {W}x{H} b{b}")
 
 
+@pytest.mark.parametrize("ver", ["0", "1", "2"])
+def test_embed_and_flip_row_kernels(gpu, oracle, rng, monkeypatch, ver):
+    """The embed row kernels (MIPX_EMBED_V: 0 one row at a time, 1 every row of the block
+    fetched first, 2 the same with non-temporal stores) and flip / rot 180 with plain or
+    non-temporal stores (MIPX_FLIP_NT), on batches with ragged row blocks, every extend mode."""
+    monkeypatch.setenv("MIPX_EMBED_V", ver)
+    monkeypatch.setenv("MIPX_FLIP_NT", "1" if ver == "2" else "0")
+    for h, w, b in ((37, 53, 3), (64, 96, 4), (130, 1100, 3), (7, 2000, 1)):
+        imgs = np.stack([rand_img(rng, h, w, b) for _ in range(2)])
+        for ext in range(6):
+            W, H = w + 37, h + 6
+            got = gpu.run_op("embed", imgs, x=17, y=3, width=W, height=H, extend=ext, background=(9, 250, 31))
+            for i in range(2):
+                assert_same(got[i], oracle.embed(imgs[i], 17, 3, W, H, ext, (9, 250, 31)), f"embed {ext} {h}x{w}x{b}")
+        for v in (0, 1):
+            got = gpu.run_op("flip", imgs, vertical=v)
+            for i in range(2):
+                assert_same(got[i], oracle.flip(imgs[i], v), f"flip{v} {h}x{w}x{b}")
+        got = gpu.run_op("rot", imgs, angle=180)
+        for i in range(2):
+            assert_same(got[i], oracle.rot(imgs[i], 180), f"rot180 {h}x{w}x{b}")
+
+
 @pytest.mark.parametrize("b", [1, 2, 3, 4])
 def test_extract_rot_flip(gpu, oracle, rng, b):
     img = rand_img(rng, 37, 53, b)
