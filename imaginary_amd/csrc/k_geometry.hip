@@ -6,9 +6,9 @@
 //    period W, MIRROR tiles the 2x2 [in, flip(in)] mosaic with period 2W,
 //    BLACK / WHITE / BACKGROUND fill).  With `origins` set it is an extract at a
 //    device-computed (left, top) — smartcrop needs no host round trip.
-//  * k_rot90_px<CW, 64, TH>: 90 / 270 for 3-band images through a pixel-major LDS
-//    tile (12 bytes per lane both ways); k_rot90_lds<B, CW, TH, T> for the other
-//    band counts; k_rot90t<B, CW> (32 x 32 tiles) past 2 GB per image.
+//  * k_rot90_px<B, CW, 64, TH>: 90 / 270 for 3- and 4-band images through a
+//    pixel-major LDS tile (4 pixels per lane both ways); k_rot90_lds<B, CW, TH, T> for
+//    1-2 bands; k_rot90t<B, CW> (32 x 32 tiles) past 2 GB per image.
 //  * k_extract_rows: row copies, dword lanes when rows and offset allow.
 #include <cstdlib>
 #include <hip/hip_runtime.h>
@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8
     }
 }
 
-// r03: 90 / 270 for 3-band images through a pixel-major LDS tile of TC input columns x TH
+// r03: 90 / 270 for 3- and 4-band images through a pixel-major LDS tile of TC input columns x TH
 // input rows.  Staging: a lane loads 4 pixels (12 bytes) of an input row and writes them as
 // 4 pixel dwords, each into its input column's run of TH dwords (slot = the pixel's place
 // in the output row), in 4-slot groups XOR-swizzled by the lane's quad so that the 16
@@ -430,11 +430,12 @@ __global__ void __launch_bounds__(256) k_rot90_lds(const u8 *__restrict__ in, u8
 // 12 bytes.  The 64 x 64 tiles of k_rot90_lds cap the same access pattern at 55 % of HBM
 // in a memory-only replica, 64 x 128 tiles taken row-band fastest at 65 %
 // (scripts/strip_probe.hip PROBE_ROT, profiles/r03/rot_probe.jsonl).
-template <bool CW, int TC, int TH>
+template <int B, bool CW, int TC, int TH>
 __global__ void __launch_bounds__(256) k_rot90_px(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int h,
                                                   long long img_bytes_, int tiles_x, int tiles_y, int yfast, int al) {
     constexpr int NQ = TC / 4, NG = TH / 4;
     static_assert(TC == 64 && TH % 16 == 0, "16 quads per tile row; whole 256-lane staging rounds");
+    static_assert(B == 3 || B == 4, "4 pixels = B dwords");
     __shared__ __attribute__((aligned(16))) uint32_t tile[TC * TH];
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     int bx, by, img;
@@ -452,23 +453,28 @@ __global__ void __launch_bounds__(256) k_rot90_px(const u8 *__restrict__ in, u8 
     int delta = 0;
     const __amdgpu_buffer_rsrc_t rs = image_rsrc_aligned(in + img * img_bytes_, img_bytes_, &delta);
     constexpr int KP = TH * NQ / 256;
-    uint32_t d[KP][3];
+    uint32_t d[KP][B];
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
         const int i = threadIdx.x + 256 * k, r = i / NQ, q = i % NQ;
-        const int abs0 = delta + ((ty0 + r) * w + tx0 + 4 * q) * 3;
+        const int abs0 = delta + ((ty0 + r) * w + tx0 + 4 * q) * B;
         const bool live = r < th && 4 * q < tw;
-        if (al) {  // rows and images on a dword: the 12 bytes are 3 dwords
+        if (B == 4) {  // 4-band images are dword aligned (rot_launch): the 16 bytes are 4 pixels
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+            const u4v p = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, live ? abs0 : 0x7ffffff0, 0, 0));
+#pragma unroll
+            for (int j = 0; j < B; ++j) d[k][j] = p[j];
+        } else if (al) {  // rows and images on a dword: the 12 bytes are 3 dwords
             typedef uint32_t u3v __attribute__((ext_vector_type(3)));
             const u3v p = __builtin_bit_cast(u3v, __builtin_amdgcn_raw_buffer_load_b96(rs, live ? abs0 : 0x7ffffff0, 0, 0));
-            d[k][0] = p[0], d[k][1] = p[1], d[k][2] = p[2];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) d[k][j] = p[j];
         } else {
             typedef uint32_t u4v __attribute__((ext_vector_type(4)));
             const u4v p = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rs, live ? abs0 & ~3 : 0x7ffffff0, 0, 0));
             const int sh = abs0 & 3;
-            d[k][0] = __builtin_amdgcn_alignbyte(p[1], p[0], sh);
-            d[k][1] = __builtin_amdgcn_alignbyte(p[2], p[1], sh);
-            d[k][2] = __builtin_amdgcn_alignbyte(p[3], p[2], sh);
+#pragma unroll
+            for (int j = 0; j < B && j < 3; ++j) d[k][j] = __builtin_amdgcn_alignbyte(p[j + 1], p[j], sh);
         }
     }
 #pragma unroll
@@ -477,10 +483,15 @@ __global__ void __launch_bounds__(256) k_rot90_px(const u8 *__restrict__ in, u8 
         if (r >= th || 4 * q >= tw) continue;
         const int s = CW ? th - 1 - r : r;  // slot: the pixel's place in its output row
         const int base = (4 * q) * TH + 4 * ((s >> 2) ^ (q & (NG - 1))) + (s & 3);
-        tile[base] = d[k][0];
-        tile[base + TH] = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], 3);
-        tile[base + 2 * TH] = __builtin_amdgcn_alignbyte(d[k][2], d[k][1], 2);
-        tile[base + 3 * TH] = d[k][2] >> 8;
+        if (B == 4) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) tile[base + j * TH] = d[k][j];
+        } else {
+            tile[base] = d[k][0];
+            tile[base + TH] = __builtin_amdgcn_alignbyte(d[k][1], d[k][0], 3);
+            tile[base + 2 * TH] = __builtin_amdgcn_alignbyte(d[k][2 % B], d[k][1], 2);
+            tile[base + 3 * TH] = d[k][2 % B] >> 8;
+        }
     }
     __syncthreads();
     const __amdgpu_buffer_rsrc_t dst = image_rsrc(out + img * img_bytes_, img_bytes_);
@@ -493,17 +504,27 @@ __global__ void __launch_bounds__(256) k_rot90_px(const u8 *__restrict__ in, u8 
         const int oy = CW ? tx0 + icol : w - 1 - (tx0 + icol);
         typedef uint32_t u4v __attribute__((ext_vector_type(4)));
         const u4v P = *reinterpret_cast<const u4v *>(tile + icol * TH + 4 * (g ^ ((icol >> 2) & (NG - 1))));
-        typedef uint32_t u3v __attribute__((ext_vector_type(3)));
-        const u3v o{__builtin_amdgcn_perm(P[1], P[0], 0x04020100u), __builtin_amdgcn_perm(P[2], P[1], 0x05040201u),
-                    __builtin_amdgcn_perm(P[3], P[2], 0x06050402u)};
-        const int off = (oy * h + ox + 4 * g) * 3;
-        if (4 * g + 4 <= th) {
-            __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u3v, o), dst, off, 0, 0);
-        } else {
-            const int nb = (th - 4 * g) * 3;
+        const int off = (oy * h + ox + 4 * g) * B;
+        if (B == 4) {
+            if (4 * g + 4 <= th) {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, P), dst, off, 0, 0);
+            } else {
 #pragma unroll
-            for (int j = 0; j < 9; ++j)
-                if (j < nb) __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(o[j >> 2] >> (8 * (j & 3))), dst, off + j, 0, 0);
+                for (int j = 0; j < 3; ++j)
+                    if (4 * g + j < th) __builtin_amdgcn_raw_buffer_store_b32(P[j], dst, off + 4 * j, 0, 0);
+            }
+        } else {
+            typedef uint32_t u3v __attribute__((ext_vector_type(3)));
+            const u3v o{__builtin_amdgcn_perm(P[1], P[0], 0x04020100u), __builtin_amdgcn_perm(P[2], P[1], 0x05040201u),
+                        __builtin_amdgcn_perm(P[3], P[2], 0x06050402u)};
+            if (4 * g + 4 <= th) {
+                __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u3v, o), dst, off, 0, 0);
+            } else {
+                const int nb = (th - 4 * g) * 3;
+#pragma unroll
+                for (int j = 0; j < 9; ++j)
+                    if (j < nb) __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(o[j >> 2] >> (8 * (j & 3))), dst, off + j, 0, 0);
+            }
         }
     }
 }
@@ -705,22 +726,27 @@ int rot_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int angle, hip
     if (angle == 180 && img_bytes(w, h, b) < 0x7fffffffLL && h <= 65535)
         return flip_rows_launch(in, out, n, w, h, b, true, true, st);
     const char *epx = tune_env("MIPX_ROT_PX");  // 0: 3-band images on k_rot90_lds (A/B)
-    if ((angle == 90 || angle == 270) && b == 3 && img_bytes(w, h, b) < 0x7fffffffLL && !(epx && *epx == '0')) {
+    // 4-band images too (profiles/r03/rot_px4_shrink_ntl_ab.jsonl: 1080p RGBA 4.00 -> 4.87 TB/s,
+    // 12 MP 3.99 -> 4.67, 4K 5.05 -> 5.01); MIPX_ROT_PX4=0 keeps them on k_rot90_lds (A/B)
+    const char *epx4 = tune_env("MIPX_ROT_PX4");
+    const bool px4 = b == 4 && !(epx4 && *epx4 == '0');
+    if ((angle == 90 || angle == 270) && (b == 3 || px4) && img_bytes(w, h, b) < 0x7fffffffLL && !(epx && *epx == '0')) {
         // input rows per tile (A/B, profiles/r03/rot_px_ab.jsonl): 128 where input rows are a
         // whole number of 128-byte lines (1080p / 4K: 5.0 TB/s against 4.6-4.9 at 32 / 64),
         // 64 where they end mid-line (12 MP, 12000 B: 4.7 against 4.5 at 128)
         const char *eph = tune_env("MIPX_ROT_PXH");
-        const int th = eph && *eph ? std::atoi(eph) : (static_cast<long long>(w) * 3) % 128 == 0 ? 128 : 64;
+        const int th = eph && *eph ? std::atoi(eph) : (static_cast<long long>(w) * b) % 128 == 0 ? 128 : 64;
         const char *eo = tune_env("MIPX_ROT_ORDER");  // 1: input row bands fastest
         const int yfast = eo && *eo ? *eo == '1' : 1;
         const int tx = (w + 63) / 64, ty = (h + th - 1) / th;
         const long long nblk = static_cast<long long>(tx) * ty * n;
         if (nblk > 0x7fffffffLL) return MIPX_EUNSUPPORTED;
         const long long ib = img_bytes(w, h, b);
-        const int al = aligned4(in) && (w * 3) % 4 == 0;
+        const int al = aligned4(in) && (w * b) % 4 == 0;
         const dim3 grid(static_cast<unsigned>(nblk));
-#define MIPX_ROTPX(CW_, TH_) \
-    hipLaunchKernelGGL((k_rot90_px<CW_, 64, TH_>), grid, dim3(256), 0, st, in, out, w, h, ib, tx, ty, yfast, al)
+#define MIPX_ROTPX(CW_, TH_)                                                                                       \
+    if (b == 3) hipLaunchKernelGGL((k_rot90_px<3, CW_, 64, TH_>), grid, dim3(256), 0, st, in, out, w, h, ib, tx, ty, yfast, al); \
+    else hipLaunchKernelGGL((k_rot90_px<4, CW_, 64, TH_>), grid, dim3(256), 0, st, in, out, w, h, ib, tx, ty, yfast, al)
         if (th == 32) {
             if (angle == 90) { MIPX_ROTPX(true, 32); } else { MIPX_ROTPX(false, 32); }
         } else if (th == 64) {

@@ -275,6 +275,20 @@ def test_batch_device_copy(gpu, rng, monkeypatch, route):
             assert np.array_equal(gpu.run_op("flatten", imgs, background=(1, 2, 3)), imgs), f"flatten {h}x{w}"
 
 
+@pytest.mark.parametrize("pxh", ["64", "128"])
+def test_rot90_rgba_pixel_tiles(gpu, oracle, rng, monkeypatch, pxh):
+    """k_rot90_px on 4-band images (the default; MIPX_ROT_PX4=0 keeps them on k_rot90_lds):
+    one b128 load and store per 4 pixels, ragged edge tiles, one-row / one-column images,
+    batches."""
+    monkeypatch.setenv("MIPX_ROT_PXH", pxh)
+    for h, w in ((130, 197), (128, 160), (1, 77), (77, 1), (3, 5), (257, 63), (66, 129)):
+        imgs = np.stack([rand_img(rng, h, w, 4) for _ in range(3)])
+        for a in (90, 270):
+            got = gpu.run_op("rot", imgs, angle=a)
+            for i in range(3):
+                assert_same(got[i], oracle.rot(imgs[i], a), f"rot{a} {h}x{w}x4 img{i} pxh={pxh}")
+
+
 @pytest.mark.parametrize("x4", ["1", "0"])
 def test_shrink_x4_and_dword_kernels(gpu, oracle, rng, monkeypatch, x4):
     """Box shrink: the 16-byte-per-lane kernel (dword-aligned rows, vs <= 257) and
