@@ -60,6 +60,8 @@ struct BcArgs {
     uint32_t mag;       // floor(x / scale) == mulhi(x, mag) for the sums here
     int seed;           // 128 scale + (scale + 1) / 2
     int wst2;           // output rows not a multiple of 16 bytes: the edge piece as dwords
+    int a16;            // host: horizontal operands 16-byte aligned (k_bcol<.., A16 = true>)
+    int sd;             // A16: staged rows start sd bytes into their LDS row (0 / 4 / 8 / 12)
     const signed char *ops;  // device_blur_ops: [NKS][64 lanes][16] horizontal, then [64][16] vertical
 };
 
@@ -82,7 +84,7 @@ __device__ __forceinline__ rc_u2 lds_rd2x32(uint32_t a) {
 // B: bands, NKS: horizontal K steps of 64 bytes, KMAX: staging chunks per lane per step.
 // 64-pixel strips: 128-pixel ones (UPW 6 / 8, operands in chunks of half) measured 10-40 %
 // slower at 2-3 waves per SIMD (profiles/r03/bcol_px_chunk_ab.jsonl)
-template <int B, int NKS, int KMAX>
+template <int B, int NKS, int KMAX, bool A16>
 __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
     constexpr int PX = kBcPX;
     constexpr int UPW = B;  // 16-byte units per wave: 64 B / 16 over the 4 waves
@@ -129,7 +131,7 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
         rr[k] = c / a.cpr;
         const int col = c - rr[k] * a.cpr;
         cof[k] = static_cast<int>(a.in_base) + B * sx + 16 * col;
-        lsl[k] = static_cast<uint32_t>(rr[k] * a.rsd + 16 * col);
+        lsl[k] = static_cast<uint32_t>(rr[k] * a.rsd + 16 * col + (A16 ? a.sd : 0));
     }
     rc_u4 rv[2][KMAX];
     auto issue = [&](auto pc, int j) {  // the input rows of step j: 16 j + half + rr
@@ -145,12 +147,16 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
         constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int k = 0; k < KMAX; ++k)
-            if (rr[k] < kBcRows) lds_wr128(stg_l + static_cast<uint32_t>(P * kBcRows * a.rsd) + lsl[k], rv[P][k] ^ 0x80808080u);
+            if (rr[k] < kBcRows) {
+                const uint32_t ad = stg_l + static_cast<uint32_t>(P * kBcRows * a.rsd) + lsl[k];
+                if (A16 && a.sd) lds_wr4x32(ad, rv[P][k] ^ 0x80808080u);  // rows shifted onto the 16-byte operand grid
+                else lds_wr128(ad, rv[P][k] ^ 0x80808080u);
+            }
     };
     // COPY edge: staged pixels outside the window repeat its edge pixel
     auto fixup = [&](auto pc) {
         constexpr int P = decltype(pc)::value;
-        u8 *sb = stgb + P * kBcRows * a.rsd;
+        u8 *sb = stgb + P * kBcRows * a.rsd + (A16 ? a.sd : 0);
         for (int i = tid; i < kBcRows * a.spx; i += kBcNT) {
             const int l = i / a.spx, pq = i - l * a.spx, p = sx + pq;
             if (p >= 0 && p < a.w) continue;
@@ -174,8 +180,14 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
                 for (int ks = 0; ks < NKS; ++ks) {
                     const uint32_t ad = sr + static_cast<uint32_t>(16 * (UPW * wave + c0 + i) + 64 * ks);
                     if (64 * ks + 16 * kg < a.kspan) {  // lanes whose 16 K bytes lie past the taps read nothing
-                        q[i][ks][0] = lds_rd2x32(ad);
-                        q[i][ks][1] = lds_rd2x32(ad + 8);
+                        if (A16) {
+                            const rc_u4 v = lds_rd128(ad);
+                            q[i][ks][0] = rc_u2{v.x, v.y};
+                            q[i][ks][1] = rc_u2{v.z, v.w};
+                        } else {
+                            q[i][ks][0] = lds_rd2x32(ad);
+                            q[i][ks][1] = lds_rd2x32(ad + 8);
+                        }
                     } else {
                         q[i][ks][0] = rc_u2{0u, 0u};
                         q[i][ks][1] = rc_u2{0u, 0u};
@@ -315,8 +327,19 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     a.sx0 = (a.half + al - 1) / al * al;
     const int px = kBcPX;
     a.spx = px + a.sx0 + a.half;
-    const int e = b * (a.sx0 - a.half), delta = e & 3;
-    a.kb0 = e & ~3;
+    // r03: the H operand starts on 16 bytes, so a unit's 16 K bytes are one ds_read_b128, and
+    // staged rows 32 mod 64 bytes apart put the 16 rows x 4 K groups of every lane group on
+    // distinct banks (two ds_read2_b32 on dword offsets hit 8 banks with 32 lanes: 4-way,
+    // profiles/r03/pmc_bcol_*.txt).  The staged rows are written sd = 0 / 4 / 8 / 12 bytes
+    // into their LDS rows (dword writes) so the operand's dword offset lands on 16 bytes and
+    // the taps keep only the 0-3 byte offset (no extra K step); MIPX_BCOL_A16=0 keeps the
+    // dword-aligned operand (A/B)
+    const int e = b * (a.sx0 - a.half);
+    const char *ea = tune_env("MIPX_BCOL_A16");
+    a.a16 = !(ea && *ea == '0');
+    a.sd = a.a16 ? (16 - (e & 12)) & 12 : 0;
+    const int delta = e & 3;
+    a.kb0 = a.a16 ? (e + a.sd) & ~15 : e & ~3;
     a.kspan = 16 + delta + b * (taps - 1);
     const int nks = (a.kspan + 63) / 64;
     if (nks > 3) return MIPX_EUNSUPPORTED;
@@ -324,9 +347,13 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     const int kmax = (kBcRows * a.cpr + kBcNT - 1) / kBcNT;
     if (kmax > 3) return MIPX_EUNSUPPORTED;
     // staging stride: every horizontal read in the row (+ 4 units of slack), dwords = 4 mod 8
-    int rsd = std::max(16 * a.cpr, a.kb0 + px * b + 64 * nks) + 16;
+    int rsd = std::max(16 * a.cpr + a.sd, a.kb0 + px * b + 64 * nks) + 16;
     rsd = (rsd + 15) & ~15;
-    while ((rsd / 4) % 8 != 4) rsd += 16;
+    if (a.a16) {
+        while ((rsd / 16) % 4 != 2) rsd += 16;
+    } else {
+        while ((rsd / 4) % 8 != 4) rsd += 16;
+    }
     a.rsd = rsd;
     const int ring = kBcRows + taps - 1 <= 32 ? 32 : 64;
     a.rmask = ring - 1;
@@ -345,16 +372,19 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
 
     const void *fn = nullptr;
-#define MIPX_BC_K(B_, NKS_)                                                                        \
-    fn = kmax == 1   ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 1>)                        \
-         : kmax == 2 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 2>)                        \
-                     : reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 3>);
+#define MIPX_BC_K2(B_, NKS_, A_)                                                                   \
+    fn = kmax == 1   ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 1, A_>)                    \
+         : kmax == 2 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 2, A_>)                    \
+                     : reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 3, A_>);
+#define MIPX_BC_K(B_, NKS_) \
+    if (a.a16) { MIPX_BC_K2(B_, NKS_, true) } else { MIPX_BC_K2(B_, NKS_, false) }
     if (b == 3) {
         if (nks == 1) { MIPX_BC_K(3, 1) } else if (nks == 2) { MIPX_BC_K(3, 2) } else { MIPX_BC_K(3, 3) }
     } else {
         if (nks == 1) { MIPX_BC_K(4, 1) } else if (nks == 2) { MIPX_BC_K(4, 2) } else { MIPX_BC_K(4, 3) }
     }
 #undef MIPX_BC_K
+#undef MIPX_BC_K2
 
     // segments: a segment's first pre steps only filter; pick the split that minimises
     // (rounds of resident blocks) x (steps + pre)

@@ -49,6 +49,11 @@ __device__ __forceinline__ rc_v2i lds_tr8(uint32_t a) {
 }
 __device__ __forceinline__ void lds_wr32(uint32_t a, uint32_t v) { asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory"); }
 __device__ __forceinline__ void lds_wr128(uint32_t a, rc_u4 v) { asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory"); }
+// 16 bytes at a 4-byte-aligned LDS address: two ds_write2_b32 (dwords 0, 1 / 2, 3)
+__device__ __forceinline__ void lds_wr4x32(uint32_t a, rc_u4 v) {
+    asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(a), "v"(v.x), "v"(v.y) : "memory");
+    asm volatile("ds_write2_b32 %0, %1, %2 offset0:2 offset1:3" ::"v"(a), "v"(v.z), "v"(v.w) : "memory");
+}
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // The wait must also be a data dependence of the values it waits for: an asm read's
 // result is an ordinary register to the compiler, which could otherwise schedule its

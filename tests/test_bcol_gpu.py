@@ -14,10 +14,12 @@ from test_parity_gpu import assert_same, rand_img, smooth_img
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["bcol", "nobcol"])
+@pytest.fixture(autouse=True, params=["bcol", "bcol_dw", "nobcol"])
 def route(request, monkeypatch):
-    """k_bcol (the default) and the kernels behind it (MIPX_BCOL=0: k_bmf / k_blur2d)."""
-    monkeypatch.setenv("MIPX_BCOL", "" if request.param == "bcol" else "0")
+    """k_bcol (the default: 16-byte-aligned horizontal operands), k_bcol with the dword-aligned
+    operands (MIPX_BCOL_A16=0) and the kernels behind it (MIPX_BCOL=0: k_bmf / k_blur2d)."""
+    monkeypatch.setenv("MIPX_BCOL", "0" if request.param == "nobcol" else "")
+    monkeypatch.setenv("MIPX_BCOL_A16", "0" if request.param == "bcol_dw" else "")
     yield request.param
 
 
