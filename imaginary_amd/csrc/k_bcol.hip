@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <vector>
 
 #include "device_common.h"
@@ -38,7 +39,7 @@ using namespace dev;
 
 constexpr int kBcRows = 16;  // rows per step (the MFMA N)
 constexpr int kBcNT = 256;   // threads per block
-constexpr int kBcPX = 64;    // output pixels per strip
+constexpr int kBcSB = 64;    // output bytes per strip and 16-byte unit per wave (strip = kBcSB * UPW bytes)
 
 struct BcArgs {
     const u8 *in;
@@ -49,9 +50,9 @@ struct BcArgs {
     int w, h;           // window = output size (COPY clamp range)
     int strips, segs, seg_steps, ksteps;
     int half;           // taps / 2
-    int sx0;            // staged rows start at window pixel x0 - sx0 (B sx0 a multiple of 16)
-    int spx;            // staged pixels per strip row
-    int kb0;            // the H operand's first staged byte (e & ~3, e = B (sx0 - half))
+    int sxb;            // staged rows start sxb bytes before the strip (a multiple of 16, >= B half)
+    int spb;            // staged bytes per strip row
+    int kb0;            // the H operand's first staged byte (e & ~3, e = sxb - B half)
     int cpr;            // 16-byte chunks per staged row
     int rsd;            // staging row stride (bytes)
     int rmask, tw;      // ring rows - 1, ring row stride (bytes)
@@ -81,13 +82,14 @@ __device__ __forceinline__ rc_u2 lds_rd2x32(uint32_t a) {
     return v;
 }
 
-// B: bands, NKS: horizontal K steps of 64 bytes, KMAX: staging chunks per lane per step.
-// 64-pixel strips: 128-pixel ones (UPW 6 / 8, operands in chunks of half) measured 10-40 %
-// slower at 2-3 waves per SIMD (profiles/r03/bcol_px_chunk_ab.jsonl)
-template <int B, int NKS, int KMAX, bool A16>
+// B: bands, NKS: horizontal K steps of 64 bytes, KMAX: staging chunks per lane per step,
+// UPW: 16-byte units per wave (strips of 64 UPW bytes; the passes are byte-column-wise and
+// the taps of output byte X sit at X + B (k - half), so strips need not start on a pixel).
+// 128-pixel strips (UPW 6 / 8, operands in chunks of half) measured 10-40 % slower at 2-3
+// waves per SIMD (profiles/r03/bcol_px_chunk_ab.jsonl)
+template <int B, int NKS, int KMAX, bool A16, int UPW>
 __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
-    constexpr int PX = kBcPX;
-    constexpr int UPW = B;  // 16-byte units per wave: 64 B / 16 over the 4 waves
+    constexpr int SB = kBcSB * UPW;  // strip bytes
     constexpr int WSR = 16 * UPW + (UPW % 2 == 0 ? 16 : 0);  // dwords = 4 mod 8: the tile writes on distinct banks
     constexpr int NPC = (16 * UPW + 63) / 64;                  // 16-byte row pieces per lane
     constexpr int UC = UPW;                                    // units per operand chunk
@@ -106,10 +108,10 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n = lane & 15, kg = lane >> 4;
 
-    const int x0 = strip * PX, xw = min(PX, a.w - x0);
-    const int vbytes = B * xw;
-    const int sx = x0 - a.sx0;                              // window pixel of staged pixel 0
-    const bool edge = sx < 0 || sx + a.spx > a.w;           // block-uniform
+    const int wb = a.w * B;                                 // window row bytes
+    const int xb0 = strip * SB, vbytes = min(SB, wb - xb0);  // the strip's output bytes in a row
+    const int sxb = xb0 - a.sxb;                            // window row byte of staged byte 0
+    const bool edge = sxb < 0 || sxb + a.spb > wb;          // block-uniform
     const int ka = seg * a.seg_steps, kz = min(a.ksteps, ka + a.seg_steps);
     const int j0 = ka - a.pre;                              // first (filter-only) step
 
@@ -130,7 +132,7 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
         const int c = tid + kBcNT * k;
         rr[k] = c / a.cpr;
         const int col = c - rr[k] * a.cpr;
-        cof[k] = static_cast<int>(a.in_base) + B * sx + 16 * col;
+        cof[k] = static_cast<int>(a.in_base) + sxb + 16 * col;
         lsl[k] = static_cast<uint32_t>(rr[k] * a.rsd + 16 * col + (A16 ? a.sd : 0));
     }
     rc_u4 rv[2][KMAX];
@@ -153,16 +155,17 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
                 else lds_wr128(ad, rv[P][k] ^ 0x80808080u);
             }
     };
-    // COPY edge: staged pixels outside the window repeat its edge pixel
+    // COPY edge: staged bytes outside the window repeat its edge pixel's byte of their band
+    // (only the nl bytes left of the window and the nr right of it are visited)
+    const int nl = max(0, -sxb), nr = max(0, sxb + a.spb - wb), no = nl + nr;
     auto fixup = [&](auto pc) {
         constexpr int P = decltype(pc)::value;
         u8 *sb = stgb + P * kBcRows * a.rsd + (A16 ? a.sd : 0);
-        for (int i = tid; i < kBcRows * a.spx; i += kBcNT) {
-            const int l = i / a.spx, pq = i - l * a.spx, p = sx + pq;
-            if (p >= 0 && p < a.w) continue;
-            const int sp = clampi(p, 0, a.w - 1) - sx;
-#pragma unroll
-            for (int z = 0; z < B; ++z) sb[l * a.rsd + pq * B + z] = sb[l * a.rsd + sp * B + z];
+        for (int i = tid; i < kBcRows * no; i += kBcNT) {
+            const int l = i / no, t = i - l * no;
+            const int q = t < nl ? t : a.spb - nr + (t - nl), X = sxb + q;
+            const int c = (X % B + B) % B;
+            sb[l * a.rsd + q] = sb[l * a.rsd + (X < 0 ? c : wb - B + c) - sxb];
         }
     };
     // horizontal pass of step j: this wave's units, 16 staged rows -> ring rows 16 j + half + n
@@ -257,7 +260,7 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
             const int we = 16 * (UPW * wave + wch);  // the piece's first byte in the strip row
             const int y = kBcRows * j + wrow;
             const bool ok = live && pc < 16 * UPW && y < a.h;
-            const int base = (y * a.w + x0) * B + we;
+            const int base = y * wb + xb0 + we;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, qv[r]), dst,
                                                    ok && we + 16 <= vbytes ? base : 0x7ffffff0, 0, 0);
             if (a.wst2) {  // rows whose byte count is not a multiple of 16: the piece at the window edge in dwords
@@ -321,12 +324,16 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     a.w = ow;
     a.h = oh;
     a.half = taps / 2;
-    // the staged origin B (x0 - sx0) sits on 16 bytes at the window's left edge, so no chunk
-    // straddles a row start (a load at a negative offset reads 0 whole)
-    const int al = b == 3 ? 16 : 4;
-    a.sx0 = (a.half + al - 1) / al * al;
-    const int px = kBcPX;
-    a.spx = px + a.sx0 + a.half;
+    // strips of 64 UPW bytes: RGBA 64 pixels (UPW 4); RGB 256 bytes (UPW 4, 85 1/3 pixels:
+    // 1080p / 4K / 12 MP 7-12 % faster than 64-pixel strips, profiles/r03/bcol_rgb256_ab.jsonl;
+    // MIPX_BCOL_RGB192=1 keeps those, A/B).  The staged origin sits sxb bytes before
+    // the strip, on 16 bytes, so no chunk straddles a row start (a load at a negative offset
+    // reads 0 whole)
+    const char *e192 = tune_env("MIPX_BCOL_RGB192");
+    const int upw = b == 4 || !(e192 && *e192 == '1') ? 4 : 3;
+    const int sbytes = kBcSB * upw;
+    a.sxb = (a.half * b + 15) / 16 * 16;
+    a.spb = sbytes + a.sxb + a.half * b;
     // r03: the H operand starts on 16 bytes, so a unit's 16 K bytes are one ds_read_b128, and
     // staged rows 32 mod 64 bytes apart put the 16 rows x 4 K groups of every lane group on
     // distinct banks (two ds_read2_b32 on dword offsets hit 8 banks with 32 lanes: 4-way,
@@ -334,20 +341,20 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     // into their LDS rows (dword writes) so the operand's dword offset lands on 16 bytes and
     // the taps keep only the 0-3 byte offset (no extra K step); MIPX_BCOL_A16=0 keeps the
     // dword-aligned operand (A/B)
-    const int e = b * (a.sx0 - a.half);
+    const int e = a.sxb - b * a.half;
     const char *ea = tune_env("MIPX_BCOL_A16");
-    a.a16 = !(ea && *ea == '0');
+    a.a16 = !(ea && *ea == '0') || upw != b;  // the 256-byte RGB strips exist only with A16
     a.sd = a.a16 ? (16 - (e & 12)) & 12 : 0;
     const int delta = e & 3;
     a.kb0 = a.a16 ? (e + a.sd) & ~15 : e & ~3;
     a.kspan = 16 + delta + b * (taps - 1);
     const int nks = (a.kspan + 63) / 64;
     if (nks > 3) return MIPX_EUNSUPPORTED;
-    a.cpr = (b * a.spx + 15) / 16;
+    a.cpr = (a.spb + 15) / 16;
     const int kmax = (kBcRows * a.cpr + kBcNT - 1) / kBcNT;
     if (kmax > 3) return MIPX_EUNSUPPORTED;
     // staging stride: every horizontal read in the row (+ 4 units of slack), dwords = 4 mod 8
-    int rsd = std::max(16 * a.cpr + a.sd, a.kb0 + px * b + 64 * nks) + 16;
+    int rsd = std::max(16 * a.cpr + a.sd, a.kb0 + sbytes + 64 * nks) + 16;
     rsd = (rsd + 15) & ~15;
     if (a.a16) {
         while ((rsd / 16) % 4 != 2) rsd += 16;
@@ -357,7 +364,7 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     a.rsd = rsd;
     const int ring = kBcRows + taps - 1 <= 32 ? 32 : 64;
     a.rmask = ring - 1;
-    int twd = (px * b) / 4;  // the transposed reads: (dwords mod 64) / 4 odd
+    int twd = sbytes / 4;  // the transposed reads: (dwords mod 64) / 4 odd
     twd = (twd + 3) & ~3;
     while (((twd & 63) >> 2) % 2 == 0) twd += 4;
     a.tw = 4 * twd;
@@ -368,16 +375,18 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     a.ops = device_blur_ops(mask, b, delta, nks);
     if (!a.ops) return MIPX_EDEVICE;
     const size_t lds = static_cast<size_t>(2 * kBcRows) * rsd + static_cast<size_t>(ring) * a.tw +
-                       static_cast<size_t>(4 * kBcRows) * (16 * (b * px / 64) + ((b * px / 64) % 2 == 0 ? 16 : 0));
+                       static_cast<size_t>(4 * kBcRows) * (16 * upw + (upw % 2 == 0 ? 16 : 0));
     if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
 
     const void *fn = nullptr;
-#define MIPX_BC_K2(B_, NKS_, A_)                                                                   \
-    fn = kmax == 1   ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 1, A_>)                    \
-         : kmax == 2 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 2, A_>)                    \
-                     : reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 3, A_>);
-#define MIPX_BC_K(B_, NKS_) \
-    if (a.a16) { MIPX_BC_K2(B_, NKS_, true) } else { MIPX_BC_K2(B_, NKS_, false) }
+#define MIPX_BC_K2(B_, NKS_, A_, U_)                                                               \
+    fn = kmax == 1   ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 1, A_, U_>)                \
+         : kmax == 2 ? reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 2, A_, U_>)                \
+                     : reinterpret_cast<const void *>(&k_bcol<B_, NKS_, 3, A_, U_>);
+#define MIPX_BC_K(B_, NKS_)                                                   \
+    if (B_ == 3 && upw == 4) { MIPX_BC_K2(B_, NKS_, true, 4) }                \
+    else if (a.a16) { MIPX_BC_K2(B_, NKS_, true, B_) }                        \
+    else { MIPX_BC_K2(B_, NKS_, false, B_) }
     if (b == 3) {
         if (nks == 1) { MIPX_BC_K(3, 1) } else if (nks == 2) { MIPX_BC_K(3, 2) } else { MIPX_BC_K(3, 3) }
     } else {
@@ -386,30 +395,30 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
 #undef MIPX_BC_K
 #undef MIPX_BC_K2
 
-    // segments: a segment's first pre steps only filter; pick the split that minimises
-    // (rounds of resident blocks) x (steps + pre)
-    a.strips = (ow + px - 1) / px;
+    // segments: a segment's first pre steps only filter.  About 6 rounds of resident blocks
+    // (profiles/r03/bcol_segs_ab.jsonl, bcol_rgb256_ab.jsonl: 1080p RGB best at 7.5 rounds,
+    // 12 MP at 8, 1080p RGBA at 3-6, C3's RGBA at 2 segments; one long segment per strip left
+    // 1080p 30-40 % slower), segments of at least max(4, 4 pre) steps so the filter-only
+    // steps stay <= 25 %
+    a.strips = (ow * b + sbytes - 1) / sbytes;
     a.ksteps = (oh + kBcRows - 1) / kBcRows;
     const long long cols = static_cast<long long>(a.strips) * n;
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBcNT, lds) != hipSuccess || per_cu < 1) per_cu = 2;
     const long long slots = 256LL * per_cu;
-    int best_segs = 1;
-    double best = 1e300;
-    for (int segs = 1; segs <= a.ksteps; ++segs) {
-        const int ss = (a.ksteps + segs - 1) / segs;
-        if (segs > 1 && ss < 4) break;
-        const long long blocks = cols * ((a.ksteps + ss - 1) / ss);
-        const double cost = static_cast<double>((blocks + slots - 1) / slots) * (ss + a.pre);
-        if (cost < best - 1e-9) {
-            best = cost;
-            best_segs = segs;
-        }
-    }
+    const int ss_min = std::max(4, 4 * a.pre);
+    int best_segs = static_cast<int>(std::max(1LL, (6 * slots + cols / 2) / cols));
+    best_segs = std::min(best_segs, std::max(1, (a.ksteps + ss_min - 1) / ss_min));
+    const char *esg = tune_env("MIPX_BCOL_SEGS");  // A/B: force the segment count
+    if (esg && *esg) best_segs = std::max(1, std::min(a.ksteps, std::atoi(esg)));
     a.seg_steps = (a.ksteps + best_segs - 1) / best_segs;
     a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
     const long long blocks = cols * a.segs;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
+    if (tune_env("MIPX_BCOL_DBG"))
+        fprintf(stderr, "k_bcol b=%d upw=%d a16=%d nks=%d kmax=%d taps=%d sxb=%d spb=%d e=%d sd=%d kb0=%d rsd=%d tw=%d ring=%d lds=%zu per_cu=%d strips=%d segs=%d seg_steps=%d pre=%d blocks=%lld\n",
+                b, upw, a.a16, nks, kmax, taps, a.sxb, a.spb, e, a.sd, a.kb0, a.rsd, a.tw, ring, lds, per_cu, a.strips, a.segs,
+                a.seg_steps, a.pre, blocks);
     hipLaunchKernelGGL(reinterpret_cast<void (*)(BcArgs)>(const_cast<void *>(fn)), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBcNT), lds, st, a);
     return launch_check("k_bcol");

@@ -14,17 +14,21 @@ from test_parity_gpu import assert_same, rand_img, smooth_img
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["bcol", "bcol_dw", "nobcol"])
+@pytest.fixture(autouse=True, params=["bcol", "bcol192", "bcol192_dw", "nobcol"])
 def route(request, monkeypatch):
-    """k_bcol (the default: 16-byte-aligned horizontal operands), k_bcol with the dword-aligned
-    operands (MIPX_BCOL_A16=0) and the kernels behind it (MIPX_BCOL=0: k_bmf / k_blur2d)."""
+    """k_bcol (the default: 256-byte strips, RGB ones starting mid-pixel, 16-byte-aligned
+    horizontal operands), RGB on 64-pixel strips (MIPX_BCOL_RGB192=1), the same with the
+    dword-aligned operands (+ MIPX_BCOL_A16=0; RGBA too) and the kernels behind it
+    (MIPX_BCOL=0: k_bmf / k_blur2d)."""
     monkeypatch.setenv("MIPX_BCOL", "0" if request.param == "nobcol" else "")
-    monkeypatch.setenv("MIPX_BCOL_A16", "0" if request.param == "bcol_dw" else "")
+    monkeypatch.setenv("MIPX_BCOL_RGB192", "1" if request.param.startswith("bcol192") else "")
+    monkeypatch.setenv("MIPX_BCOL_A16", "0" if request.param == "bcol192_dw" else "")
     yield request.param
 
 
 SHAPES = [(64, 76, 3), (130, 516, 3), (9, 600, 4), (50, 260, 4), (3, 8, 4), (33, 20, 3), (17, 132, 3), (200, 388, 4),
-          (47, 140, 3), (95, 300, 4), (300, 64, 3), (1, 128, 4), (700, 96, 3), (37, 1028, 3)]
+          (47, 140, 3), (95, 300, 4), (300, 64, 3), (1, 128, 4), (700, 96, 3), (37, 1028, 3), (20, 88, 3), (19, 84, 3),
+          (40, 172, 3), (12, 256, 3)]
 
 
 @pytest.mark.parametrize("sigma", [0.3, 1.0, 2.2, 3.0, 5.0, 7.5])
