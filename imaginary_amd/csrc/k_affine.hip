@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
 // down start), each lane gathers its 16 output bytes from LDS, and the chunk is stored
 // to all yf output rows (the r02 kernel loaded every output byte from global memory,
 // once per output row: 15 % of HBM).
-template <int B>
+template <int B, bool NT>
 __global__ void __launch_bounds__(256) k_zoom_rows(const u8 *__restrict__ in, u8 *__restrict__ out, int w, int ow,
                                                    int xf, int yf, float rxf, long long in_img, long long out_img) {
     __shared__ __attribute__((aligned(16))) uint32_t seg[1024 + 8];
@@ -308,7 +308,9 @@ __global__ void __launch_bounds__(256) k_zoom_rows(const u8 *__restrict__ in, u8
     const bool wide = nb == 16 && (reinterpret_cast<uintptr_t>(q) & 15u) == 0 && (row_out & 15) == 0;
     for (int r = 0; r < yf; ++r, q += row_out) {
         if (wide) {
-            *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
+            typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+            if (NT) __builtin_nontemporal_store(u4v{v[0], v[1], v[2], v[3]}, reinterpret_cast<u4v *>(q));
+            else *reinterpret_cast<uint4 *>(q) = uint4{v[0], v[1], v[2], v[3]};
         } else {
             for (int k = 0; k < nb; ++k) q[k] = static_cast<u8>(v[k >> 2] >> (8 * (k & 3)));
         }
@@ -375,8 +377,16 @@ int zoom_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int xf, int y
     if (img_bytes(w, h, b) >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     const dim3 grid((ow * b + 4095) / 4096, h, n);
     const float rxf = 1.0f / static_cast<float>(xf);
-    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_zoom_rows<B_>, grid, dim3(256), 0, st, in, out, w, ow, xf, yf, rxf,
-                                              img_bytes(w, h, b), img_bytes(ow, h * yf, b)));
+    // whole 4 KiB row chunks: MIPX_ZOOM_NT=1 stores them non-temporally, as embed / flip do
+    // (A/B; not yet measured on zoom, so plain stores stay the default)
+    const char *en = tune_env("MIPX_ZOOM_NT");
+    if (en && *en == '1') {
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_zoom_rows<B_, true>), grid, dim3(256), 0, st, in, out, w, ow, xf, yf,
+                                                  rxf, img_bytes(w, h, b), img_bytes(ow, h * yf, b)));
+    } else {
+        MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_zoom_rows<B_, false>), grid, dim3(256), 0, st, in, out, w, ow, xf, yf,
+                                                  rxf, img_bytes(w, h, b), img_bytes(ow, h * yf, b)));
+    }
     return launch_check("k_zoom_rows");
 }
 
