@@ -377,10 +377,11 @@ int zoom_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int xf, int y
     if (img_bytes(w, h, b) >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
     const dim3 grid((ow * b + 4095) / 4096, h, n);
     const float rxf = 1.0f / static_cast<float>(xf);
-    // whole 4 KiB row chunks: MIPX_ZOOM_NT=1 stores them non-temporally, as embed / flip do
-    // (A/B; not yet measured on zoom, so plain stores stay the default)
+    // whole 4 KiB row chunks stored non-temporally, as embed / flip do (profiles/r03/
+    // zoom_nt_ab.jsonl: 1080p RGB x2 4.67 -> 5.76 TB/s, 1024x768 RGBA x3 5.21 -> 6.40);
+    // MIPX_ZOOM_NT=0 keeps plain stores (A/B)
     const char *en = tune_env("MIPX_ZOOM_NT");
-    if (en && *en == '1') {
+    if (!(en && *en == '0')) {
         MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_zoom_rows<B_, true>), grid, dim3(256), 0, st, in, out, w, ow, xf, yf,
                                                   rxf, img_bytes(w, h, b), img_bytes(ow, h * yf, b)));
     } else {

@@ -617,7 +617,7 @@ def test_affine_matches_oracle(gpu, oracle, rng, h, w, b, xs, ys, extend):
 @pytest.mark.parametrize("nt", ["1", "0"])
 @pytest.mark.parametrize("b", [1, 2, 3, 4])
 def test_zoom_flatten_bw_match_oracle(gpu, oracle, rng, monkeypatch, b, nt):
-    monkeypatch.setenv("MIPX_ZOOM_NT", nt)  # zoom rows with non-temporal or plain (default) stores
+    monkeypatch.setenv("MIPX_ZOOM_NT", nt)  # zoom rows with non-temporal (default) or plain stores
     imgs = np.stack([rand_img(rng, 19, 23, b), smooth_img(rng, 19, 23, b)])
     for xf, yf in ((2, 2), (3, 1), (1, 4), (5, 3)):
         got = gpu.run_op("zoom", imgs, xfac=xf, yfac=yf)
