@@ -201,8 +201,10 @@ def test_extract_rot_flip(gpu, oracle, rng, b):
     assert_same(r, img, "rot90^4 == identity")
 
 
+@pytest.mark.parametrize("nt", ["0", "1"])
 @pytest.mark.parametrize("b", [1, 2, 3, 4])
-def test_extract_batches_any_alignment(gpu, oracle, rng, b):
+def test_extract_batches_any_alignment(gpu, oracle, rng, monkeypatch, b, nt):
+    monkeypatch.setenv("MIPX_EXTRACT_NT", nt)  # row copies with plain / non-temporal stores
     """Extract over batches of odd-size images (later images start unaligned) and odd
     windows: the dword copy, the embed-interior path and the per-pixel remap."""
     for h, w, left, top, ow, oh in ((37, 53, 5, 7, 31, 20), (40, 64, 4, 3, 32, 16), (29, 301, 101, 2, 157, 25)):
