@@ -12,3 +12,6 @@ for l in open(sys.argv[1]):
     d=json.loads(l); k=[x for x in d if x.startswith("MIPX")][0]
     if d["round"]==1: print(d["op"], d["w"], d["h"], d["b"], d["out"], k, repr(d[k]), d["ms"], d["alg_GBps"], d.get("same_as_first"))
 PY
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 800 python3 -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?; tail -3 $O/pytest_gpu.log; exit $rc
