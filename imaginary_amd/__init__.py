@@ -8,6 +8,7 @@ from ._abi import lib, MipxError, MipxPlan, MipxOpts, MipxInput, LIB_PATH, TYPES
 from ._abi import (MIPX_OK, MIPX_EINVAL, MIPX_EUNSUPPORTED, MIPX_ENOMEM, MIPX_ENODEV, MIPX_EDEVICE,  # noqa: F401
                    MIPX_ETIMEOUT, MIPX_ENOTINIT, MIPX_ESTALE)
 from .engine import (DeviceBuffer, Engine, device_count, execute, fit_dimension, make_input,  # noqa: F401
-                     make_opts, plan_chain, plan_make, run_op, smartcrop_origins, synchronize)
+                     make_opts, plan_chain, plan_make, reduce_sampling, run_op, set_reduce_sampling,
+                     smartcrop_origins, synchronize)
 
 __version__ = "0.2.0"

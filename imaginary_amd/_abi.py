@@ -150,6 +150,8 @@ _SIG = {
     "mipx_op_smartcrop_origin": (C.c_int, [_U8P, _P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _P]),
     "mipx_op_workspace_bytes": (C.c_size_t, [_I, _I, _I, _I, _I, C.c_double, C.c_double]),
     "mipx_tuning_reload": (C.c_int, []),
+    "mipx_set_reduce_sampling": (C.c_int, [C.c_int32]),
+    "mipx_reduce_sampling": (C.c_int, []),
     "mipx_set_device": (C.c_int, [C.c_int]),
     "mipx_dev_malloc": (C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
     "mipx_dev_free": (C.c_int, [_P]),

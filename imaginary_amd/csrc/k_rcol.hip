@@ -73,7 +73,7 @@ struct RcArgs {
     const int *sumh;          // device_reduce_i8(hs) per-phase tap sums
     const float *tabf;        // device_reduce_table(hs): [129][htaps] (edge operands, narrow images)
     const signed char *tabhf; // device_reduce_i8s_fold(hs, B): the COPY edge folded in
-    int centre;               // MIPX_REDUCE_CENTRE: centre sampling convention
+    int centre;               // centre sampling convention (mipx_set_reduce_sampling)
     int wst;                  // each wave's 16 rows x 16 UPW bytes go out as 16-byte row pieces
 };
 

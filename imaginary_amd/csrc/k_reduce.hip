@@ -332,6 +332,298 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
     }
 }
 
+// ===========================================================================
+// The same fused 2 x 2 reduce under libvips' centre sampling convention
+// (PARITY_ASSUMPTIONS.md row 1 flipped: X = (o + 0.5) * 2 - 0.5 = 2o + 0.5).
+//
+// Every output then sits at phase 64 (x = 0.5): tap i of the 13-point mask lies at
+// (i - 5.5) / 2, so taps 0..11 are the Lanczos lobe at +-0.25 .. +-2.75 and tap 12
+// (3.25) is zero.  The mask is symmetric about 5.5, so with t_k = matrixi[64][k]
+//     o = sum_{k=0..5} t_k * (p[2o - 5 + k] + p[2o + 6 - k])
+// (6 pair products, vs 4 at the corner convention's phase 0).  The host checks the
+// shape on the integer table before choosing the kernel.
+//  * Vertical: lane t owns dword t of the strip and keeps the 12 rows of the current
+//    window converted in a static register ring (slot = row mod 12; a 12-row chunk
+//    adds 24 rows = two ring periods, so the slots are compile-time constants).
+//  * Horizontal: an item reads the 2K + 10 intermediate pixels its K outputs need
+//    (14 dwords for both RGB and RGBA) and stores 12 / 8 contiguous bytes.
+// Same strip / band / LDS geometry as k_reduce2x2<B, 66>, so the demand-driven
+// windows of execute_plan round to the same tiles.
+// ===========================================================================
+template <int B>
+struct R2C {
+    static constexpr int kThreads = 256, kPitch = 288;
+    static constexpr int TW = B == 3 ? 160 : 120;      // = R2<B, 1>::TW
+    static constexpr int NPX = 2 * TW + 10;            // intermediate px 2x0-5 .. 2x0+2TW+4
+    static constexpr int K = B == 3 ? 4 : 2;
+    static constexpr int OFF0 = B == 3 ? 1 : 0;
+    static constexpr int ND = (B * NPX + OFF0 + 3) / 4;
+    static constexpr int WD = (B * (2 * K + 10) + OFF0 + 3) / 4;  // window dwords per item
+    static_assert(ND <= kThreads && ND <= kPitch, "strip too wide");
+    static_assert(WD == 14, "item window");
+    static_assert(TW == R2<B, 1>::TW, "same tiles as the corner kernel");
+};
+
+struct Reduce2cArgs {
+    const u8 *in;
+    u8 *out;
+    int w, h, ow, oh;
+    int n_strips, n_bands, band_rows;
+    int s_base, y_base, x_end, y_end;
+    long long in_img, out_img;
+    float t[6];   // matrixi[64][0..5] / 4096 (exact)
+    float bias;   // 2^-13: RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5)
+};
+
+// four byte columns as scalar floats: the centre kernel's multiply-adds stay plain
+// v_fma_f32 (packed v_pk_fma_f32 issued as many instructions but waited twice as
+// long on issue, PMC in profiles/r04)
+struct S4 {
+    float x, y, z, w;
+};
+__device__ __forceinline__ S4 cvt4s(uint32_t v) {
+    return S4{ubyte_once<0>(v), ubyte_once<1>(v), ubyte_once<2>(v), ubyte_once<3>(v)};
+}
+__device__ __forceinline__ S4 fma4(float t, const S4 &r, const S4 &acc) {
+    return S4{__builtin_fmaf(t, r.x, acc.x), __builtin_fmaf(t, r.y, acc.y), __builtin_fmaf(t, r.z, acc.z),
+              __builtin_fmaf(t, r.w, acc.w)};
+}
+__device__ __forceinline__ S4 add4(const S4 &a, const S4 &b) { return S4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+
+template <int B, bool RING>
+__device__ __forceinline__ void reduce2c_tile(const Reduce2cArgs &a, int img, int strip, int band, uint32_t *lds) {
+    using G = R2C<B>;
+    constexpr int kThreads = G::kThreads, kPitch = G::kPitch, TW = G::TW, K = G::K, R = kR;
+    const int tid = threadIdx.x;
+    const int x0 = (a.s_base + strip) * TW;
+    const int row_bytes = a.w * B;
+    const int px0 = 2 * x0 - 5;
+    const int base = (B * px0) & ~3;
+    const int byte0 = base + 4 * tid;
+    const bool vlane = tid < G::ND && byte0 >= 0 && byte0 + 4 <= row_bytes;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<u8 *>(a.in + img * a.in_img), 0, static_cast<int>(a.in_img), 0x00020000);
+    const uint32_t voff = vlane ? static_cast<uint32_t>(byte0) : 0x80000000u;
+    const int y0 = a.y_base + band * a.band_rows;  // a multiple of 12: 2 * y0 == 0 (mod 12)
+    const int y1 = min(y0 + a.band_rows, a.y_end);
+    const float t0 = a.t[0], t1 = a.t[1], t2 = a.t[2], t3 = a.t[3], t4 = a.t[4], t5 = a.t[5], bias = a.bias;
+    const int nl = px0 < 0 ? -px0 : 0;
+    const int x_last = min(x0 + TW, a.x_end) - 1;
+    const int fr = a.w - px0;
+    const int fr_end = min(2 * x_last + 6 - px0, G::NPX - 1);
+    const int nr = fr_end >= fr ? fr_end - fr + 1 : 0;
+    const bool edge = nl > 0 || nr > 0;
+
+    auto load_row = [&](int r) -> uint32_t {
+        r = clampi(r, 0, a.h - 1);
+        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * row_bytes, 0));
+    };
+
+    // RING: the 12 rows of the window converted in a register ring, 6 pair sums per
+    // output (slot s holds input row 2 * yc + d with d == s (mod 12)).
+    // Otherwise (default) the six open outputs' accumulators: a new row r adds t_k r to
+    // every output o with k = r - 2o + 5 in [0, 11] (slot = o mod 6): the same 12
+    // multiply-adds per output byte, half the registers (24 instead of 48)
+    constexpr int NS = RING ? 12 : 6;
+    S4 ring[NS];
+    const S4 BI = {bias, bias, bias, bias};
+    auto tap = [&](int k) -> float {  // t_k of the symmetric 12-tap mask
+        const int m = k < 6 ? k : 11 - k;
+        return m == 0 ? t0 : m == 1 ? t1 : m == 2 ? t2 : m == 3 ? t3 : m == 4 ? t4 : t5;
+    };
+    if (RING) {
+#pragma unroll
+        for (int d = -5; d <= 4; ++d) ring[(d + 12) % NS] = cvt4s(load_row(2 * y0 + d));
+    } else {
+        // outputs y0 .. y0 + 4 are open before the first step: rows 2 y0 - 5 .. 2 y0 + 4
+#pragma unroll
+        for (int j = 0; j < 5; ++j) ring[j] = BI;
+#pragma unroll
+        for (int d = -5; d <= 4; ++d) {
+            const S4 r = cvt4s(load_row(2 * y0 + d));
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int k = d - 2 * j + 5;
+                if (k >= 0 && k <= 11) {
+                    const float tk = tap(k);
+                    ring[j] = fma4(tk, r, ring[j]);
+                }
+            }
+        }
+    }
+    uint32_t nx[R], ny[R];  // rows 2o + 5 and 2o + 6 of output row o = yc + u
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        nx[u] = load_row(2 * (y0 + u) + 5);
+        ny[u] = load_row(2 * (y0 + u) + 6);
+    }
+    int buf = 0;
+    for (int yc = y0; yc < y1; yc += R, buf ^= 1) {
+        uint32_t *L = lds + buf * (R * kPitch);
+        const bool more = yc + R < y1;
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            uint32_t d;
+            if (RING) {
+                ring[(2 * u + 5) % 12] = cvt4s(nx[u]);
+                ring[(2 * u + 6) % 12] = cvt4s(ny[u]);
+                if (more) {
+                    nx[u] = load_row(2 * (yc + R + u) + 5);
+                    ny[u] = load_row(2 * (yc + R + u) + 6);
+                }
+                // pair k: rows 2o - 5 + k and 2o + 6 - k
+#define RC_LO(k) ring[(2 * u + 7 + (k)) % 12]
+#define RC_HI(k) ring[(2 * u + 6 - (k) + 12) % 12]
+                S4 acc = fma4(t5, add4(RC_LO(5), RC_HI(5)), BI);
+                acc = fma4(t4, add4(RC_LO(4), RC_HI(4)), acc);
+                acc = fma4(t3, add4(RC_LO(3), RC_HI(3)), acc);
+                acc = fma4(t2, add4(RC_LO(2), RC_HI(2)), acc);
+                acc = fma4(t1, add4(RC_LO(1), RC_HI(1)), acc);
+                acc = fma4(t0, add4(RC_LO(0), RC_HI(0)), acc);
+#undef RC_LO
+#undef RC_HI
+                d = pack4b(acc.x, acc.y, acc.z, acc.w);
+            } else {
+                // rows 2o + 5 (tap 10 - 2j of output o + j) and 2o + 6 (tap 11 - 2j);
+                // output o + 5 opens with tap 0, output o closes with tap 11
+                const S4 ra = cvt4s(nx[u]);
+                const S4 rb = cvt4s(ny[u]);
+                if (more) {
+                    nx[u] = load_row(2 * (yc + R + u) + 5);
+                    ny[u] = load_row(2 * (yc + R + u) + 6);
+                }
+                ring[(u + 5) % 6] = fma4(t0, ra, BI);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const float tk = tap(10 - 2 * j);
+                    ring[(u + j) % 6] = fma4(tk, ra, ring[(u + j) % 6]);
+                }
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const float tk = tap(11 - 2 * j);
+                    ring[(u + j) % 6] = fma4(tk, rb, ring[(u + j) % 6]);
+                }
+                const S4 acc = ring[u % 6];
+                d = pack4b(acc.x, acc.y, acc.z, acc.w);
+            }
+            if (tid < G::ND) L[u * kPitch + tid] = d;
+        }
+        if (edge) {  // EXTEND_COPY inside the LDS image
+            __syncthreads();
+            u8 *Lb = reinterpret_cast<u8 *>(L);
+            const int nfill = nl + nr;
+            for (int i = tid; i < R * nfill * B; i += kThreads) {
+                const int u = i / (nfill * B);
+                const int rem = i - u * nfill * B;
+                const int f = rem / B, c = rem - f * B;
+                const int dst = f < nl ? f : fr + (f - nl);
+                const int srcp = f < nl ? nl : fr - 1;
+                Lb[u * kPitch * 4 + B * dst + G::OFF0 + c] = Lb[u * kPitch * 4 + B * srcp + G::OFF0 + c];
+            }
+        }
+        __syncthreads();
+        constexpr int items_per_row = TW / K;
+        for (int it = tid; it < R * items_per_row; it += kThreads) {
+            const int u = it / items_per_row;
+            const int j = it - u * items_per_row;
+            const int x = x0 + K * j;
+            const int y = yc + u;
+            if (y >= a.y_end || x >= a.x_end) continue;
+            const uint32_t *row = L + u * kPitch;
+            constexpr int W0 = (B * 2 * K) / 4;
+            uint32_t win[14];
+            if (B == 3) {
+                const uint2 *r2 = reinterpret_cast<const uint2 *>(row + W0 * j);
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    const uint2 dd = r2[q];
+                    win[2 * q] = dd.x;
+                    win[2 * q + 1] = dd.y;
+                }
+            } else {
+                const uint4 *r4 = reinterpret_cast<const uint4 *>(row + W0 * j);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const uint4 dd = r4[q];
+                    win[4 * q] = dd.x, win[4 * q + 1] = dd.y, win[4 * q + 2] = dd.z, win[4 * q + 3] = dd.w;
+                }
+                const uint2 dd = *reinterpret_cast<const uint2 *>(row + W0 * j + 12);
+                win[12] = dd.x;
+                win[13] = dd.y;
+            }
+            // push form: window pixel t (intermediate pixel 2x - 5 + t) feeds output k with
+            // tap t - 2k, so a pixel is converted once, each output byte takes 12
+            // multiply-adds, and only the K x B accumulators stay live
+            auto pxf = [&](int t, int c) -> float {
+                const int lb = B * t + c + G::OFF0;
+                const uint32_t dd = win[lb >> 2];
+                switch (lb & 3) {
+                    case 0: return ubyte_once<0>(dd);
+                    case 1: return ubyte_once<1>(dd);
+                    case 2: return ubyte_once<2>(dd);
+                    default: return ubyte_once<3>(dd);
+                }
+            };
+            float acc[K][B];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int c = 0; c < B; ++c) acc[k][c] = bias;
+#pragma unroll
+            for (int t = 0; t < 2 * K + 10; ++t) {
+                float v[B];
+#pragma unroll
+                for (int c = 0; c < B; ++c) v[c] = pxf(t, c);
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int kk = t - 2 * k;
+                    if (kk < 0 || kk > 11) continue;
+                    const float tk = tap(kk);
+#pragma unroll
+                    for (int c = 0; c < B; ++c) acc[k][c] = __builtin_fmaf(tk, v[c], acc[k][c]);
+                }
+            }
+            const float (&o)[K][B] = acc;
+            u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
+            const bool full = x + K <= a.ow;
+            if (B == 3) {
+                const uint32_t d0 = pack4b(o[0][0], o[0][1], o[0][2], o[1][0]);
+                const uint32_t d1 = pack4b(o[1][1], o[1][2], o[2][0], o[2][1]);
+                const uint32_t d2 = pack4b(o[2][2], o[3][0], o[3][1], o[3][2]);
+                if (full && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
+                    *reinterpret_cast<uint3 *>(q) = uint3{d0, d1, d2};
+                } else {
+                    const uint32_t dd[3] = {d0, d1, d2};
+                    const int nb = (full ? K : a.ow - x) * B;
+                    for (int i = 0; i < nb; ++i) q[i] = static_cast<u8>(dd[i >> 2] >> (8 * (i & 3)));
+                }
+            } else {
+                const uint32_t d0 = pack4b(o[0][0], o[0][1], o[0][2], o[0][3]);
+                const uint32_t d1 = pack4b(o[1][0], o[1][1], o[1][2], o[1][3]);
+                uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
+                if (full && (reinterpret_cast<uintptr_t>(q) & 7u) == 0) {
+                    *reinterpret_cast<uint2 *>(q) = uint2{d0, d1};
+                } else {
+                    q32[0] = d0;
+                    if (full) q32[1] = d1;
+                }
+            }
+        }
+    }
+}
+
+// W5: ask for 5 waves per SIMD (96 VGPRs; RGB then spills 16 bytes per lane)
+template <int B, bool RING, int W5>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W5 ? 5 : 1, 8))) k_reduce2c(Reduce2cArgs a) {
+    __shared__ uint32_t lds[2 * kR * R2C<B>::kPitch];
+    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int strip = t % a.n_strips;
+    const int rest = t / a.n_strips;
+    const int band = rest % a.n_bands;
+    const int img = rest / a.n_bands;
+    reduce2c_tile<B, RING>(a, img, strip, band, lds);
+}
+
 // Variant bits (A/B in one process via MIPX_R2_VARIANT; default = best measured):
 // bit 0: R = 6 (else 12), bit 1: register prefetch of the next chunk,
 // bit 2: packed-FP32 vertical taps, bit 3: memory-only diagnostic (not exact),
@@ -488,16 +780,83 @@ bool reduce2_taps(float c[4]) {
     return true;
 }
 
+// The centre convention's phase-64 mask: 12 non-zero taps symmetric about 5.5 and a
+// zero tap 12 (k_reduce2c).  Returns t_0..t_5.
+bool reduce2c_taps(float t[6]) {
+    std::vector<int> tab;
+    reduce_table(2.0, tab);
+    const int n = reduce_points(2.0);
+    if (n != 13) return false;
+    const int *r = tab.data() + 64 * n;
+    if (r[12] != 0) return false;
+    for (int i = 0; i < 6; ++i) {
+        if (r[i] != r[11 - i]) return false;
+        t[i] = static_cast<float>(r[i]);
+    }
+    return true;
+}
+
 // Fused path applies to shrink exactly 2 x 2 on 3- or 4-band images whose rows
-// are dword aligned.
+// are dword aligned: k_reduce2x2 at the corner convention, k_reduce2c at the centre one.
 bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
     if (hs != 2.0 || vs != 2.0) return false;
-    if (reduce_centre()) return false;  // centre convention: every output at phase 64, no 7-tap form
     if (b != 3 && b != 4) return false;
     if ((w * b) % 4 != 0 || (reinterpret_cast<uintptr_t>(in) % 4) != 0) return false;
     if (w < 8 || h < 8) return false;
+    if (reduce_centre()) {
+        static const bool centre_ok = [] { float t[6]; return reduce2c_taps(t); }();
+        return centre_ok;
+    }
     static const bool shape_ok = [] { float c[4]; return reduce2_taps(c); }();
     return shape_ok;
+}
+
+// k_reduce2c over the output region [x0, x1) x [y0, y1) (same tiles as k_reduce2x2<B, 66>)
+static int reduce2c_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x0, int y0, int x1, int y1,
+                                  hipStream_t st) {
+    Reduce2cArgs a{};
+    if (!reduce2c_taps(a.t)) return MIPX_EINVAL;
+    for (float &t : a.t) t /= 4096.0f;
+    a.bias = 1.0f / 8192.0f;
+    a.in = in;
+    a.out = out;
+    a.w = w;
+    a.h = h;
+    a.ow = out_size_reduce(w, 2.0);
+    a.oh = out_size_reduce(h, 2.0);
+    if (x0 < 0 || y0 < 0 || x1 > a.ow || y1 > a.oh || x0 >= x1 || y0 >= y1) return MIPX_EINVAL;
+    const int tw = b == 3 ? R2C<3>::TW : R2C<4>::TW;
+    a.s_base = x0 / tw;
+    a.x_end = x1;
+    a.y_base = y0 / kR * kR;
+    a.y_end = y1;
+    a.n_strips = (x1 + tw - 1) / tw - a.s_base;
+    const int chunks = (y1 - a.y_base + kR - 1) / kR;
+    const char *eb = tune_env("MIPX_R2C_BAND");  // 12-row chunks per band (A/B)
+    const int cpb = (eb && *eb) ? std::max(1, std::atoi(eb)) : 2;
+    a.band_rows = std::max(1, std::min(chunks, cpb)) * kR;
+    a.n_bands = (y1 - a.y_base + a.band_rows - 1) / a.band_rows;
+    a.in_img = img_bytes(w, h, b);
+    a.out_img = img_bytes(a.ow, a.oh, b);
+    const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
+    if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
+    const char *ep = tune_env("MIPX_R2C_RING");  // A/B: the 12-row pair ring instead of accumulators
+    const bool ring = ep && *ep == '1';
+    const char *ew = tune_env("MIPX_R2C_W5");    // A/B: 5 waves per SIMD
+    const bool w5 = ew && *ew == '1';
+    const dim3 grid(static_cast<unsigned>(tiles)), blk(256);
+#define MIPX_R2C(BB, RR, WW) hipLaunchKernelGGL((k_reduce2c<BB, RR, WW>), grid, blk, 0, st, a)
+    if (b == 3) {
+        if (ring) MIPX_R2C(3, true, 0);
+        else if (w5) MIPX_R2C(3, false, 1);
+        else MIPX_R2C(3, false, 0);
+    } else {
+        if (ring) MIPX_R2C(4, true, 0);
+        else if (w5) MIPX_R2C(4, false, 1);
+        else MIPX_R2C(4, false, 0);
+    }
+#undef MIPX_R2C
+    return launch_check("k_reduce2c");
 }
 
 // k_reduce2x2 build variant.  Only the shipped one (66) is compiled now; the r01 / r02
@@ -523,6 +882,7 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
 // Every computed pixel is the same sum as in the full launch.
 int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x0, int y0, int x1, int y1,
                           hipStream_t st) {
+    if (reduce_centre()) return reduce2c_window_launch(in, out, n, w, h, b, x0, y0, x1, y1, st);
     float c[4];
     if (!reduce2_taps(c)) return MIPX_EINVAL;
     Reduce2Args a{};

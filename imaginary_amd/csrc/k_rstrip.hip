@@ -75,7 +75,7 @@ struct RsArgs {
     int tv, th, padv, padh;
     int tpav, tpah;              // pair-table width (taps / 2 + 1)
     double vs, hs;
-    int centre;                  // MIPX_REDUCE_CENTRE
+    int centre;                  // centre sampling convention (mipx_set_reduce_sampling)
     const uint32_t *vpairs, *hpairs;  // [129][2][tpa] int16 tap pairs
     int diag;                    // A/B diagnostic (MIPX_RSTRIP_DIAG): 1 skip vertical, 2 skip horizontal
 };

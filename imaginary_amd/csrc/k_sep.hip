@@ -41,7 +41,7 @@ struct SepTaps {
     float rounding, inv_scale;  // conv rounding
     int dot;                 // integer dot paths (MIPX_SEP_DOT=0 selects the float path)
     int tq;                  // conv vpass: rows transposed once per 4-row quad (MIPX_SEP_TQ=0: per output row)
-    int centre;              // reduce: centre sampling convention (MIPX_REDUCE_CENTRE=1)
+    int centre;              // reduce: centre sampling convention (mipx_set_reduce_sampling)
 };
 
 constexpr int kVpPairs = 8;     // tap pairs of the unrolled vertical reduce (taps <= 16: shrink < 2.75)

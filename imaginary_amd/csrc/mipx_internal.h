@@ -26,8 +26,9 @@ int hip_fail(hipError_t e, const char *what);  // records detail, returns MIPX_E
 // mipx_tuning_reload): nullptr when unset.  Launchers call this, never getenv.
 const char *tune_env(const char *name);
 void tune_reload();
-// MIPX_REDUCE_CENTRE=1: every Lanczos reduce samples output o at (o + 0.5) * shrink - 0.5
-// (libvips' centre convention) instead of o * shrink (PARITY_ASSUMPTIONS.md row 1)
+// mipx_set_reduce_sampling(MIPX_SAMPLE_CENTRE): every Lanczos reduce samples output o at
+// (o + 0.5) * shrink - 0.5 (libvips' centre convention) instead of o * shrink
+// (PARITY_ASSUMPTIONS.md row 1)
 bool reduce_centre();
 inline double reduce_x_host(int o, double s, bool centre) { return centre ? (o + 0.5) * s - 0.5 : o * s; }
 

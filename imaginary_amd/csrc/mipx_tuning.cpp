@@ -1,4 +1,5 @@
-// mipx_tuning.cpp — kernel-selection knobs (MIPX_* environment variables) read once.
+// mipx_tuning.cpp — kernel-selection knobs (MIPX_* environment variables) read once,
+// and the parity settings (mipx_set_reduce_sampling).
 //
 // The launchers pick kernels and layouts by geometry; a few MIPX_* variables force
 // an alternative for A/B runs and tests (e.g. MIPX_RCOL=0).  They are snapshotted
@@ -57,10 +58,11 @@ const char *tune_env(const char *name) {
     return it == s->kv.end() ? nullptr : it->second.c_str();
 }
 
-bool reduce_centre() {
-    const char *e = tune_env("MIPX_REDUCE_CENTRE");
-    return e && *e == '1';
-}
+namespace {
+std::atomic<int> g_sampling{MIPX_SAMPLE_CORNER};  // PARITY_ASSUMPTIONS.md row 1
+}  // namespace
+
+bool reduce_centre() { return g_sampling.load(std::memory_order_relaxed) == MIPX_SAMPLE_CENTRE; }
 
 void tune_reload() {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -68,6 +70,14 @@ void tune_reload() {
 }
 
 }  // namespace mipx
+
+extern "C" int mipx_set_reduce_sampling(int32_t convention) {
+    if (convention != MIPX_SAMPLE_CORNER && convention != MIPX_SAMPLE_CENTRE) return MIPX_EINVAL;
+    mipx::g_sampling.store(convention, std::memory_order_relaxed);
+    return MIPX_OK;
+}
+
+extern "C" int mipx_reduce_sampling(void) { return mipx::g_sampling.load(std::memory_order_relaxed); }
 
 extern "C" int mipx_tuning_reload(void) {
     mipx::tune_reload();

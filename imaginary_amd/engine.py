@@ -14,7 +14,20 @@ from ._abi import (MipxCfg, MipxImg, MipxInput, MipxOpts, MipxPlan, check, lib, 
                    EXTEND, GRAVITY, TYPES, sync_tuning)
 
 __all__ = ["DeviceBuffer", "make_opts", "make_input", "plan_make", "fit_dimension", "Engine",
-           "run_op", "execute", "device_count", "synchronize"]
+           "run_op", "execute", "device_count", "synchronize", "set_reduce_sampling", "reduce_sampling"]
+
+SAMPLING = {"corner": 0, "centre": 1}
+
+
+def set_reduce_sampling(convention: str) -> None:
+    """libvips' Lanczos3 reduce sampling convention, PARITY_ASSUMPTIONS.md row 1:
+    "corner" (X = o * shrink) or "centre" (X = (o + 0.5) * shrink - 0.5).  Set it
+    while no work is in flight (mipx_set_reduce_sampling)."""
+    check(lib.mipx_set_reduce_sampling(SAMPLING[convention]), "mipx_set_reduce_sampling")
+
+
+def reduce_sampling() -> str:
+    return {v: k for k, v in SAMPLING.items()}[lib.mipx_reduce_sampling()]
 
 
 def device_count() -> int:
@@ -128,11 +141,20 @@ class Engine:
         sync_tuning()
         check(lib.mipx_init(C.byref(cfg)), "mipx_init")
 
+    @classmethod
+    def attach(cls) -> "Engine":
+        """A handle on the engine already running in this process (started by another
+        Engine, with whatever configuration it chose); mipx_init is not called."""
+        if lib.mipx_queue_count() <= 0:
+            raise MipxError(-7, "Engine.attach: no engine running")
+        return cls.__new__(cls)
+
     def submit(self, plan: MipxPlan, img: np.ndarray, wm: Optional[np.ndarray] = None, device: int = -1,
                out: Optional[np.ndarray] = None):
         """Queue one request; returns (ticket, out).  `out` (optional) receives the
-        result: contiguous uint8 of the plan's output shape."""
-        sync_tuning()
+        result: contiguous uint8 of the plan's output shape.  The MIPX_* kernel knobs are
+        re-read in Engine(), run_op and execute, not per request: a reload
+        must not race the queue workers' launches."""
         if not (img.dtype == np.uint8 and img.ndim == 3 and img.strides[2] == 1
                 and img.strides[1] == img.shape[2]):
             img = np.ascontiguousarray(img, dtype=np.uint8)  # rows may keep a wider stride

@@ -232,11 +232,15 @@ _ENGINE: Optional[Engine] = None
 
 
 def engine() -> Engine:
-    """The process-wide request engine (mipx_init is idempotent, so this also
-    re-initialises after an mipx_shutdown)."""
+    """The process-wide request engine.  An engine already running in this process is
+    used as it is, whoever started it and with whatever configuration (mipx_init
+    refuses a second, different configuration, so this never calls it then); after an
+    mipx_shutdown, or before any engine, a default one is started."""
     global _ENGINE
-    if _ENGINE is not None and _abi.lib.mipx_queue_count() > 0:
-        return _ENGINE  # still up (possibly started by another Engine with its own config)
+    if _abi.lib.mipx_queue_count() > 0:
+        if _ENGINE is None:
+            _ENGINE = Engine.attach()
+        return _ENGINE
     _ENGINE = Engine()
     return _ENGINE
 

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MIPX_ABI_VERSION 4
+#define MIPX_ABI_VERSION 5
 
 /* ---- error codes ---- */
 #define MIPX_OK 0
@@ -248,10 +248,24 @@ int mipx_op_smartcrop_origin(const uint8_t *d_in, int32_t *d_origins, int32_t n,
 size_t mipx_op_workspace_bytes(int32_t op, int32_t n, int32_t w, int32_t h, int32_t bands,
                                double p0, double p1);
 
+/* ---- parity settings (PARITY_ASSUMPTIONS.md) ----
+ * The sampling convention of libvips' Lanczos3 reduce (reducev.cpp / reduceh.cpp;
+ * PARITY_ASSUMPTIONS.md row 1): MIPX_SAMPLE_CORNER, output o samples X = o * shrink,
+ * or MIPX_SAMPLE_CENTRE, X = (o + 0.5) * shrink - 0.5.  Process-wide, read by every
+ * reduce kernel and by the demand-driven region walk; output sizes (the planner) do
+ * not depend on it.  Set it before the first request or between launches, never while
+ * work is in flight.  MIPX_EINVAL for any other value. */
+#define MIPX_SAMPLE_CORNER 0
+#define MIPX_SAMPLE_CENTRE 1
+int mipx_set_reduce_sampling(int32_t convention);
+int mipx_reduce_sampling(void);
+
 /* ---- engine tuning (tests and benchmarks) ----
  * Kernel-selection knobs (MIPX_* environment variables, e.g. MIPX_RCOL=0 for the
- * previous generic reduce) are read once, on first use.  mipx_tuning_reload()
- * re-reads them; call it only between launches (A/B scripts, tests). */
+ * previous generic reduce) are read once, on first use.  Every knob only chooses
+ * among kernels that give identical bytes; none changes a result.
+ * mipx_tuning_reload() re-reads them; call it only between launches (A/B scripts,
+ * tests). */
 int mipx_tuning_reload(void);
 
 /* ---- device memory helpers (so a binding needs no other HIP wrapper) ---- */

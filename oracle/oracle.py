@@ -301,3 +301,7 @@ def reduce_fast_batch(imgs, hshrink, vshrink, threads):
 
 def set_switch(name: str, value: int):
     lib().ref_set_switch(name.encode(), int(value))
+
+
+def get_switch(name: str) -> int:
+    return int(lib().ref_get_switch(name.encode()))

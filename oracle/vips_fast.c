@@ -14,9 +14,10 @@
  *  - OpenMP across images (each image single-threaded, as libvips' per-request
  *    concurrency 1 in imaginary), compiled -O3 for x86-64-v3 (AVX2).
  *
- * It shares the coefficient table with the oracle (ref_reduce_table) and only
- * the default parity switches; tests/test_oracle.py checks it is byte-identical
- * to ref_reduce on random and edge-case inputs.
+ * It shares the coefficient table with the oracle (ref_reduce_table), both
+ * settings of the reduce_centre switch and the defaults of the others;
+ * tests/test_oracle.py checks it is byte-identical to ref_reduce on random and
+ * edge-case inputs under both sampling conventions.
  */
 #include <math.h>
 #include <stdlib.h>
@@ -30,13 +31,18 @@ static inline int clampi_f(int v, int lo, int hi) { return v < lo ? lo : (v > hi
 static inline int vround(double v) { return (int)floor(v + 0.5); }
 static inline int phase_of(double X) { return (((int)(X * TRANSFORM_SCALE * 2) & (TRANSFORM_SCALE * 2 - 1)) + 1) >> 1; }
 static inline unsigned char rnd12(int s) { return (unsigned char)clampi_f((s + 2048) >> 12, 0, 255); }
+/* sample position: the corner convention o * s, or with the reduce_centre switch
+ * (o + 0.5) * s - 0.5, as vips_ref.c reduce_pos */
+static inline double pos_of(int o, double s) {
+    return ref_get_switch("reduce_centre") ? (o + 0.5) * s - 0.5 : o * s;
+}
 
 static int reducev_fast(const unsigned char *in, int w, int h, int b, unsigned char *out, int oh, double vs,
                         const int *tab, int n, int *acc) {
     const int pad = n / 2 - 1;
     const size_t ne = (size_t)w * b;
     for (int y = 0; y < oh; y++) {
-        const double Y = y * vs;
+        const double Y = pos_of(y, vs);
         const int iy = (int)Y;
         const int *c = tab + phase_of(Y) * n;
         memset(acc, 0, ne * sizeof(int));
@@ -56,7 +62,7 @@ static int reduceh_fast(const unsigned char *in, int w, int h, int b, unsigned c
                         const int *tab, int n, int *cols, const int **coef) {
     const int pad = n / 2 - 1;
     for (int x = 0; x < ow; x++) {  /* per output column: first tap and mask, once */
-        const double X = x * hs;
+        const double X = pos_of(x, hs);
         cols[x] = (int)X - pad;
         coef[x] = tab + phase_of(X) * n;
     }
@@ -112,8 +118,7 @@ static int plan_fast(fast_plan *p, int w, int h, double hs, double vs) {
 }
 
 static int defaults_only(void) {
-    return !(ref_get_switch("reduce_hfirst") || ref_get_switch("reduce_centre") ||
-             ref_get_switch("reduce_round_coeff"));
+    return !(ref_get_switch("reduce_hfirst") || ref_get_switch("reduce_round_coeff"));
 }
 
 int ref_reduce_fast(const ref_img *in, ref_img *out, double hshrink, double vshrink) {

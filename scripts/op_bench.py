@@ -38,9 +38,13 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--ab", default="", help="KNOB=v1,v2,...: same-process A/B of a MIPX_* knob")
     ap.add_argument("--warm-ms", type=float, default=200.0, help="device-time warm-up; 0: none, one group (PMC runs)")
+    ap.add_argument("--sampling", choices=["corner", "centre"], default=None,
+                    help="reduce sampling convention (mipx_set_reduce_sampling); default: the library's")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     check(lib.mipx_set_device(0))
+    if a.sampling:
+        check(lib.mipx_set_reduce_sampling({"corner": 0, "centre": 1}[a.sampling]))
     w, h, b, n = a.w, a.h, a.b, a.n
     s2 = a.s2 or a.s
     if a.op in ("reduce", "reducev", "reduceh"):
@@ -118,7 +122,8 @@ def main():
         return sorted(groups)[len(groups) // 2]
 
     alg = n * (w * h * b + ow * oh * b)
-    line = {"op": a.op, "w": w, "h": h, "b": b, "n": n, "s": a.s, "s2": s2, "out": [ow, oh]}
+    line = {"op": a.op, "w": w, "h": h, "b": b, "n": n, "s": a.s, "s2": s2, "out": [ow, oh],
+            "sampling": ["corner", "centre"][lib.mipx_reduce_sampling()]}
     if not a.ab:
         ms = measure()
         print(json.dumps({**line, "ms": round(ms, 4), "alg_GBps": round(alg / ms / 1e6, 1)}))

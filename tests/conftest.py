@@ -32,6 +32,19 @@ def gpu():
     return ia
 
 
+@pytest.fixture(params=["corner", "centre"])
+def convention(request, oracle, gpu):
+    """Both settings of PARITY_ASSUMPTIONS.md row 1 (libvips reduce sampling: X = o * s
+    or X = (o + 0.5) * s - 0.5), in the engine (mipx_set_reduce_sampling) and in the
+    oracle; the defaults come back afterwards."""
+    prev_engine, prev_oracle = gpu.reduce_sampling(), oracle.get_switch("reduce_centre")
+    gpu.set_reduce_sampling(request.param)
+    oracle.set_switch("reduce_centre", int(request.param == "centre"))
+    yield request.param
+    gpu.set_reduce_sampling(prev_engine)
+    oracle.set_switch("reduce_centre", prev_oracle)
+
+
 @pytest.fixture
 def rng():
     return np.random.default_rng(20241220)

@@ -33,7 +33,7 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_version_and_errors_without_gpu():
     import imaginary_amd as ia
-    assert ia.lib.mipx_abi_version() == 4
+    assert ia.lib.mipx_abi_version() == 5
     assert b"gfx950" in ia.lib.mipx_version()
     assert ia.lib.mipx_strerror(-2).startswith(b"operation not supported")
 

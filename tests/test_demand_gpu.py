@@ -9,7 +9,8 @@ import pytest
 
 import imaginary_amd as ia
 
-pytestmark = pytest.mark.gpu
+# every case under both reduce sampling conventions (the centre one runs k_reduce2c)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("convention")]
 
 
 def _chain(oracle, w, h, b, stages):

@@ -54,6 +54,10 @@ def test_reduce_table_shrink2_known_answer(oracle):
     assert np.array_equal(load_golden("tables.npz")["reduce_2_0"], t)
     # every phase stays normalised within truncation error
     assert np.all(np.abs(t.sum(1) - 4096) <= 13)
+    # phase 64 (x = 0.5): every output of a shrink-2 reduce under the centre sampling
+    # convention; 12 non-zero taps symmetric about 5.5, tap 12 (at 3.25) zero
+    assert t[64].tolist() == [15, 61, -139, -272, 555, 1828, 1828, 555, -272, -139, 61, 15, 0]
+    assert t[64].sum() == 4096
 
 
 @pytest.mark.parametrize("s,n", [(1.6, 11), (2.0, 13), (2.4666, 15), (1.3333, 9), (8.0, 49)])
@@ -127,9 +131,20 @@ def test_cpu_baseline_batch_matches_single(oracle, rng):
 @pytest.mark.parametrize("h,w,b,hs,vs", [(216, 384, 3, 2.0, 2.0), (270, 480, 3, 1.6, 1.5976331360946747),
                                          (101, 131, 4, 4 / 3, 4 / 3), (37, 53, 1, 2.4, 1.0), (29, 31, 2, 1.0, 1.7),
                                          (9, 7, 3, 3.7, 2.9), (64, 300, 4, 14.2, 1.3)])
-def test_fast_cpu_baseline_is_the_oracle(oracle, h, w, b, hs, vs):
+@pytest.mark.parametrize("centre", [0, 1])
+def test_fast_cpu_baseline_is_the_oracle(oracle, h, w, b, hs, vs, centre):
     """bench.py times vips_fast.c as the CPU baseline; it must compute exactly the
-    oracle's reduce (interior, clamped edges, one-axis and tiny images)."""
+    oracle's reduce (interior, clamped edges, one-axis and tiny images) under both
+    sampling conventions (PARITY_ASSUMPTIONS.md row 1)."""
+    prev = oracle.get_switch("reduce_centre")
+    oracle.set_switch("reduce_centre", centre)
+    try:
+        _fast_vs_oracle(oracle, h, w, b, hs, vs)
+    finally:
+        oracle.set_switch("reduce_centre", prev)
+
+
+def _fast_vs_oracle(oracle, h, w, b, hs, vs):
     rng = np.random.default_rng(h * w + b)
     img = rng.integers(0, 256, (h, w, b), dtype=np.uint8)
     assert np.array_equal(oracle.reduce_fast(img, hs, vs), oracle.reduce(img, hs, vs))

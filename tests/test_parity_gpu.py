@@ -49,7 +49,7 @@ REDUCE_CASES = [
 
 
 @pytest.mark.parametrize("h,w,b,hs,vs", REDUCE_CASES)
-def test_reduce_matches_oracle(gpu, oracle, rng, h, w, b, hs, vs):
+def test_reduce_matches_oracle(gpu, oracle, rng, convention, h, w, b, hs, vs):
     imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
     got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
     for i in range(len(imgs)):
@@ -70,19 +70,23 @@ def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
 
 
-@pytest.mark.parametrize("var", [66])
-def test_reduce2x2_variants_exact(gpu, oracle, rng, var, monkeypatch):
-    """The fused 2x2 kernel (the shipped build, variant 66; the r01/r02 A/B builds
-    are recorded under profiles/ and no longer compiled) is bit-exact, including
-    strips that end at the image edge."""
-    monkeypatch.setenv("MIPX_R2_VARIANT", str(var))
-    for h, w, b in ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1001 * 4 // 4 - 1, 4), (200, 646, 3)):
+@pytest.mark.parametrize("var", ["acc", "ring", "w5"])
+def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, var, monkeypatch):
+    """The fused 2x2 kernels (corner: k_reduce2x2 variant 66, the r01/r02 A/B builds
+    are recorded under profiles/ and no longer compiled; centre: k_reduce2c with
+    open accumulators, the 12-row pair ring (MIPX_R2C_RING), 5 waves per SIMD (MIPX_R2C_W5))
+    are bit-exact, including strips that end at the image edge, images shorter than a band
+    and the smallest eligible sizes."""
+    monkeypatch.setenv("MIPX_R2C_RING", "1" if var == "ring" else "0")
+    monkeypatch.setenv("MIPX_R2C_W5", "1" if var == "w5" else "0")
+    for h, w, b in ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1001 * 4 // 4 - 1, 4), (200, 646, 3),
+                    (8, 8, 4), (9, 12, 3), (25, 164, 3), (131, 1000, 4), (1081, 324, 3), (16, 3840, 3)):
         if (w * b) % 4:
             continue
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
         got = gpu.run_op("reduce", imgs, hshrink=2.0, vshrink=2.0)
         for i in range(2):
-            assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"var {var} {h}x{w}x{b} img{i}")
+            assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"{convention} {var} {h}x{w}x{b} img{i}")
 
 
 @pytest.mark.parametrize("fused", ["0", "1"])
@@ -125,7 +129,7 @@ def test_reduce_extremes(gpu, oracle):
 
 
 @pytest.mark.slow
-def test_reduce_4k_to_1080p_full_size(gpu, oracle, rng):
+def test_reduce_4k_to_1080p_full_size(gpu, oracle, rng, convention):
     """BASELINE C2 geometry at full size (3840x2160x3 -> 1920x1080x3), bit-exact."""
     imgs = np.stack([rand_img(rng, 2160, 3840, 3), smooth_img(rng, 2160, 3840, 3)])
     got = gpu.run_op("reduce", imgs, hshrink=2.0, vshrink=2.0)

@@ -93,18 +93,20 @@ def test_unaligned_rows_probe_fallback(gpu, oracle, rng, monkeypatch, probe):
 
 
 @pytest.fixture
-def centre(oracle, monkeypatch):
-    """PARITY_ASSUMPTIONS.md row 1 flipped: libvips' centre sampling convention
-    (X = (o + 0.5) * shrink - 0.5) in the engine (MIPX_REDUCE_CENTRE=1) and the oracle."""
-    monkeypatch.setenv("MIPX_REDUCE_CENTRE", "1")
+def centre(oracle, gpu):
+    """libvips' centre sampling convention (X = (o + 0.5) * shrink - 0.5, PARITY_ASSUMPTIONS.md
+    row 1) in the engine (mipx_set_reduce_sampling) and the oracle."""
+    prev_engine, prev_oracle = gpu.reduce_sampling(), oracle.get_switch("reduce_centre")
+    gpu.set_reduce_sampling("centre")
     oracle.set_switch("reduce_centre", 1)
     yield
-    oracle.set_switch("reduce_centre", 0)
+    gpu.set_reduce_sampling(prev_engine)
+    oracle.set_switch("reduce_centre", prev_oracle)
 
 
 def test_reduce_centre_c2_c1_shapes(gpu, oracle, rng, centre):
-    """C2 (4K RGB -> 1080p, shrink 2: the fused 2x2 kernel steps aside, every output sits
-    at phase 64) and C1's 480x270 -> 300x169, plus the kernels behind k_rcol (unaligned
+    """C2 (4K RGB -> 1080p, shrink 2: every output sits at phase 64, k_reduce2c) and
+    C1's 480x270 -> 300x169, plus the kernels behind k_rcol (unaligned
     rows: k_rmf2; one axis: the separable passes) and a windowed plan."""
     for h, w, b, hs, vs in ((2160, 3840, 3, 2.0, 2.0), (270, 480, 3, 1.6, 1.5976331360946747),
                             (375, 500, 3, 1.46484375, 1.46484375), (301, 1333, 3, 1.6666666666666667, 1.6666666666666667),
