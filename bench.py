@@ -10,8 +10,8 @@ collective on the data path ("scaling": "weak").  torch is plumbing only:
 device memory, the stream, and a gloo barrier / max-reduce for the timing.
 
 A step = one mipx_execute_dev() of the bimg plan for /resize?width=1920&height=1080
-on a 3840x2160x3 decoded image (one Lanczos3 reduce 2x2, the fused k_reduce2x2
-kernel) over the whole resident batch.
+on a 3840x2160x3 decoded image (one Lanczos3 reduce 2x2: the fused k_reduce2x2 at the
+corner sampling convention, k_reduce2c at the centre one) over the whole resident batch.
 """
 import argparse
 import json
@@ -32,9 +32,9 @@ W_OUT, H_OUT = 1920, 1080
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-# MIPX_REDUCE_CENTRE=1: libvips' centre sampling convention (PARITY_ASSUMPTIONS.md row 1), checked
-# against the oracle under the same switch
-CENTRE = os.environ.get("MIPX_REDUCE_CENTRE") == "1"
+# the kernel C2 runs under each reduce sampling convention (PARITY_ASSUMPTIONS.md row 1):
+# its roofline and PMC traffic record are this kernel's
+C2_KERNEL = {"corner": "k_reduce2x2<3, 66>", "centre": "k_reduce2c<3, false, 0>"}
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--c1-seconds", type=float, default=4.0, help="C1 CPU reference: seconds of timing")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--sampling", choices=["corner", "centre"], default=None,
+                    help="libvips reduce sampling convention (PARITY_ASSUMPTIONS.md row 1); default: the library's")
     return ap.parse_args()
 
 
@@ -143,24 +145,27 @@ def c1_cpu_reference(args):
                      "end to end over HTTP on an i7 with libvips 7.42 (operation not stated)"}
 
 
-# the newest committed PMC traffic record of the C2 kernel (profiles/<round>/traffic_*.json)
-TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", "r03", "traffic_r03.json"),
+# the newest committed PMC traffic record of the C2 kernel (profiles/<round>/traffic_*.json:
+# one record, or {"records": [...]}, each naming its kernel)
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", "r04", "traffic_r04.json"),
+                 os.path.join(ROOT, "profiles", "r03", "traffic_r03.json"),
                  os.path.join(ROOT, "profiles", "r02", "traffic_r02.json"),
                  os.path.join(ROOT, "profiles", "r01", "traffic_v17.json")]
 
 
-def pmc_traffic(kernel_name_hint):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes of this kernel
-    (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections calibrated in
-    profiles/r01/calib_*.csv); None when no matching summary exists."""
+def pmc_traffic(kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes of exactly this
+    kernel (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections calibrated in
+    profiles/r01/calib_*.csv); None when no record names it."""
     for path in TRAFFIC_JSONS:
         try:
             with open(path) as f:
                 t = json.load(f)
         except OSError:
             continue
-        if t.get("kernel") == kernel_name_hint:
-            return t["traffic_bytes"], os.path.relpath(path, ROOT)
+        for rec in t.get("records", [t]):
+            if rec.get("kernel") == kernel:
+                return rec["traffic_bytes"], os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -208,6 +213,10 @@ def main():
     from imaginary_amd._abi import check, lib
     import ctypes as C
     check(lib.mipx_set_device(local), "mipx_set_device")
+    if args.sampling:
+        ia.set_reduce_sampling(args.sampling)
+    sampling = ia.reduce_sampling()
+    kernel = C2_KERNEL[sampling]
 
     n = args.batch
     plan = ia.plan_make(ia.make_opts(width=W_OUT, height=H_OUT, embed=1), ia.make_input(W_IN, H_IN, BANDS, "png"))
@@ -248,8 +257,7 @@ def main():
     verify = None
     if not args.no_verify and rank == 0:
         from oracle import oracle as o
-        if CENTRE:
-            o.set_switch("reduce_centre", 1)
+        o.set_switch("reduce_centre", int(sampling == "centre"))
         idx = [0, n - 1]
         got = d_out[idx].cpu().numpy().reshape(len(idx), H_OUT, W_OUT, BANDS)
         src = d_in[idx].cpu().numpy().reshape(len(idx), H_IN, W_IN, BANDS)
@@ -261,8 +269,7 @@ def main():
         value = images / wall_max
         alg_bytes = n * (in_img + out_img)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        variant = os.environ.get("MIPX_R2_VARIANT", "66")
-        traffic, traffic_src = pmc_traffic(f"k_reduce2x2<3, {variant}>")
+        traffic, traffic_src = pmc_traffic(kernel)
         line = {
             "metric": "images/sec (4K RGB->1080p Lanczos3 batch) + achieved HBM GB/s, 1/2/4/8 GPUs",
             "value": round(value, 1),
@@ -277,12 +284,12 @@ def main():
             "dtype": "u8",
             "data": "synthetic uniform-random uchar, device-resident (seed 20241220+rank)",
             "config": {"workload": "C2: batched 3840x2160x3 -> 1920x1080x3 Lanczos3 reduce (bimg "
-                                   "/resize?width=1920&height=1080), " +
-                                   ("centre sampling convention (PARITY_ASSUMPTIONS row 1 flipped), k_rcol"
-                                    if CENTRE else "fused k_reduce2x2"),
+                                   f"/resize?width=1920&height=1080), {sampling} sampling convention "
+                                   f"(PARITY_ASSUMPTIONS.md row 1), {kernel.split('<')[0]}",
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world} (independent shards)"},
             "achieved_hbm_gbs": round(achieved, 1),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},

@@ -134,6 +134,9 @@ def encode(px: np.ndarray, t: str, quality: Optional[int] = None, compression: O
     kw = {}
     if fmt in ("JPEG", "WEBP"):
         kw["quality"] = quality or DEFAULT_QUALITY
+    if fmt == "JPEG":
+        # libvips jpegsave's automatic chroma subsampling: 4:2:0 below Q 90, 4:4:4 from Q 90
+        kw["subsampling"] = 0 if kw["quality"] >= 90 else 2
     if fmt == "PNG" and compression is not None:
         kw["compress_level"] = compression
     try:

@@ -403,9 +403,8 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     a.strips = (ow * b + sbytes - 1) / sbytes;
     a.ksteps = (oh + kBcRows - 1) / kBcRows;
     const long long cols = static_cast<long long>(a.strips) * n;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBcNT, lds) != hipSuccess || per_cu < 1) per_cu = 2;
-    const long long slots = 256LL * per_cu;
+    const int per_cu = occupancy_per_cu(fn, kBcNT, lds, 2);
+    const long long slots = static_cast<long long>(device_cu_count()) * per_cu;
     const int ss_min = std::max(4, 4 * a.pre);
     int best_segs = static_cast<int>(std::max(1LL, (6 * slots + cols / 2) / cols));
     best_segs = std::min(best_segs, std::max(1, (a.ksteps + ss_min - 1) / ss_min));

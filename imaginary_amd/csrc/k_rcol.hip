@@ -583,9 +583,8 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // steps; pick the split that minimises (rounds of resident blocks) x (steps + 2)
     a.strips = (ow + 63) / 64;
     const long long cols = static_cast<long long>(a.strips) * n;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kRcNT, lds) != hipSuccess || per_cu < 1) per_cu = 2;
-    const long long slots = 256LL * per_cu;
+    const int per_cu = occupancy_per_cu(fn, kRcNT, lds, 2);
+    const long long slots = static_cast<long long>(device_cu_count()) * per_cu;
     int best_segs = 1;
     double best = 1e300;
     for (int segs = 1; segs <= a.ksteps; ++segs) {

@@ -77,7 +77,6 @@ struct RsArgs {
     double vs, hs;
     int centre;                  // centre sampling convention (mipx_set_reduce_sampling)
     const uint32_t *vpairs, *hpairs;  // [129][2][tpa] int16 tap pairs
-    int diag;                    // A/B diagnostic (MIPX_RSTRIP_DIAG): 1 skip vertical, 2 skip horizontal
 };
 
 __device__ __forceinline__ int ring_slot(int p, int ring) {
@@ -208,7 +207,7 @@ __global__ void __launch_bounds__(kRsThreads) k_rstrip(RsArgs a) {
 
     for (int yc = yb0; yc < yb1; yc += kRsR) {
         // ---- vertical pass: wave w -> intermediate rows yc + 2w, yc + 2w + 1 ----
-        if (!(a.diag & 1)) {
+        {  // vertical pass
             const int k0 = 2 * wave;
             const int y0r = yc + k0;
             if (y0r < yb1) {
@@ -315,7 +314,7 @@ __global__ void __launch_bounds__(kRsThreads) k_rstrip(RsArgs a) {
             lds_barrier();
         }
         // ---- horizontal pass: lane = output pixel x0 + xl of rows yc + hrow0 + HG i ----
-        if (!(a.diag & 2)) {
+        {  // horizontal pass
 #pragma unroll
             for (int i = 0; i < kRsR / HG; ++i) {
                 const int k = hrow0 + HG * i;
@@ -423,8 +422,6 @@ int reduce_strip_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doubl
     a.vs = vs;
     a.hs = hs;
     a.centre = reduce_centre();
-    const char *edg = tune_env("MIPX_RSTRIP_DIAG");
-    a.diag = (edg && *edg) ? std::atoi(edg) : 0;
     // every row of every image starts dword aligned: no per-row byte skew
     const bool sk = (a.pitch % 4) != 0 || (a.in_img % 4) != 0 || (reinterpret_cast<uintptr_t>(in) % 4) != 0;
     // strip width: 128 output pixels when the staged span fits 64 lanes x 16

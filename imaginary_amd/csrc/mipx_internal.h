@@ -32,6 +32,15 @@ void tune_reload();
 bool reduce_centre();
 inline double reduce_x_host(int o, double s, bool centre) { return centre ? (o + 0.5) * s - 0.5 : o * s; }
 
+// ---- device properties, cached per device (mipx_tuning.cpp) --------------------
+// compute units of the current device (256 on an MI355X in SPX mode; fewer per
+// partition in CPX / DPX modes)
+int device_cu_count();
+// resident workgroups per CU for kernel fn at `threads` threads and `lds` dynamic LDS
+// bytes on the current device (hipOccupancyMaxActiveBlocksPerMultiprocessor, queried
+// once per (device, fn, threads, lds)); `fallback` when the query fails
+int occupancy_per_cu(const void *fn, int threads, size_t lds, int fallback);
+
 // ---- device capability probes (k_probe.hip), run once per device -------------
 // Do direct-to-LDS dword buffer loads honour byte offsets that are not multiples of 4?
 bool lds_dma_unaligned_ok();

@@ -13,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "mipx_internal.h"
@@ -67,6 +68,43 @@ bool reduce_centre() { return g_sampling.load(std::memory_order_relaxed) == MIPX
 void tune_reload() {
     std::lock_guard<std::mutex> lk(g_mu);
     take_snapshot_locked();
+}
+
+}  // namespace mipx
+
+namespace mipx {
+
+int device_cu_count() {
+    static std::mutex mu;
+    static std::map<int, int> cus;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cus.find(dev);
+    if (it != cus.end()) return it->second;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    cus.emplace(dev, n);
+    return n;
+}
+
+int occupancy_per_cu(const void *fn, int threads, size_t lds, int fallback) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, const void *, int, size_t>, int> occ;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fallback;
+    const auto key = std::make_tuple(dev, fn, threads, lds);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = occ.find(key);
+        if (it != occ.end()) return it->second;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess || per_cu < 1)
+        per_cu = fallback;
+    std::lock_guard<std::mutex> lk(mu);
+    occ.emplace(key, per_cu);
+    return per_cu;
 }
 
 }  // namespace mipx

@@ -17,6 +17,7 @@ bimg.Resize there.
 """
 from __future__ import annotations
 
+import ctypes as C
 import dataclasses
 import json
 import math
@@ -341,7 +342,10 @@ def process_bytes(buf: bytes, opts: Dict[str, Any], wm=None) -> Image:
         if e.code == _abi.MIPX_EUNSUPPORTED:
             raise EngineUnsupported(str(e)) from e
         raise ImaginaryError(f"image processing error: {e}", 500) from e
-    if plan.load_shrink > 1:  # process() re-plans on the codec-shrunk size
+    rotates = any(step[0] in ("rot", "flip") for step in plan.describe())
+    if plan.load_shrink > 1 and itype == "jpeg" and rotates and not opts.get("no_auto_rotate"):
+        px = _rotate_reencode_shrink_on_load(buf, hdr, itype, opts, wm_px)
+    elif plan.load_shrink > 1:  # process() re-plans on the codec-shrunk size
         src = Decoded(np.zeros((1, 1, hdr.bands), np.uint8), itype, hdr.orientation, hdr.w, hdr.h)
         px = process(src, opts, wm=wm_px, redecode=redecode)
     else:
@@ -354,6 +358,69 @@ def process_bytes(buf: bytes, opts: Dict[str, Any], wm=None) -> Image:
             raise ImaginaryError(f"image processing error: {e}", 500) from e
         body = codec.encode(px, "jpeg", quality or None)
     return Image(body, codec.mime_type(codec.sniff_type(body)))
+
+
+_ROTATION_KEYS = ("rotate", "flip", "flop", "no_auto_rotate")
+JPEG_REENCODE_QUALITY = 100  # bimg getImageBuffer: vips_jpegsave_bridge(strip 1, Q 100, no interlace)
+
+
+def _drop_leading_steps(plan, k: int, w: int, h: int):
+    """The plan without its first k steps, taking a w x h input."""
+    rest = _abi.MipxPlan()
+    C.memmove(C.byref(rest), C.byref(plan), C.sizeof(plan))
+    rest.in_w, rest.in_h, rest.load_shrink = w, h, 1
+    rest.n_steps = plan.n_steps - k
+    for i in range(rest.n_steps):
+        rest.steps[i] = plan.steps[i + k]
+    return rest
+
+
+def _rotate_reencode_shrink_on_load(buf: bytes, hdr, itype: str, opts: Dict[str, Any], wm_px):
+    """bimg 1.1.9 resizer() for a JPEG that rotates or flips (EXIF orientation or an
+    explicit rotate / flip / flop) and then shrinks on load (image.go:96 -> bimg
+    resizer.go): rotateAndFlipImage runs on the FULL-size decode, the rotated image is
+    re-encoded (getImageBuffer: jpegsave, Q 100, metadata stripped) and that buffer is
+    what shrinkOnLoad decodes at 1/s; every later step is the plan's own (bimg computes
+    its factors before the re-encode, from the caller's options).
+      1. decode at full size;
+      2. rotate / flip on the engine (the plan's rotation steps, at full size);
+      3. re-encode with the host codec (JPEG Q 100, no EXIF);
+      4. decode that with the DCT shrink the plan asks for;
+      5. run the rest of the plan on it."""
+    full = codec.decode(buf)
+    rot_opts = {k: opts[k] for k in _ROTATION_KEYS if k in opts}
+    rot_plan = plan_make(make_opts(**rot_opts), make_input(full.shape[1], full.shape[0], full.shape[2], "png",
+                                                           hdr.orientation))
+    rot_ops = [step[0] for step in rot_plan.describe()]
+    if not rot_ops or any(op not in ("rot", "flip") for op in rot_ops):
+        raise ImaginaryError(f"rotation plan {rot_ops}: expected rot / flip steps only", 500)
+    upright = _run(rot_plan, full, None)
+    buf2 = codec.encode(upright, "jpeg", JPEG_REENCODE_QUALITY)
+    inp = make_input(hdr.w, hdr.h, hdr.bands, itype, hdr.orientation)
+    if wm_px is not None:
+        wm_px = wm_px if wm_px.ndim == 3 else wm_px[:, :, None]
+        opts = dict(opts, wm_enable=1)
+        inp.wm_w, inp.wm_h, inp.wm_bands = wm_px.shape[1], wm_px.shape[0], wm_px.shape[2]
+    try:
+        plan = plan_make(make_opts(**opts), inp)
+        px = codec.decode(buf2, plan.load_shrink)
+        # the decode the plan was made for is the un-rotated image at 1/s: same size,
+        # axes swapped by a quarter turn
+        swap = upright.shape[:2] != full.shape[:2]
+        inp.decoded_w, inp.decoded_h = (px.shape[0], px.shape[1]) if swap else (px.shape[1], px.shape[0])
+        plan = plan_make(make_opts(**opts), inp)
+    except _abi.MipxError as e:
+        if e.code == _abi.MIPX_EUNSUPPORTED:
+            raise EngineUnsupported(str(e)) from e
+        raise ImaginaryError(f"image processing error: {e}", 500) from e
+    steps = plan.describe()
+    k = len(rot_ops)
+    if [st[0] for st in steps[:k]] != rot_ops:
+        raise ImaginaryError(f"plan {steps}: expected the rotation steps {rot_ops} first", 500)
+    rest = _drop_leading_steps(plan, k, px.shape[1], px.shape[0])
+    if rest.n_steps == 0:
+        return px
+    return _run(rest, px, wm_px)
 
 
 # ---- image.go operations ----------------------------------------------------------------

@@ -8,6 +8,8 @@ testdata files (tests/golden/testdata/, copied verbatim as data).
 """
 import os
 
+import numpy as np
+
 import pytest
 
 from conftest import ROOT
@@ -101,3 +103,58 @@ def test_watermark_image_over_bytes(im):
 def test_text_watermark_falls_back(im):
     with pytest.raises(im.EngineUnsupported):
         im.Watermark(read("imaginary.jpg"), im.build_params_from_query({"text": "hello"}))
+
+
+def _drop_leading(p, k, w, h):
+    """An oracle plan without its first k steps, taking a w x h input."""
+    import ctypes
+    from oracle import oracle as o
+    rest = o.RefPlan()
+    ctypes.memmove(ctypes.byref(rest), ctypes.byref(p), ctypes.sizeof(p))
+    rest.in_w, rest.in_h, rest.load_shrink, rest.n_steps = w, h, 1, p.n_steps - k
+    for i in range(rest.n_steps):
+        rest.steps[i] = p.steps[i + k]
+    return rest
+
+
+ROTATED = [("orient6.jpg", {"width": 300}), ("orient6.jpg", {"width": 200, "height": 200}),
+           ("imaginary.jpg", {"width": 200, "rotate": 90}), ("imaginary.jpg", {"width": 120, "flip": "true"})]
+
+
+@pytest.mark.parametrize("fixture,query", ROTATED, ids=[f"{f}-{'-'.join(q)}" for f, q in ROTATED])
+def test_rotated_jpeg_reencodes_before_shrink_on_load(im, oracle, fixture, query):
+    """bimg's resizer for a JPEG that rotates or flips (EXIF orientation 6, or an explicit
+    rotate / flip) and shrinks on load: rotate the FULL decode, re-encode it (JPEG Q 100,
+    no EXIF), decode that at 1/s, run the rest of the plan (image.go:96, :255-265).
+    imaginary.Resize over bytes must equal that chain run stage by stage on the host
+    with the oracle's pixels and the same codec calls, byte for byte."""
+    from imaginary_amd import codec
+    buf = read(fixture)
+    hdr = codec.header(buf)
+    o = im.build_params_from_query({k: str(v) for k, v in query.items()})
+    got = im.Resize(buf, o)
+    opts = {k: v for k, v in im.bimg_options(o).items() if k not in ("type", "quality", "compression")}
+    opts["embed"] = 1
+    full = codec.decode(buf)
+    rot = {k: opts[k] for k in ("rotate", "flip", "flop", "no_auto_rotate") if k in opts}
+    e, rp = oracle.plan(rot, dict(w=hdr.w, h=hdr.h, bands=hdr.bands, type=3, orientation=hdr.orientation))
+    assert e == 0 and rp.n_steps >= 1
+    upright = oracle.execute(rp, full)
+    buf2 = codec.encode(upright, "jpeg", 100)
+    inp = dict(w=hdr.w, h=hdr.h, bands=hdr.bands, type=1, orientation=hdr.orientation)
+    e, p0 = oracle.plan(opts, inp)
+    assert e == 0 and p0.load_shrink > 1, "the case must shrink on load"
+    px = codec.decode(buf2, p0.load_shrink)
+    swap = upright.shape[:2] != full.shape[:2]
+    dw, dh = (px.shape[0], px.shape[1]) if swap else (px.shape[1], px.shape[0])
+    e, p1 = oracle.plan(opts, dict(inp, decoded_w=dw, decoded_h=dh))
+    assert e == 0
+    want_px = oracle.execute(_drop_leading(p1, rp.n_steps, px.shape[1], px.shape[0]), px)
+    assert (want_px.shape[1], want_px.shape[0]) == (p1.out_w, p1.out_h)
+    want = codec.encode(want_px, "jpeg")
+    assert size_of(got.body) == (p1.out_w, p1.out_h)
+    assert got.body == want, "engine output differs from the stage-by-stage chain"
+    # the test tells the two sequences apart: rotating the shrink-on-load decode instead
+    # (the pre-r04 engine) gives other pixels
+    old = oracle.execute(p1, codec.decode(buf, p0.load_shrink))
+    assert old.shape == want_px.shape and not np.array_equal(old, want_px)

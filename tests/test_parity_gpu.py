@@ -70,15 +70,16 @@ def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
 
 
-@pytest.mark.parametrize("var", ["acc", "ring", "w5"])
+@pytest.mark.parametrize("var", ["dot", "ring", "vdot_hpush", "vring_hdot", "vmix_hpush", "vmix_hdot", "vpk_hpush"])
 def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, var, monkeypatch):
     """The fused 2x2 kernels (corner: k_reduce2x2 variant 66, the r01/r02 A/B builds
     are recorded under profiles/ and no longer compiled; centre: k_reduce2c with
-    open accumulators, the 12-row pair ring (MIPX_R2C_RING), 5 waves per SIMD (MIPX_R2C_W5))
-    are bit-exact, including strips that end at the image edge, images shorter than a band
-    and the smallest eligible sizes."""
-    monkeypatch.setenv("MIPX_R2C_RING", "1" if var == "ring" else "0")
-    monkeypatch.setenv("MIPX_R2C_W5", "1" if var == "w5" else "0")
+    v_dot2_f32_f16 on f16 pixel pairs in both passes, or the f32 ring / push passes behind
+    MIPX_R2C_VM=1 / MIPX_R2C_HM=0) are bit-exact, including strips that end at the image
+    edge, images shorter than a band and the smallest eligible sizes."""
+    monkeypatch.setenv("MIPX_R2C_VM", "1" if var in ("ring", "vring_hdot") else "3" if "vmix" in var else
+                       "4" if "vpk" in var else "2")
+    monkeypatch.setenv("MIPX_R2C_HM", "0" if "hpush" in var or var == "ring" else "1")
     for h, w, b in ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1001 * 4 // 4 - 1, 4), (200, 646, 3),
                     (8, 8, 4), (9, 12, 3), (25, 164, 3), (131, 1000, 4), (1081, 324, 3), (16, 3840, 3)):
         if (w * b) % 4:
