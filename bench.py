@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 # the kernel C2 runs under each reduce sampling convention (PARITY_ASSUMPTIONS.md row 1):
 # its roofline and PMC traffic record are this kernel's
-C2_KERNEL = {"corner": "k_reduce2x2<3, 66>", "centre": "k_reduce2c<3, false, 0>"}
+C2_KERNEL = {"corner": "k_reduce2x2<3, 66>", "centre": "k_reduce2c<3>"}
 
 def parse():
     ap = argparse.ArgumentParser()

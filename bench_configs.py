@@ -106,7 +106,8 @@ def line(name, workload, images, wall_s, dev_ms, alg_bytes, verified, extra=None
          "ms_per_step": round(wall_s * 1e3, 3), "device_ms_per_step": round(dev_ms, 3),
          "achieved_gbs": round(alg_bytes / (dev_ms * 1e-3) / 1e9, 1),
          "hbm_frac": round(alg_bytes / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-         "alg_bytes_per_step": alg_bytes, "verified_vs_oracle": verified}
+         "alg_bytes_per_step": alg_bytes, "verified_vs_oracle": verified,
+         "sampling": ["corner", "centre"][lib.mipx_reduce_sampling()]}
     if extra:
         d.update(extra)
     print(json.dumps(d), flush=True)
@@ -273,7 +274,14 @@ def main():
     ap.add_argument("--e2e-queues", type=int, default=1, help="request queues (streams + worker) per device")
     ap.add_argument("--c5-requests", type=int, default=512 * int(os.environ.get("WORLD_SIZE", "1")),
                     help="total requests, sharded across ranks (4096 at 8 GPUs)")
+    ap.add_argument("--sampling", choices=["corner", "centre"], default=None,
+                    help="libvips reduce sampling convention (PARITY_ASSUMPTIONS.md row 1), engine and oracle")
     args = ap.parse_args()
+    if args.sampling:
+        import imaginary_amd as ia
+        from oracle import oracle as o
+        ia.set_reduce_sampling(args.sampling)
+        o.set_switch("reduce_centre", int(args.sampling == "centre"))
     globals()["WARM_MS"] = args.warm_ms
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)

@@ -202,13 +202,18 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
             for (int k = 0; k < ND; ++k) v[k] = sp[k];
 #pragma unroll
             for (int k = 0; k < B; ++k) t[k] = __builtin_amdgcn_alignbyte(v[k + 1], v[k], sh);
-            const u8 *tb = reinterpret_cast<const u8 *>(t);
             int16_t hv[B];
 #pragma unroll
             for (int c = 0; c < B; ++c) {
-                // byte pairs (tap 0, 1) and (2, 3) of channel c, zero-extended to int16
-                const uint32_t p01 = static_cast<uint32_t>(tb[c]) | (static_cast<uint32_t>(tb[c + B]) << 16);
-                const uint32_t p23 = static_cast<uint32_t>(tb[c + 2 * B]) | (static_cast<uint32_t>(tb[c + 3 * B]) << 16);
+                // byte pairs (tap 0, 1) and (2, 3) of channel c, zero-extended to int16: one
+                // v_perm each (selector 0x0c = a zero byte; bytes of t[hi] are 4-7)
+                auto pair = [&](int j0, int j1) -> uint32_t {
+                    const int d0 = j0 >> 2, d1 = j1 >> 2;
+                    const uint32_t sel = static_cast<uint32_t>((j0 & 3) | (0x0c << 8) | (((j1 & 3) + 4) << 16) | (0x0c << 24));
+                    return __builtin_amdgcn_perm(t[d1], t[d0], sel);
+                };
+                const uint32_t p01 = pair(c, c + B);
+                const uint32_t p23 = pair(c + 2 * B, c + 3 * B);
                 int acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, p01), __builtin_bit_cast(af_s2, c01), 2048, false);
                 acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, p23), __builtin_bit_cast(af_s2, c23), acc, false);
                 hv[c] = static_cast<int16_t>(acc >> 12);
@@ -218,17 +223,25 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
             for (int c = 0; c < B; ++c) hq[c] = hv[c];
         }
     }
+    // the tile's output-row positions, once per block (fp64 as affine_pos): first H row
+    // and the packed int16 tap pairs, read back by every lane of the row's wave
+    uint32_t *vpos = reinterpret_cast<uint32_t *>(hrow + a.nr_max * a.hs);  // [ty][3]
+    if (tid < a.ty && y0 + tid <= y_last) {
+        int ty;
+        const int iy = af_ix(y0 + tid, a.yscale, &ty);
+        const int *cy = a.tab + ty * 4;
+        vpos[3 * tid] = static_cast<uint32_t>((iy - 2 - r0) * a.hs);
+        vpos[3 * tid + 1] = (static_cast<uint32_t>(cy[0]) & 0xffffu) | (static_cast<uint32_t>(cy[1]) << 16);
+        vpos[3 * tid + 2] = (static_cast<uint32_t>(cy[2]) & 0xffffu) | (static_cast<uint32_t>(cy[3]) << 16);
+    }
     __syncthreads();
     // ---- 3. vertical pass: wave rows y0 + wave, + 4, ...; lane dword columns lane + 64 k ----
     u8 *ob = a.out + img * a.out_img;
     const int vbytes = (x_last - x0 + 1) * B;
     for (int y = y0 + wave; y <= y_last; y += 4) {
-        int ty;
-        const int iy = af_ix(y, a.yscale, &ty);
-        const int *cy = a.tab + ty * 4;
-        const uint32_t y01 = (static_cast<uint32_t>(cy[0]) & 0xffffu) | (static_cast<uint32_t>(cy[1]) << 16);
-        const uint32_t y23 = (static_cast<uint32_t>(cy[2]) & 0xffffu) | (static_cast<uint32_t>(cy[3]) << 16);
-        const int16_t *h0 = hrow + (iy - 2 - r0) * a.hs;
+        const uint32_t *vp = vpos + 3 * (y - y0);
+        const uint32_t y01 = vp[1], y23 = vp[2];
+        const int16_t *h0 = hrow + vp[0];
 #pragma unroll
         for (int k = 0; k < B; ++k) {
             const int d = lane + 64 * k;
@@ -356,7 +369,8 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
             g.nr_max = nrows;
             g.hs = kAfTX * b;
             g.out_aligned = (a.ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
-            const size_t lds = ((static_cast<size_t>(g.nr_max) * g.ncb + 15) & ~size_t(15)) + static_cast<size_t>(g.nr_max) * g.hs * 2;
+            const size_t lds = ((static_cast<size_t>(g.nr_max) * g.ncb + 15) & ~size_t(15)) +
+                               static_cast<size_t>(g.nr_max) * g.hs * 2 + 12 * static_cast<size_t>(ty);
             if (lds > 40 * 1024 || ncols * b > 4 * 4096) continue;
             const long long ytiles = (a.oh + ty - 1) / ty;
             if (ytiles > 65535) continue;

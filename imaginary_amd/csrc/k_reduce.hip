@@ -340,28 +340,23 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
 // (i - 5.5) / 2, so taps 0..11 are the Lanczos lobe at +-0.25 .. +-2.75 and tap 12
 // (3.25) is zero; the host checks that shape (and the symmetry T_i = T_11-i) on the
 // integer table before choosing this kernel.  Output o of either pass is
-//     o = sum_{i=0..11} T_i p[2o - 5 + i]
-// Twelve products per output byte instead of the corner convention's seven, so the
-// arithmetic is the part to make cheap:
-//  * DOT (default): pixels enter the products as packed f16 pairs (1024 + p, a
-//    v_perm of the byte next to 0x64), taps as f16 T_i / 4096 (all exact: 11-bit
-//    integers), and v_dot2_f32_f16 takes two taps per instruction; every partial sum
-//    is an exact multiple of 2^-13 below 2^11 in magnitude, so the sum is exact, and
-//    the seed 2^-13 - 1024 * sum(T) / 4096 removes the 1024 offsets.  Vertically a
-//    pair register holds rows (2m + 1, 2m + 2) of one byte column; output o reads the
-//    six pairs m = o - 3 .. o + 2, so each pair is built once and read by six outputs.
-//    Horizontally a pair holds window pixels (2q, 2q + 1) of one channel; output k of
-//    an item reads q = k .. k + 5.
-//  * RING (A/B): the 12 rows converted to f32 in a register ring, six pair sums and
-//    six v_fma_f32 per byte; the horizontal pass then pushes each converted pixel into
-//    the K x B accumulators (12 v_fma_f32 per output byte).
-// Geometry: lane t of the vertical pass owns dword t of the strip (channel agnostic)
-// and walks a band of output rows in 12-row chunks (two ring periods, so every slot
-// index is a compile-time constant); the rounded uchar intermediate goes to a
-// double-buffered LDS image, and items of K output pixels read the 14 dwords they
-// need from it (2K + 10 intermediate pixels) and store 12 / 8 contiguous bytes.  Same
-// strips / bands as k_reduce2x2<B, 66>, so execute_plan's demand windows round to the
-// same tiles.
+//     o = sum_{i=0..11} T_i p[2o - 5 + i] = sum_{k=0..5} T_k (p[2o - 5 + k] + p[2o + 6 - k])
+// Twelve multiply-adds per byte and pass instead of the corner convention's seven,
+// and that arithmetic, not HBM, bounds the kernel (a memory-only build
+// of the same access pattern streams 1.25x faster).
+//  * Vertical: lane t owns dword t of the strip (channel agnostic) and keeps the 12
+//    rows of the current window converted to f32 in a register ring (slot = row mod
+//    12; a 12-row chunk adds 24 rows = two ring periods, so every slot index is a
+//    compile-time constant); six pair sums and six v_fma_f32 per byte.
+//  * Horizontal: an item of K output pixels reads the 2K + 10 intermediate pixels it
+//    needs (14 dwords for RGB and RGBA) and pushes each converted pixel into the
+//    K x B accumulators it feeds (12 v_fma_f32 per output byte; only the accumulators
+//    stay live, so the kernel fits 96 VGPRs and 5 workgroups per CU).
+// All multiply-adds are plain f32 ops: the packed v_pk_add_f32 / v_pk_fma_f32, the
+// f16 v_dot2c_f32_f16 and v_fma_mix_f32 forms were built, bit-exact, and slower
+// (profiles/r04/reduce2c/, issue costs in profiles/r04/valu_rate_probe.jsonl).
+// Same strips / bands as k_reduce2x2<B, 66>, so execute_plan's demand windows round to
+// the same tiles.
 // ===========================================================================
 template <int B>
 struct R2C {
@@ -386,15 +381,9 @@ struct Reduce2cArgs {
     long long in_img, out_img;
     float t[6];   // T_0..T_5 = matrixi[64][0..5] / 4096 (exact; T_11-i = T_i)
     float bias;   // 2^-13: RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5)
-    float seed;   // DOT: 2^-13 - 1024 * sum(T) / 4096 (removes the f16 offsets)
 };
 
-typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-// four byte columns as scalar floats (RING): the multiply-adds stay plain v_fma_f32
-// (packed v_pk_fma_f32 issued as many instructions but waited twice as long on
-// issue, PMC in profiles/r04)
+// four byte columns as scalar floats: the multiply-adds stay plain v_fma_f32
 struct S4 {
     float x, y, z, w;
 };
@@ -407,13 +396,7 @@ __device__ __forceinline__ S4 fma4(float t, const S4 &r, const S4 &acc) {
 }
 __device__ __forceinline__ S4 add4(const S4 &a, const S4 &b) { return S4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
 
-__device__ __forceinline__ float dot2(uint32_t px, h2v taps, float acc) {
-    return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, px), taps, acc, false);
-}
-constexpr uint32_t kF16Magic = 0x64646464u;  // byte 0x64 above a pixel byte: f16 1024 + p
-
-// VM: 1 = RING (f32 ring + pair sums), 2 = DOT (f16 pairs + v_dot2); HM: 0 = f32 push, 1 = DOT
-template <int B, int VM, int HM>
+template <int B>
 __device__ __forceinline__ void reduce2c_tile(const Reduce2cArgs &a, int img, int strip, int band, uint32_t *lds) {
     using G = R2C<B>;
     constexpr int kThreads = G::kThreads, kPitch = G::kPitch, TW = G::TW, K = G::K, R = kR;
@@ -430,12 +413,10 @@ __device__ __forceinline__ void reduce2c_tile(const Reduce2cArgs &a, int img, in
     const int y0 = a.y_base + band * a.band_rows;  // a multiple of 12: 2 * y0 == 0 (mod 12)
     const int y1 = min(y0 + a.band_rows, a.y_end);
     const float t0 = a.t[0], t1 = a.t[1], t2 = a.t[2], t3 = a.t[3], t4 = a.t[4], t5 = a.t[5], bias = a.bias;
-    const float seed = a.seed;
-    const float mseed = a.bias - 1024.0f * (a.t[0] + a.t[1] + a.t[2] + a.t[3] + a.t[4] + a.t[5]);
-    // DOT tap pairs (T_2q, T_2q+1), q = 0..5: (t0,t1) (t2,t3) (t4,t5) (t5,t4) (t3,t2) (t1,t0)
-    const h2v TP[6] = {h2v{(_Float16)t0, (_Float16)t1}, h2v{(_Float16)t2, (_Float16)t3},
-                       h2v{(_Float16)t4, (_Float16)t5}, h2v{(_Float16)t5, (_Float16)t4},
-                       h2v{(_Float16)t3, (_Float16)t2}, h2v{(_Float16)t1, (_Float16)t0}};
+    auto tap = [&](int k) -> float {  // T_k of the symmetric 12-tap mask
+        const int m = k < 6 ? k : 11 - k;
+        return m == 0 ? t0 : m == 1 ? t1 : m == 2 ? t2 : m == 3 ? t3 : m == 4 ? t4 : t5;
+    };
     const int nl = px0 < 0 ? -px0 : 0;
     const int x_last = min(x0 + TW, a.x_end) - 1;
     const int fr = a.w - px0;
@@ -447,39 +428,12 @@ __device__ __forceinline__ void reduce2c_tile(const Reduce2cArgs &a, int img, in
         r = clampi(r, 0, a.h - 1);
         return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * row_bytes, 0));
     };
-    // DOT: rows a, b of 4 byte columns -> 4 f16 pairs (1024 + a_j, 1024 + b_j)
-    auto pairs4 = [&](uint32_t ra, uint32_t rb, uint32_t *q) {
-        const uint32_t lo = __builtin_amdgcn_perm(rb, ra, 0x05010400u);  // a0 b0 a1 b1
-        const uint32_t hi = __builtin_amdgcn_perm(rb, ra, 0x07030602u);  // a2 b2 a3 b3
-        q[0] = __builtin_amdgcn_perm(kF16Magic, lo, 0x04010400u);
-        q[1] = __builtin_amdgcn_perm(kF16Magic, lo, 0x04030402u);
-        q[2] = __builtin_amdgcn_perm(kF16Magic, hi, 0x04010400u);
-        q[3] = __builtin_amdgcn_perm(kF16Magic, hi, 0x04030402u);
-    };
 
-    // RING: slot s holds input row 2 yc + d, d == s (mod 12).
-    // DOT: slot s holds the pair m = (rows 2m + 1, 2m + 2) with m - yc == s (mod 6)
-    S4 ring[VM == 1 || VM == 4 ? 12 : 1];
-    uint32_t pr[VM == 0 || VM == 2 ? 6 : 1][4];
-    // MIX: slot s holds input row 2 yc + d (d == s mod 12) as two registers of u16 halves,
-    // (b0, b2) and (b1, b3); even rows carry 0x64 above each byte, so adding an odd row's
-    // plain halves (v_pk_add_u16) gives the f16 1024 + a + b of the pair directly
-    uint32_t mr[VM == 3 ? 12 : 1][2];
-    auto mix_row = [&](uint32_t r, bool even, uint32_t *q) {
-        q[0] = even ? __builtin_amdgcn_perm(kF16Magic, r, 0x04020400u) : __builtin_amdgcn_perm(r, r, 0x0c020c00u);
-        q[1] = even ? __builtin_amdgcn_perm(kF16Magic, r, 0x04030401u) : __builtin_amdgcn_perm(r, r, 0x0c030c01u);
-    };
+    // ring slot s holds input row 2 yc + d, d == s (mod 12)
+    S4 ring[12];
     const S4 BI = {bias, bias, bias, bias};
-    if (VM == 1 || VM == 4) {
 #pragma unroll
-        for (int d = -5; d <= 4; ++d) ring[(d + 12) % 12] = cvt4s(load_row(2 * y0 + d));
-    } else if (VM == 3) {
-#pragma unroll
-        for (int d = -5; d <= 4; ++d) mix_row(load_row(2 * y0 + d), (d & 1) == 0, mr[(d + 12) % 12]);
-    } else {
-#pragma unroll
-        for (int m = -3; m <= 1; ++m) pairs4(load_row(2 * (y0 + m) + 1), load_row(2 * (y0 + m) + 2), pr[(m + 6) % 6]);
-    }
+    for (int d = -5; d <= 4; ++d) ring[(d + 12) % 12] = cvt4s(load_row(2 * y0 + d));
     uint32_t nx[R], ny[R];  // rows 2o + 5 and 2o + 6 of output row o = yc + u
 #pragma unroll
     for (int u = 0; u < R; ++u) {
@@ -492,86 +446,24 @@ __device__ __forceinline__ void reduce2c_tile(const Reduce2cArgs &a, int img, in
         const bool more = yc + R < y1;
 #pragma unroll
         for (int u = 0; u < R; ++u) {
-            uint32_t d;
-            if (VM == 0) {  // MEMORY-ONLY DIAGNOSTIC (temporary)
-                d = nx[u] + ny[u];
-            } else if (VM == 1 || VM == 4) {
-                ring[(2 * u + 5) % 12] = cvt4s(nx[u]);
-                ring[(2 * u + 6) % 12] = cvt4s(ny[u]);
-            } else if (VM == 3) {
-                mix_row(nx[u], false, mr[(2 * u + 5) % 12]);
-                mix_row(ny[u], true, mr[(2 * u + 6) % 12]);
-            } else {
-                pairs4(nx[u], ny[u], pr[(u + 2) % 6]);  // pair m = o + 2
-            }
-            if (more) {
+            ring[(2 * u + 5) % 12] = cvt4s(nx[u]);
+            ring[(2 * u + 6) % 12] = cvt4s(ny[u]);
+            if (more) {  // this register now fetches the next chunk's row
                 nx[u] = load_row(2 * (yc + R + u) + 5);
                 ny[u] = load_row(2 * (yc + R + u) + 6);
             }
-            if (VM == 0) {
-            } else if (VM == 1) {
-                // pair k: rows 2o - 5 + k and 2o + 6 - k
+            // pair k: rows 2o - 5 + k and 2o + 6 - k
 #define RC_LO(k) ring[(2 * u + 7 + (k)) % 12]
 #define RC_HI(k) ring[(2 * u + 6 - (k) + 12) % 12]
-                S4 acc = fma4(t5, add4(RC_LO(5), RC_HI(5)), BI);
-                acc = fma4(t4, add4(RC_LO(4), RC_HI(4)), acc);
-                acc = fma4(t3, add4(RC_LO(3), RC_HI(3)), acc);
-                acc = fma4(t2, add4(RC_LO(2), RC_HI(2)), acc);
-                acc = fma4(t1, add4(RC_LO(1), RC_HI(1)), acc);
-                acc = fma4(t0, add4(RC_LO(0), RC_HI(0)), acc);
+            S4 acc = fma4(t5, add4(RC_LO(5), RC_HI(5)), BI);
+            acc = fma4(t4, add4(RC_LO(4), RC_HI(4)), acc);
+            acc = fma4(t3, add4(RC_LO(3), RC_HI(3)), acc);
+            acc = fma4(t2, add4(RC_LO(2), RC_HI(2)), acc);
+            acc = fma4(t1, add4(RC_LO(1), RC_HI(1)), acc);
+            acc = fma4(t0, add4(RC_LO(0), RC_HI(0)), acc);
 #undef RC_LO
 #undef RC_HI
-                d = pack4b(acc.x, acc.y, acc.z, acc.w);
-            } else if (VM == 4) {
-                // the ring's pair sums and multiply-adds two byte columns per v_pk_add_f32 /
-                // v_pk_fma_f32 (each ~0.8 of a v_fma_f32's issue cost per result on one wave,
-                // scripts/probe/valu_rate_probe.hip)
-                typedef float f2 __attribute__((ext_vector_type(2)));
-                f2 lo = {bias, bias}, hi = {bias, bias};
-#pragma unroll
-                for (int k = 5; k >= 0; --k) {
-                    const S4 &A = ring[(2 * u + 7 + k) % 12], &Bv = ring[(2 * u + 6 - k + 12) % 12];
-                    const float tk = k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : k == 3 ? t3 : k == 4 ? t4 : t5;
-                    const f2 T = {tk, tk};
-                    lo = __builtin_elementwise_fma(T, f2{A.x, A.y} + f2{Bv.x, Bv.y}, lo);
-                    hi = __builtin_elementwise_fma(T, f2{A.z, A.w} + f2{Bv.z, Bv.w}, hi);
-                }
-                d = pack4b(lo.x, lo.y, hi.x, hi.y);
-            } else if (VM == 3) {
-                // pair k: rows 2o - 5 + k and 2o + 6 - k (one even, one odd); v_fma_mix_f32 takes
-                // each f16 half of the u16 sum straight into the f32 multiply-add
-                float acc[4] = {mseed, mseed, mseed, mseed};
-#pragma unroll
-                for (int k = 5; k >= 0; --k) {
-                    const uint32_t *lo = mr[(2 * u + 7 + k) % 12], *hi = mr[(2 * u + 6 - k + 12) % 12];
-                    const float tk = k == 0 ? t0 : k == 1 ? t1 : k == 2 ? t2 : k == 3 ? t3 : k == 4 ? t4 : t5;
-                    const h2v s02 = __builtin_bit_cast(h2v, static_cast<uint32_t>(__builtin_bit_cast(
-                        uint32_t, __builtin_bit_cast(u16x2, lo[0]) + __builtin_bit_cast(u16x2, hi[0]))));
-                    const h2v s13 = __builtin_bit_cast(h2v, static_cast<uint32_t>(__builtin_bit_cast(
-                        uint32_t, __builtin_bit_cast(u16x2, lo[1]) + __builtin_bit_cast(u16x2, hi[1]))));
-                    acc[0] = __builtin_fmaf(static_cast<float>(s02.x), tk, acc[0]);
-                    acc[2] = __builtin_fmaf(static_cast<float>(s02.y), tk, acc[2]);
-                    acc[1] = __builtin_fmaf(static_cast<float>(s13.x), tk, acc[1]);
-                    acc[3] = __builtin_fmaf(static_cast<float>(s13.y), tk, acc[3]);
-                }
-                d = pack4b(acc[0], acc[1], acc[2], acc[3]);
-            } else {
-                // two independent chains per byte (pairs 0-2 from the seed, 3-5 from 0): the
-                // partial sums and their total are exact, so the split changes nothing
-                float acc[4] = {seed, seed, seed, seed}, acc2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int q = 0; q < 3; ++q) {  // pair m = o - 3 + q, and m + 3
-                    const uint32_t *pq = pr[(u + 3 + q) % 6];
-                    const uint32_t *pq2 = pr[(u + 6 + q) % 6];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        acc[j] = dot2(pq[j], TP[q], acc[j]);
-                        acc2[j] = dot2(pq2[j], TP[q + 3], acc2[j]);
-                    }
-                }
-                d = pack4b(acc[0] + acc2[0], acc[1] + acc2[1], acc[2] + acc2[2], acc[3] + acc2[3]);
-            }
-            if (tid < G::ND) L[u * kPitch + tid] = d;
+            if (tid < G::ND) L[u * kPitch + tid] = pack4b(acc.x, acc.y, acc.z, acc.w);
         }
         if (edge) {  // EXTEND_COPY inside the LDS image
             __syncthreads();
@@ -616,74 +508,33 @@ __device__ __forceinline__ void reduce2c_tile(const Reduce2cArgs &a, int img, in
                 win[12] = dd.x;
                 win[13] = dd.y;
             }
+            // window pixel t (intermediate pixel 2x - 5 + t) feeds output k with tap t - 2k
             float o[K][B];
-            if (HM == 2) {  // MEMORY-ONLY DIAGNOSTIC (temporary)
 #pragma unroll
-                for (int k = 0; k < K; ++k)
+            for (int k = 0; k < K; ++k)
 #pragma unroll
-                    for (int c = 0; c < B; ++c) o[k][c] = __uint_as_float(win[(k * B + c) % 14] & 0x437f0000u);
-            } else if (HM == 1) {
-                // window pixels (2q, 2q + 1) of channel c as an f16 pair, q = 0 .. K + 4
+                for (int c = 0; c < B; ++c) o[k][c] = bias;
+#pragma unroll
+            for (int t = 0; t < 2 * K + 10; ++t) {
+                float v[B];
 #pragma unroll
                 for (int c = 0; c < B; ++c) {
-                    uint32_t qp[K + 5];
-#pragma unroll
-                    for (int q = 0; q < K + 5; ++q) {
-                        const int lb0 = B * 2 * q + c + G::OFF0, lb1 = lb0 + B;
-                        const int d0 = lb0 >> 2, d1 = lb1 >> 2, s0 = lb0 & 3, s1 = lb1 & 3;
-                        if (d0 == d1) {
-                            qp[q] = __builtin_amdgcn_perm(kF16Magic, win[d0],
-                                                          static_cast<uint32_t>(s0 | (4 << 8) | (s1 << 16) | (4 << 24)));
-                        } else {  // d1 == d0 + 1: gather the two bytes, then interleave 0x64
-                            const uint32_t g = __builtin_amdgcn_perm(win[d1], win[d0],
-                                                                     static_cast<uint32_t>(s0 | ((s1 + 4) << 8)));
-                            qp[q] = __builtin_amdgcn_perm(kF16Magic, g, 0x04010400u);
-                        }
-                    }
-#pragma unroll
-                    for (int k = 0; k < K; ++k) {
-                        float acc = seed, acc2 = 0.f;
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) {
-                            acc = dot2(qp[k + q], TP[q], acc);
-                            acc2 = dot2(qp[k + q + 3], TP[q + 3], acc2);
-                        }
-                        o[k][c] = acc + acc2;
+                    const int lb = B * t + c + G::OFF0;
+                    const uint32_t dd = win[lb >> 2];
+                    switch (lb & 3) {
+                        case 0: v[c] = ubyte_once<0>(dd); break;
+                        case 1: v[c] = ubyte_once<1>(dd); break;
+                        case 2: v[c] = ubyte_once<2>(dd); break;
+                        default: v[c] = ubyte_once<3>(dd); break;
                     }
                 }
-            } else {
-                // push form: window pixel t (intermediate pixel 2x - 5 + t) feeds output k
-                // with tap t - 2k; only the K x B accumulators stay live
-                auto tap = [&](int k) -> float {
-                    const int m = k < 6 ? k : 11 - k;
-                    return m == 0 ? t0 : m == 1 ? t1 : m == 2 ? t2 : m == 3 ? t3 : m == 4 ? t4 : t5;
-                };
 #pragma unroll
-                for (int k = 0; k < K; ++k)
+                for (int k = 0; k < K; ++k) {
+                    const int kk = t - 2 * k;
+                    if (kk < 0 || kk > 11) continue;
+                    const float tk = tap(kk);
 #pragma unroll
-                    for (int c = 0; c < B; ++c) o[k][c] = bias;
-#pragma unroll
-                for (int t = 0; t < 2 * K + 10; ++t) {
-                    float v[B];
-#pragma unroll
-                    for (int c = 0; c < B; ++c) {
-                        const int lb = B * t + c + G::OFF0;
-                        const uint32_t dd = win[lb >> 2];
-                        switch (lb & 3) {
-                            case 0: v[c] = ubyte_once<0>(dd); break;
-                            case 1: v[c] = ubyte_once<1>(dd); break;
-                            case 2: v[c] = ubyte_once<2>(dd); break;
-                            default: v[c] = ubyte_once<3>(dd); break;
-                        }
-                    }
-#pragma unroll
-                    for (int k = 0; k < K; ++k) {
-                        const int kk = t - 2 * k;
-                        if (kk < 0 || kk > 11) continue;
-                        const float tk = tap(kk);
-#pragma unroll
-                        for (int c = 0; c < B; ++c) o[k][c] = __builtin_fmaf(tk, v[c], o[k][c]);
-                    }
+                    for (int c = 0; c < B; ++c) o[k][c] = __builtin_fmaf(tk, v[c], o[k][c]);
                 }
             }
             u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
@@ -714,15 +565,15 @@ __device__ __forceinline__ void reduce2c_tile(const Reduce2cArgs &a, int img, in
     }
 }
 
-template <int B, int VM, int HM>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VM == 4 ? 5 : 1, 8))) k_reduce2c(Reduce2cArgs a) {
+template <int B>
+__global__ void __launch_bounds__(256) k_reduce2c(Reduce2cArgs a) {
     __shared__ uint32_t lds[2 * kR * R2C<B>::kPitch];
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = t % a.n_strips;
     const int rest = t / a.n_strips;
     const int band = rest % a.n_bands;
     const int img = rest / a.n_bands;
-    reduce2c_tile<B, VM, HM>(a, img, strip, band, lds);
+    reduce2c_tile<B>(a, img, strip, band, lds);
 }
 
 // Variant bits (A/B in one process via MIPX_R2_VARIANT; default = best measured):
@@ -901,6 +752,8 @@ bool reduce2c_taps(float t[6]) {
 // are dword aligned: k_reduce2x2 at the corner convention, k_reduce2c at the centre one.
 bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
     if (hs != 2.0 || vs != 2.0) return false;
+    const char *e2 = tune_env("MIPX_REDUCE2");  // 0: leave 2 x 2 to the generic reduce (A/B)
+    if (e2 && *e2 == '0') return false;
     if (b != 3 && b != 4) return false;
     if ((w * b) % 4 != 0 || (reinterpret_cast<uintptr_t>(in) % 4) != 0) return false;
     if (w < 8 || h < 8) return false;
@@ -917,10 +770,8 @@ static int reduce2c_window_launch(const u8 *in, u8 *out, int n, int w, int h, in
                                   hipStream_t st) {
     Reduce2cArgs a{};
     if (!reduce2c_taps(a.t)) return MIPX_EINVAL;
-    float sum = 0.0f;
-    for (float &t : a.t) sum += 2.0f * t, t /= 4096.0f;
+    for (float &t : a.t) t /= 4096.0f;
     a.bias = 1.0f / 8192.0f;
-    a.seed = a.bias - 1024.0f * sum / 4096.0f;
     a.in = in;
     a.out = out;
     a.w = w;
@@ -943,34 +794,15 @@ static int reduce2c_window_launch(const u8 *in, u8 *out, int n, int w, int h, in
     a.out_img = img_bytes(a.ow, a.oh, b);
     const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
-    // A/B knobs: MIPX_R2C_VM=1 the f32 ring vertical pass, MIPX_R2C_HM=0 the f32 push
-    // horizontal pass (defaults: both on v_dot2_f32_f16)
-    const char *ev = tune_env("MIPX_R2C_VM");
-    const char *eh = tune_env("MIPX_R2C_HM");
-    const int vm = (ev && *ev >= '0' && *ev <= '4') ? *ev - '0' : 2;
-    const int hm = (eh && *eh == '0') ? 0 : (eh && *eh == '2') ? 2 : 1;
     const dim3 grid(static_cast<unsigned>(tiles)), blk(256);
-#define MIPX_R2C(BB)                                                                             \
-    if (vm == 0) hipLaunchKernelGGL((k_reduce2c<BB, 0, 2>), grid, blk, 0, st, a);                \
-    else if (vm == 1 && hm == 0) hipLaunchKernelGGL((k_reduce2c<BB, 1, 0>), grid, blk, 0, st, a);     \
-    else if (vm == 1) hipLaunchKernelGGL((k_reduce2c<BB, 1, 1>), grid, blk, 0, st, a);           \
-    else if (vm == 3 && hm == 0) hipLaunchKernelGGL((k_reduce2c<BB, 3, 0>), grid, blk, 0, st, a); \
-    else if (vm == 4) hipLaunchKernelGGL((k_reduce2c<BB, 4, 0>), grid, blk, 0, st, a);           \
-    else if (vm == 3) hipLaunchKernelGGL((k_reduce2c<BB, 3, 1>), grid, blk, 0, st, a);           \
-    else if (hm == 0) hipLaunchKernelGGL((k_reduce2c<BB, 2, 0>), grid, blk, 0, st, a);           \
-    else hipLaunchKernelGGL((k_reduce2c<BB, 2, 1>), grid, blk, 0, st, a);
-    if (b == 3) {
-        MIPX_R2C(3)
-    } else {
-        MIPX_R2C(4)
-    }
-#undef MIPX_R2C
+    if (b == 3) hipLaunchKernelGGL((k_reduce2c<3>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((k_reduce2c<4>), grid, blk, 0, st, a);
     return launch_check("k_reduce2c");
 }
 
 // k_reduce2x2 build variant.  Only the shipped one (66) is compiled now; the r01 / r02
 // A/B builds (strip widths, register prefetch, LDS row strides) are recorded under
-// profiles/r01 and profiles/r02 (scripts/ab_reduce.py ran them).
+// profiles/r01 and profiles/r02 (scripts/ab_reduce.py, in git history, ran them).
 constexpr int kR2Default = 66;  // wide strips, R = 12 + register prefetch: measured best (profiles/r01/v10_wide_ab.log)
 int reduce2_variant() {
     const char *e = tune_env("MIPX_R2_VARIANT");

@@ -70,16 +70,11 @@ def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
 
 
-@pytest.mark.parametrize("var", ["dot", "ring", "vdot_hpush", "vring_hdot", "vmix_hpush", "vmix_hdot", "vpk_hpush"])
-def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, var, monkeypatch):
-    """The fused 2x2 kernels (corner: k_reduce2x2 variant 66, the r01/r02 A/B builds
-    are recorded under profiles/ and no longer compiled; centre: k_reduce2c with
-    v_dot2_f32_f16 on f16 pixel pairs in both passes, or the f32 ring / push passes behind
-    MIPX_R2C_VM=1 / MIPX_R2C_HM=0) are bit-exact, including strips that end at the image
-    edge, images shorter than a band and the smallest eligible sizes."""
-    monkeypatch.setenv("MIPX_R2C_VM", "1" if var in ("ring", "vring_hdot") else "3" if "vmix" in var else
-                       "4" if "vpk" in var else "2")
-    monkeypatch.setenv("MIPX_R2C_HM", "0" if "hpush" in var or var == "ring" else "1")
+def test_reduce2x2_variants_exact(gpu, oracle, rng, convention):
+    """The fused 2x2 kernels (corner: k_reduce2x2 variant 66, the r01/r02 A/B builds are
+    recorded under profiles/ and no longer compiled; centre: k_reduce2c) are bit-exact,
+    including strips that end at the image edge, images shorter than a band and the
+    smallest eligible sizes."""
     for h, w, b in ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1001 * 4 // 4 - 1, 4), (200, 646, 3),
                     (8, 8, 4), (9, 12, 3), (25, 164, 3), (131, 1000, 4), (1081, 324, 3), (16, 3840, 3)):
         if (w * b) % 4:
@@ -87,7 +82,7 @@ def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, var, monkeypatch
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
         got = gpu.run_op("reduce", imgs, hshrink=2.0, vshrink=2.0)
         for i in range(2):
-            assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"{convention} {var} {h}x{w}x{b} img{i}")
+            assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"{convention} {h}x{w}x{b} img{i}")
 
 
 @pytest.mark.parametrize("fused", ["0", "1"])
@@ -209,9 +204,10 @@ def test_extract_rot_flip(gpu, oracle, rng, b):
 @pytest.mark.parametrize("nt", ["0", "1"])
 @pytest.mark.parametrize("b", [1, 2, 3, 4])
 def test_extract_batches_any_alignment(gpu, oracle, rng, monkeypatch, b, nt):
-    monkeypatch.setenv("MIPX_EXTRACT_NT", nt)  # row copies with plain / non-temporal stores
     """Extract over batches of odd-size images (later images start unaligned) and odd
-    windows: the dword copy, the embed-interior path and the per-pixel remap."""
+    windows: the dword copy, the embed-interior path and the per-pixel remap, with plain
+    and non-temporal row stores (MIPX_EXTRACT_NT)."""
+    monkeypatch.setenv("MIPX_EXTRACT_NT", nt)
     for h, w, left, top, ow, oh in ((37, 53, 5, 7, 31, 20), (40, 64, 4, 3, 32, 16), (29, 301, 101, 2, 157, 25)):
         imgs = np.stack([rand_img(rng, h, w, b) for _ in range(3)])
         got = gpu.run_op("extract", imgs, left=left, top=top, width=ow, height=oh)
