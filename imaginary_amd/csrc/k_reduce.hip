@@ -823,7 +823,19 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
 // Every computed pixel is the same sum as in the full launch.
 int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x0, int y0, int x1, int y1,
                           hipStream_t st) {
-    if (reduce_centre()) return reduce2c_window_launch(in, out, n, w, h, b, x0, y0, x1, y1, st);
+    if (reduce_centre()) {
+        // k_reduce2m (vertical products on the matrix cores) by default; MIPX_R2M=0 keeps
+        // the all-VALU k_reduce2c (A/B)
+        const char *em = tune_env("MIPX_R2M");
+        float tf[6];
+        if (!(em && *em == '0') && reduce2c_taps(tf)) {
+            int taps[12];
+            for (int i = 0; i < 6; ++i) taps[i] = taps[11 - i] = static_cast<int>(tf[i]);
+            const int e = reduce2m_window_launch(in, out, n, w, h, b, x0, y0, x1, y1, taps, st);
+            if (e != MIPX_EUNSUPPORTED) return e;
+        }
+        return reduce2c_window_launch(in, out, n, w, h, b, x0, y0, x1, y1, st);
+    }
     float c[4];
     if (!reduce2_taps(c)) return MIPX_EINVAL;
     Reduce2Args a{};

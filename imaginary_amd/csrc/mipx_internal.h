@@ -151,6 +151,10 @@ bool reduce2_eligible(const uint8_t *in, int w, int h, int b, double hs, double 
 int reduce2_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, hipStream_t st);
 int reduce2_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int x0, int y0, int x1,
                           int y1, hipStream_t st);
+// k_reduce2m.hip: the centre-convention 2 x 2 reduce with its vertical pass on the matrix
+// cores; taps12 = matrixi[64][0..11]
+int reduce2m_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int x0, int y0, int x1,
+                           int y1, const int *taps12, hipStream_t st);
 // k_shrink.hip
 int shrink_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int hs, int vs, hipStream_t st);
 int shrink_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int hs, int vs, int x0, int y0,
