@@ -355,7 +355,10 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
     const char *es = tune_env("MIPX_AFFINE_SEP");  // 0: the per-pixel gather kernel (A/B)
     if (!(es && *es == '0') && n <= 65535) {
         auto ixh = [](int o, double s) { return static_cast<int>((o + 0.5) / s - 0.5 + 1.0); };
+        const char *et = tune_env("MIPX_AFFINE_TY");  // first tile height tried: 32 / 16 / 8 (A/B)
+        const int ty0 = (et && *et) ? std::atoi(et) : 32;
         for (const int ty : {32, 16, 8}) {
+            if (ty > ty0) continue;
             int ncols = 0, nrows = 0;
             for (int x0 = 0; x0 < a.ow; x0 += kAfTX)
                 ncols = std::max(ncols, ixh(std::min(x0 + kAfTX, a.ow) - 1, xs) - ixh(x0, xs) + 4);

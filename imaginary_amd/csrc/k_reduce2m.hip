@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #include "device_common.h"
 #include "lds_ops.h"
@@ -39,7 +40,6 @@ using namespace dev;
 
 constexpr int kMTW = 64;    // output pixels per strip
 constexpr int kMN = 16;     // output rows per step (the MFMA N)
-constexpr int kMRing = 64;  // staged input rows (slot = row & 63)
 constexpr int kMNT = 256;
 
 template <int B>
@@ -50,6 +50,7 @@ struct R2M {
     static constexpr int CPR = (OFF + B * (2 * kMTW + 10) + 15) / 16;  // 16-byte chunks per staged row
     static constexpr int RS = B == 3 ? 432 : 592;            // row stride: (RS / 4 mod 64) / 4 odd
     static constexpr int KM = (32 * CPR + kMNT - 1) / kMNT;  // chunks per lane per step (32 rows)
+    static constexpr int OS = B == 3 ? 208 : 272;            // HM output tile row stride (conflict-free)
     static_assert(RS >= 16 * CPR + ISH, "row stride");
     static_assert(((RS / 4) % 64 / 4) % 2 == 1, "conflict-free transposed reads");
 };
@@ -63,18 +64,24 @@ struct R2mArgs {
     int n_strips, n_bands, band_steps;
     long long in_img, out_img;
     int seed;               // 128 sum(T) + 2048
-    int tap[12];            // T_0..T_11 = matrixi[64][0..11]
+    const rc_u4 *ops;       // [64 lanes][bh, bl, wh, wl]: the MFMA tap operands (r2m_operands)
     float tf[6];            // T_0..T_5 / 4096 for the horizontal pass (T_11-i = T_i)
     float bias;             // 2^-13
 };
 
-template <int B>
+// RG: staged input rows in the ring (slot = row mod RG; a step reads 42 rows and stages
+// the next 32 once they are read, so any RG >= 42 holds them; smaller rings let more
+// workgroups share a CU)
+template <int B, bool HM, int RG>
 __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     using G = R2M<B>;
     constexpr int K = G::K, RS = G::RS, CPR = G::CPR, KM = G::KM;
-    __shared__ __attribute__((aligned(16))) u8 smem[(kMRing + kMN) * RS];
-    const uint32_t ring_l = rc_lds(smem), inter_l = ring_l + kMRing * RS;
-    u8 *inter = smem + kMRing * RS;
+    static_assert(RG >= 42, "ring holds a step's rows");
+    __shared__ __attribute__((aligned(16))) u8 smem[(RG + kMN) * RS + (HM ? kMN * G::OS : 0)];
+    const uint32_t ring_l = rc_lds(smem), inter_l = ring_l + RG * RS;
+    u8 *inter = smem + RG * RS;
+    const uint32_t otile_l = inter_l + kMN * RS;  // HM: [16 rows][OS]; wave w owns bytes 4 (16 w) B ..
+    auto slot = [](int r) { return static_cast<uint32_t>(r + 2 * RG) % static_cast<uint32_t>(RG); };  // r >= -5
 
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
     const int strip = static_cast<int>(t % static_cast<uint32_t>(a.n_strips)) + a.s_base;
@@ -119,30 +126,20 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
 #pragma unroll
         for (int j = 0; j < KM; ++j)
             if (rr[j] < nrows)
-                lds_wr128(ring_l + static_cast<uint32_t>(((r0 + rr[j]) & (kMRing - 1)) * RS) + lof[j],
+                lds_wr128(ring_l + slot(r0 + rr[j]) * RS + lof[j],
                           v[j] ^ 0x80808080u);
     };
 
-    // ---- B operand: output row n, K = 16 kg + e <-> staged row 8 kg + e (e < 8) or
-    // 32 + 8 kg + e - 8, tap i = row - 2n (T = 64 hi + lo) ----
-    rc_v4i bh, bl;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t hw = 0, lw = 0;
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-            const int e = 4 * q + e4;
-            const int row = e < 8 ? 8 * kg + e : 32 + 8 * kg + e - 8;
-            const int i = row - 2 * n;
-            const int tv = (i >= 0 && i < 12) ? a.tap[i] : 0;
-            const int hi = tv >> 6, lo = tv - 64 * hi;  // floor split: lo in [0, 63]
-            hw |= (static_cast<uint32_t>(hi) & 0xffu) << (8 * e4);
-            lw |= (static_cast<uint32_t>(lo) & 0xffu) << (8 * e4);
-        }
-        bh[q] = static_cast<int>(hw);
-        bl[q] = static_cast<int>(lw);
+    // ---- the tap operands of both products (host-built, r2m_operands) ----
+    const rc_u4 *op = a.ops + 4 * lane;
+    const rc_v4i bh = __builtin_bit_cast(rc_v4i, op[0]), bl = __builtin_bit_cast(rc_v4i, op[1]);
+    rc_v4i wh{0, 0, 0, 0}, wl{0, 0, 0, 0};
+    if (HM) {
+        wh = __builtin_bit_cast(rc_v4i, op[2]);
+        wl = __builtin_bit_cast(rc_v4i, op[3]);
     }
     const int sd = a.seed;
+    const bool row_al16 = ((a.ow * B) & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0;
 
     // ---- prime: the first step's 42 rows, then the next step's 32 into registers ----
     {
@@ -176,32 +173,39 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
         // ---- vertical: 16-byte column tiles dealt to the waves ----
         {
             const int r1 = bk + 8 * kg + (n >> 1);
-            const uint32_t a1 = ring_l + static_cast<uint32_t>((r1 & (kMRing - 1)) * RS + 8 * (n & 1));
-            const uint32_t a2 = ring_l + static_cast<uint32_t>(((r1 + 32) & (kMRing - 1)) * RS + 8 * (n & 1));
+            const uint32_t a1 = ring_l + slot(r1) * RS + 8 * (n & 1);
+            const uint32_t a2 = ring_l + slot(r1 + 32) * RS + 8 * (n & 1);
             const uint32_t iq = inter_l + static_cast<uint32_t>(n * RS + 4 * kg + G::ISH);
-            for (int ct = wave; ct < CPR; ct += 8) {
-                const bool two = ct + 4 < CPR;
-                rc_v2i p1 = lds_tr8(a1 + 16 * ct), p2 = lds_tr8(a2 + 16 * ct);
-                rc_v2i q1 = p1, q2 = p2;
-                if (two) {
-                    q1 = lds_tr8(a1 + 16 * (ct + 4));
-                    q2 = lds_tr8(a2 + 16 * (ct + 4));
+            auto tile = [&](int c, rc_v2i u1, rc_v2i u2) {
+                const rc_v4i av = rc_v4i{u1.x, u1.y, u2.x, u2.y};
+                rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
+                dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
+                dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
+                uint32_t lo, hi;
+                const int s0 = (dh[0] << 6) + dl[0], s1 = (dh[1] << 6) + dl[1];
+                const int s2 = (dh[2] << 6) + dl[2], s3 = (dh[3] << 6) + dl[3];
+                asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(s0), "v"(s1));
+                asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(s2), "v"(s3));
+                // HM: the intermediate is kept as byte - 128 (the horizontal MFMA's B operand)
+                lds_wr32(iq + 16 * c, __builtin_amdgcn_perm(hi, lo, 0x05040100u) ^ (HM ? 0x80808080u : 0u));
+            };
+            // four tiles per batch: their reads under one wait, their products interleaved
+            for (int c0 = wave; c0 < CPR; c0 += 16) {
+                rc_v2i p[4][2];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int ct = c0 + 4 * i;
+                    if (ct < CPR) {
+                        p[i][0] = lds_tr8(a1 + 16 * ct);
+                        p[i][1] = lds_tr8(a2 + 16 * ct);
+                    } else {
+                        p[i][0] = p[i][1] = rc_v2i{0, 0};
+                    }
                 }
-                lgkm_wait_for<0>(p1, p2, q1, q2);
-                auto tile = [&](int c, rc_v2i u1, rc_v2i u2) {
-                    const rc_v4i av = rc_v4i{u1.x, u1.y, u2.x, u2.y};
-                    rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
-                    dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
-                    dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
-                    uint32_t lo, hi;
-                    const int s0 = (dh[0] << 6) + dl[0], s1 = (dh[1] << 6) + dl[1];
-                    const int s2 = (dh[2] << 6) + dl[2], s3 = (dh[3] << 6) + dl[3];
-                    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(s0), "v"(s1));
-                    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(s2), "v"(s3));
-                    lds_wr32(iq + 16 * c, __builtin_amdgcn_perm(hi, lo, 0x05040100u));
-                };
-                tile(ct, p1, p2);
-                if (two) tile(ct + 4, q1, q2);
+                lgkm_wait_for<0>(p[0][0], p[0][1], p[1][0], p[1][1], p[2][0], p[2][1], p[3][0], p[3][1]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (c0 + 4 * i < CPR) tile(c0 + 4 * i, p[i][0], p[i][1]);
             }
         }
         rc_barrier();  // the intermediate complete; the ring's rows of step k read
@@ -220,6 +224,61 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                 inter[u * RS + ib0 + B * d + c] = inter[u * RS + ib0 + B * sp + c];
             }
             rc_barrier();
+        }
+        if (HM) {
+            // ---- horizontal on the matrix cores: D[out byte j][row u] = W[j][window byte] x
+            // inter[window byte][u]; a group = GP output pixels of all 16 rows ----
+            constexpr int GP = B == 3 ? 4 : 2, NG = kMTW / GP;
+            // wave w: groups GPW w .. (16 px); D dwords -> the wave's part of the output tile,
+            // then 16-byte row pieces to HBM
+            constexpr int GPW = NG / 4;
+            if (x0 + 16 * wave >= a.ow) continue;
+#pragma unroll
+            for (int gb = 0; gb < GPW; gb += 4) {
+                rc_v4i bv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t ws = static_cast<uint32_t>((ib0 & ~7) + 2 * B * GP * (GPW * wave + gb + i));
+                    bv[i] = __builtin_bit_cast(rc_v4i, lds_rd2x64(inter_l + static_cast<uint32_t>(n * RS) + ws + 16 * kg));
+                }
+                lgkm_wait_for<0>(bv[0], bv[1], bv[2], bv[3]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
+                    dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(wh, bv[i], dh, 0, 0, 0);
+                    dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(wl, bv[i], dl, 0, 0, 0);
+                    uint32_t lo, hi;
+                    const int s0 = (dh[0] << 6) + dl[0], s1 = (dh[1] << 6) + dl[1];
+                    const int s2 = (dh[2] << 6) + dl[2], s3 = (dh[3] << 6) + dl[3];
+                    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(s0), "v"(s1));
+                    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(s2), "v"(s3));
+                    if (4 * kg < B * GP)
+                        lds_wr32(otile_l + static_cast<uint32_t>(n * G::OS + 16 * B * wave + B * GP * (gb + i) + 4 * kg),
+                                 __builtin_amdgcn_perm(hi, lo, 0x05040100u));
+                }
+            }
+            {
+                constexpr int LPR = B;  // 16-byte pieces per tile row of a wave (16 px x B bytes)
+                const int u = lane / LPR, c = lane - u * LPR;
+                lgkm_wait();
+                if (u < kMN) {
+                    const rc_u4 v = lds_rd128(otile_l + static_cast<uint32_t>(u * G::OS + 16 * B * wave + 16 * c));
+                    lgkm_wait();
+                    const int y = kMN * k + u;
+                    const int xb = (x0 + 16 * wave) * B + 16 * c;
+                    const int rowb = a.ow * B;
+                    if (y < a.oh && xb < rowb) {
+                        u8 *q = dst + static_cast<size_t>(y) * rowb + xb;
+                        if (row_al16 && xb + 16 <= rowb) {
+                            *reinterpret_cast<rc_u4 *>(q) = v;
+                        } else {
+                            const int nb = min(16, rowb - xb);
+                            for (int e = 0; e < nb; ++e) q[e] = static_cast<u8>(v[e >> 2] >> (8 * (e & 3)));
+                        }
+                    }
+                }
+            }
+            continue;
         }
         // ---- horizontal: items of K output pixels, 14 window dwords each ----
         constexpr int ipr = kMTW / K;
@@ -311,6 +370,37 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     }
 }
 
+// The per-lane tap operands, [lane][bh, bl, wh, wl] x 16 bytes.  Lane (n = lane & 15,
+// kg = lane >> 4) holds K = 16 kg + e, e = 0..15 (the same labelling on both operands
+// of a product, so the contraction order is free):
+//   vertical B, output row n: K <-> staged row 8 kg + e (e < 8) or 32 + 8 kg + e - 8
+//     (the two ds_read_b64_tr_b8 of a column tile), tap i = row - 2 n;
+//   horizontal A, output byte j = n of a group (pixel j / B, channel j % B; j < B GP):
+//     K = window byte = SH + B (2 (j / B) + i) + j % B, SH = ib0 mod 8 (the window starts
+//     8-byte aligned).
+// Every tap T = 64 hi + lo (floor split: lo in [0, 63]), hi in bh / wh, lo in bl / wl.
+template <int B>
+std::vector<uint32_t> r2m_operands(const int *tap) {
+    using G = R2M<B>;
+    constexpr int GPB = B == 3 ? 12 : 8, SH = (G::OFF + G::ISH) & 7;
+    std::vector<uint32_t> v(64 * 16, 0);
+    for (int lane = 0; lane < 64; ++lane) {
+        const int n = lane & 15, kg = lane >> 4;
+        for (int e = 0; e < 16; ++e) {
+            const int row = e < 8 ? 8 * kg + e : 32 + 8 * kg + e - 8;
+            const int iv = row - 2 * n;
+            const int tv = (iv >= 0 && iv < 12) ? tap[iv] : 0;
+            const int r = 16 * kg + e - SH - n % B;
+            const int ih = r >= 0 && r % B == 0 ? r / B - 2 * (n / B) : -1;
+            const int th = (n < GPB && ih >= 0 && ih < 12) ? tap[ih] : 0;
+            const int t4[4] = {tv >> 6, tv - 64 * (tv >> 6), th >> 6, th - 64 * (th >> 6)};
+            for (int o = 0; o < 4; ++o)
+                v[16 * lane + 4 * o + e / 4] |= (static_cast<uint32_t>(t4[o]) & 0xffu) << (8 * (e % 4));
+        }
+    }
+    return v;
+}
+
 }  // namespace
 
 // k_reduce2m over the output region [x0, x1) x [y0, y1) of a 2 x 2 reduce at the centre
@@ -333,10 +423,12 @@ int reduce2m_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
     if (a.in_img >= 0x7fffffffLL - 64) return MIPX_EUNSUPPORTED;
     int sum = 0;
     for (int i = 0; i < 12; ++i) {
-        a.tap[i] = taps12[i];
         sum += taps12[i];
         if (taps12[i] < -128 * 64 || taps12[i] > 127 * 64 + 63) return MIPX_EUNSUPPORTED;  // i8 hi / lo split
     }
+    const std::vector<uint32_t> ops = b == 3 ? r2m_operands<3>(taps12) : r2m_operands<4>(taps12);
+    a.ops = static_cast<const rc_u4 *>(device_blob(ops.data(), ops.size() * sizeof(uint32_t)));
+    if (!a.ops) return MIPX_EDEVICE;
     for (int i = 0; i < 6; ++i) a.tf[i] = static_cast<float>(taps12[i]) / 4096.0f;
     a.bias = 1.0f / 8192.0f;
     a.seed = 128 * sum + 2048;
@@ -352,8 +444,27 @@ int reduce2m_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
     const long long blocks = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const dim3 grid(static_cast<unsigned>(blocks)), blk(kMNT);
-    if (b == 3) hipLaunchKernelGGL(k_reduce2m<3>, grid, blk, 0, st, a);
-    else hipLaunchKernelGGL(k_reduce2m<4>, grid, blk, 0, st, a);
+    const char *eh = tune_env("MIPX_R2M_H");  // 0: horizontal pass on the VALU (A/B)
+    const bool hm = !(eh && *eh == '0');
+    const char *eg = tune_env("MIPX_R2M_RING");  // staged rows in the ring: 42 / 48 / 64 (A/B)
+    const int rg = (eg && *eg) ? std::atoi(eg) : 48;
+#define MIPX_R2M_GO(B_)                                                                          \
+    if (rg == 42) {                                                                              \
+        if (hm) hipLaunchKernelGGL((k_reduce2m<B_, true, 42>), grid, blk, 0, st, a);            \
+        else hipLaunchKernelGGL((k_reduce2m<B_, false, 42>), grid, blk, 0, st, a);              \
+    } else if (rg == 64) {                                                                       \
+        if (hm) hipLaunchKernelGGL((k_reduce2m<B_, true, 64>), grid, blk, 0, st, a);            \
+        else hipLaunchKernelGGL((k_reduce2m<B_, false, 64>), grid, blk, 0, st, a);              \
+    } else {                                                                                     \
+        if (hm) hipLaunchKernelGGL((k_reduce2m<B_, true, 48>), grid, blk, 0, st, a);            \
+        else hipLaunchKernelGGL((k_reduce2m<B_, false, 48>), grid, blk, 0, st, a);              \
+    }
+    if (b == 3) {
+        MIPX_R2M_GO(3)
+    } else {
+        MIPX_R2M_GO(4)
+    }
+#undef MIPX_R2M_GO
     return launch_check("k_reduce2m");
 }
 

@@ -99,6 +99,8 @@ const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt | 257 y2
 const int *device_bicubic_table();     // 129 x 4
 // float copy of the integer gaussmat mask; *scale = mask sum
 const float *device_gauss_table(double sigma, double min_ampl, int *n_taps, int *scale);
+// `bytes` of host data on the current device, cached by contents (small constant tables)
+const void *device_blob(const void *data, size_t bytes);
 void free_device_tables();
 
 // ---- generic separable passes (k_sep.hip) -----------------------------------
