@@ -11,7 +11,7 @@ device memory, the stream, and a gloo barrier / max-reduce for the timing.
 
 A step = one mipx_execute_dev() of the bimg plan for /resize?width=1920&height=1080
 on a 3840x2160x3 decoded image (one Lanczos3 reduce 2x2: the fused k_reduce2x2 at the
-corner sampling convention, k_reduce2c at the centre one) over the whole resident batch.
+corner sampling convention, k_reduce2m at the centre one) over the whole resident batch.
 """
 import argparse
 import json
@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 # the kernel C2 runs under each reduce sampling convention (PARITY_ASSUMPTIONS.md row 1):
 # its roofline and PMC traffic record are this kernel's
-C2_KERNEL = {"corner": "k_reduce2x2<3, 66>", "centre": "k_reduce2c<3>"}
+C2_KERNEL = {"corner": "k_reduce2x2<3, 66>", "centre": "k_reduce2m<3>"}
 
 def parse():
     ap = argparse.ArgumentParser()

@@ -332,249 +332,9 @@ __device__ __forceinline__ void reduce2_tile(const Reduce2Args &a, int img, int 
     }
 }
 
-// ===========================================================================
-// The same fused 2 x 2 reduce under libvips' centre sampling convention
-// (PARITY_ASSUMPTIONS.md row 1 flipped: X = (o + 0.5) * 2 - 0.5 = 2o + 0.5).
-//
-// Every output then sits at phase 64 (x = 0.5): tap i of the 13-point mask lies at
-// (i - 5.5) / 2, so taps 0..11 are the Lanczos lobe at +-0.25 .. +-2.75 and tap 12
-// (3.25) is zero; the host checks that shape (and the symmetry T_i = T_11-i) on the
-// integer table before choosing this kernel.  Output o of either pass is
-//     o = sum_{i=0..11} T_i p[2o - 5 + i] = sum_{k=0..5} T_k (p[2o - 5 + k] + p[2o + 6 - k])
-// Twelve multiply-adds per byte and pass instead of the corner convention's seven,
-// and that arithmetic, not HBM, bounds the kernel (a memory-only build
-// of the same access pattern streams 1.25x faster).
-//  * Vertical: lane t owns dword t of the strip (channel agnostic) and keeps the 12
-//    rows of the current window converted to f32 in a register ring (slot = row mod
-//    12; a 12-row chunk adds 24 rows = two ring periods, so every slot index is a
-//    compile-time constant); six pair sums and six v_fma_f32 per byte.
-//  * Horizontal: an item of K output pixels reads the 2K + 10 intermediate pixels it
-//    needs (14 dwords for RGB and RGBA) and pushes each converted pixel into the
-//    K x B accumulators it feeds (12 v_fma_f32 per output byte; only the accumulators
-//    stay live, so the kernel fits 96 VGPRs and 5 workgroups per CU).
-// All multiply-adds are plain f32 ops: the packed v_pk_add_f32 / v_pk_fma_f32, the
-// f16 v_dot2c_f32_f16 and v_fma_mix_f32 forms were built, bit-exact, and slower
-// (profiles/r04/reduce2c/, issue costs in profiles/r04/valu_rate_probe.jsonl).
-// Same strips / bands as k_reduce2x2<B, 66>, so execute_plan's demand windows round to
-// the same tiles.
-// ===========================================================================
-template <int B>
-struct R2C {
-    static constexpr int kThreads = 256, kPitch = 288;
-    static constexpr int TW = B == 3 ? 160 : 120;      // = R2<B, 1>::TW
-    static constexpr int NPX = 2 * TW + 10;            // intermediate px 2x0-5 .. 2x0+2TW+4
-    static constexpr int K = B == 3 ? 4 : 2;
-    static constexpr int OFF0 = B == 3 ? 1 : 0;
-    static constexpr int ND = (B * NPX + OFF0 + 3) / 4;
-    static constexpr int WD = (B * (2 * K + 10) + OFF0 + 3) / 4;  // window dwords per item
-    static_assert(ND <= kThreads && ND <= kPitch, "strip too wide");
-    static_assert(WD == 14, "item window");
-    static_assert(TW == R2<B, 1>::TW, "same tiles as the corner kernel");
-};
-
-struct Reduce2cArgs {
-    const u8 *in;
-    u8 *out;
-    int w, h, ow, oh;
-    int n_strips, n_bands, band_rows;
-    int s_base, y_base, x_end, y_end;
-    long long in_img, out_img;
-    float t[6];   // T_0..T_5 = matrixi[64][0..5] / 4096 (exact; T_11-i = T_i)
-    float bias;   // 2^-13: RNE(sum/4096 + 2^-13) == floor(sum/4096 + 0.5)
-};
-
-// four byte columns as scalar floats: the multiply-adds stay plain v_fma_f32
-struct S4 {
-    float x, y, z, w;
-};
-__device__ __forceinline__ S4 cvt4s(uint32_t v) {
-    return S4{ubyte_once<0>(v), ubyte_once<1>(v), ubyte_once<2>(v), ubyte_once<3>(v)};
-}
-__device__ __forceinline__ S4 fma4(float t, const S4 &r, const S4 &acc) {
-    return S4{__builtin_fmaf(t, r.x, acc.x), __builtin_fmaf(t, r.y, acc.y), __builtin_fmaf(t, r.z, acc.z),
-              __builtin_fmaf(t, r.w, acc.w)};
-}
-__device__ __forceinline__ S4 add4(const S4 &a, const S4 &b) { return S4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
-
-template <int B>
-__device__ __forceinline__ void reduce2c_tile(const Reduce2cArgs &a, int img, int strip, int band, uint32_t *lds) {
-    using G = R2C<B>;
-    constexpr int kThreads = G::kThreads, kPitch = G::kPitch, TW = G::TW, K = G::K, R = kR;
-    const int tid = threadIdx.x;
-    const int x0 = (a.s_base + strip) * TW;
-    const int row_bytes = a.w * B;
-    const int px0 = 2 * x0 - 5;
-    const int base = (B * px0) & ~3;
-    const int byte0 = base + 4 * tid;
-    const bool vlane = tid < G::ND && byte0 >= 0 && byte0 + 4 <= row_bytes;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<u8 *>(a.in + img * a.in_img), 0, static_cast<int>(a.in_img), 0x00020000);
-    const uint32_t voff = vlane ? static_cast<uint32_t>(byte0) : 0x80000000u;
-    const int y0 = a.y_base + band * a.band_rows;  // a multiple of 12: 2 * y0 == 0 (mod 12)
-    const int y1 = min(y0 + a.band_rows, a.y_end);
-    const float t0 = a.t[0], t1 = a.t[1], t2 = a.t[2], t3 = a.t[3], t4 = a.t[4], t5 = a.t[5], bias = a.bias;
-    auto tap = [&](int k) -> float {  // T_k of the symmetric 12-tap mask
-        const int m = k < 6 ? k : 11 - k;
-        return m == 0 ? t0 : m == 1 ? t1 : m == 2 ? t2 : m == 3 ? t3 : m == 4 ? t4 : t5;
-    };
-    const int nl = px0 < 0 ? -px0 : 0;
-    const int x_last = min(x0 + TW, a.x_end) - 1;
-    const int fr = a.w - px0;
-    const int fr_end = min(2 * x_last + 6 - px0, G::NPX - 1);
-    const int nr = fr_end >= fr ? fr_end - fr + 1 : 0;
-    const bool edge = nl > 0 || nr > 0;
-
-    auto load_row = [&](int r) -> uint32_t {
-        r = clampi(r, 0, a.h - 1);
-        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, r * row_bytes, 0));
-    };
-
-    // ring slot s holds input row 2 yc + d, d == s (mod 12)
-    S4 ring[12];
-    const S4 BI = {bias, bias, bias, bias};
-#pragma unroll
-    for (int d = -5; d <= 4; ++d) ring[(d + 12) % 12] = cvt4s(load_row(2 * y0 + d));
-    uint32_t nx[R], ny[R];  // rows 2o + 5 and 2o + 6 of output row o = yc + u
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-        nx[u] = load_row(2 * (y0 + u) + 5);
-        ny[u] = load_row(2 * (y0 + u) + 6);
-    }
-    int buf = 0;
-    for (int yc = y0; yc < y1; yc += R, buf ^= 1) {
-        uint32_t *L = lds + buf * (R * kPitch);
-        const bool more = yc + R < y1;
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-            ring[(2 * u + 5) % 12] = cvt4s(nx[u]);
-            ring[(2 * u + 6) % 12] = cvt4s(ny[u]);
-            if (more) {  // this register now fetches the next chunk's row
-                nx[u] = load_row(2 * (yc + R + u) + 5);
-                ny[u] = load_row(2 * (yc + R + u) + 6);
-            }
-            // pair k: rows 2o - 5 + k and 2o + 6 - k
-#define RC_LO(k) ring[(2 * u + 7 + (k)) % 12]
-#define RC_HI(k) ring[(2 * u + 6 - (k) + 12) % 12]
-            S4 acc = fma4(t5, add4(RC_LO(5), RC_HI(5)), BI);
-            acc = fma4(t4, add4(RC_LO(4), RC_HI(4)), acc);
-            acc = fma4(t3, add4(RC_LO(3), RC_HI(3)), acc);
-            acc = fma4(t2, add4(RC_LO(2), RC_HI(2)), acc);
-            acc = fma4(t1, add4(RC_LO(1), RC_HI(1)), acc);
-            acc = fma4(t0, add4(RC_LO(0), RC_HI(0)), acc);
-#undef RC_LO
-#undef RC_HI
-            if (tid < G::ND) L[u * kPitch + tid] = pack4b(acc.x, acc.y, acc.z, acc.w);
-        }
-        if (edge) {  // EXTEND_COPY inside the LDS image
-            __syncthreads();
-            u8 *Lb = reinterpret_cast<u8 *>(L);
-            const int nfill = nl + nr;
-            for (int i = tid; i < R * nfill * B; i += kThreads) {
-                const int u = i / (nfill * B);
-                const int rem = i - u * nfill * B;
-                const int f = rem / B, c = rem - f * B;
-                const int dst = f < nl ? f : fr + (f - nl);
-                const int srcp = f < nl ? nl : fr - 1;
-                Lb[u * kPitch * 4 + B * dst + G::OFF0 + c] = Lb[u * kPitch * 4 + B * srcp + G::OFF0 + c];
-            }
-        }
-        __syncthreads();
-        constexpr int items_per_row = TW / K;
-        for (int it = tid; it < R * items_per_row; it += kThreads) {
-            const int u = it / items_per_row;
-            const int j = it - u * items_per_row;
-            const int x = x0 + K * j;
-            const int y = yc + u;
-            if (y >= a.y_end || x >= a.x_end) continue;
-            const uint32_t *row = L + u * kPitch;
-            constexpr int W0 = (B * 2 * K) / 4;
-            uint32_t win[14];
-            if (B == 3) {
-                const uint2 *r2 = reinterpret_cast<const uint2 *>(row + W0 * j);
-#pragma unroll
-                for (int q = 0; q < 7; ++q) {
-                    const uint2 dd = r2[q];
-                    win[2 * q] = dd.x;
-                    win[2 * q + 1] = dd.y;
-                }
-            } else {
-                const uint4 *r4 = reinterpret_cast<const uint4 *>(row + W0 * j);
-#pragma unroll
-                for (int q = 0; q < 3; ++q) {
-                    const uint4 dd = r4[q];
-                    win[4 * q] = dd.x, win[4 * q + 1] = dd.y, win[4 * q + 2] = dd.z, win[4 * q + 3] = dd.w;
-                }
-                const uint2 dd = *reinterpret_cast<const uint2 *>(row + W0 * j + 12);
-                win[12] = dd.x;
-                win[13] = dd.y;
-            }
-            // window pixel t (intermediate pixel 2x - 5 + t) feeds output k with tap t - 2k
-            float o[K][B];
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-#pragma unroll
-                for (int c = 0; c < B; ++c) o[k][c] = bias;
-#pragma unroll
-            for (int t = 0; t < 2 * K + 10; ++t) {
-                float v[B];
-#pragma unroll
-                for (int c = 0; c < B; ++c) {
-                    const int lb = B * t + c + G::OFF0;
-                    const uint32_t dd = win[lb >> 2];
-                    switch (lb & 3) {
-                        case 0: v[c] = ubyte_once<0>(dd); break;
-                        case 1: v[c] = ubyte_once<1>(dd); break;
-                        case 2: v[c] = ubyte_once<2>(dd); break;
-                        default: v[c] = ubyte_once<3>(dd); break;
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    const int kk = t - 2 * k;
-                    if (kk < 0 || kk > 11) continue;
-                    const float tk = tap(kk);
-#pragma unroll
-                    for (int c = 0; c < B; ++c) o[k][c] = __builtin_fmaf(tk, v[c], o[k][c]);
-                }
-            }
-            u8 *q = a.out + img * a.out_img + (static_cast<size_t>(y) * a.ow + x) * B;
-            const bool full = x + K <= a.ow;
-            if (B == 3) {
-                const uint32_t d0 = pack4b(o[0][0], o[0][1], o[0][2], o[1][0]);
-                const uint32_t d1 = pack4b(o[1][1], o[1][2], o[2][0], o[2][1]);
-                const uint32_t d2 = pack4b(o[2][2], o[3][0], o[3][1], o[3][2]);
-                if (full && (reinterpret_cast<uintptr_t>(q) & 3u) == 0) {
-                    *reinterpret_cast<uint3 *>(q) = uint3{d0, d1, d2};
-                } else {
-                    const uint32_t dd[3] = {d0, d1, d2};
-                    const int nb = (full ? K : a.ow - x) * B;
-                    for (int i = 0; i < nb; ++i) q[i] = static_cast<u8>(dd[i >> 2] >> (8 * (i & 3)));
-                }
-            } else {
-                const uint32_t d0 = pack4b(o[0][0], o[0][1], o[0][2], o[0][3]);
-                const uint32_t d1 = pack4b(o[1][0], o[1][1], o[1][2], o[1][3]);
-                uint32_t *q32 = reinterpret_cast<uint32_t *>(q);
-                if (full && (reinterpret_cast<uintptr_t>(q) & 7u) == 0) {
-                    *reinterpret_cast<uint2 *>(q) = uint2{d0, d1};
-                } else {
-                    q32[0] = d0;
-                    if (full) q32[1] = d1;
-                }
-            }
-        }
-    }
-}
-
-template <int B>
-__global__ void __launch_bounds__(256) k_reduce2c(Reduce2cArgs a) {
-    __shared__ uint32_t lds[2 * kR * R2C<B>::kPitch];
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int strip = t % a.n_strips;
-    const int rest = t / a.n_strips;
-    const int band = rest % a.n_bands;
-    const int img = rest / a.n_bands;
-    reduce2c_tile<B>(a, img, strip, band, lds);
-}
+// The centre sampling convention's 2 x 2 reduce is k_reduce2m (k_reduce2m.hip); its
+// all-VALU predecessor k_reduce2c (r04, 1.84-1.88 ms per C2 step) was removed once the
+// matrix-core kernel beat it, its measurements are under profiles/r04/reduce2c/.
 
 // Variant bits (A/B in one process via MIPX_R2_VARIANT; default = best measured):
 // bit 0: R = 6 (else 12), bit 1: register prefetch of the next chunk,
@@ -733,7 +493,7 @@ bool reduce2_taps(float c[4]) {
 }
 
 // The centre convention's phase-64 mask: 12 non-zero taps symmetric about 5.5 and a
-// zero tap 12 (k_reduce2c).  Returns t_0..t_5.
+// zero tap 12 (k_reduce2m).  Returns t_0..t_5.
 bool reduce2c_taps(float t[6]) {
     std::vector<int> tab;
     reduce_table(2.0, tab);
@@ -749,7 +509,7 @@ bool reduce2c_taps(float t[6]) {
 }
 
 // Fused path applies to shrink exactly 2 x 2 on 3- or 4-band images whose rows
-// are dword aligned: k_reduce2x2 at the corner convention, k_reduce2c at the centre one.
+// are dword aligned: k_reduce2x2 at the corner convention, k_reduce2m at the centre one.
 bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
     if (hs != 2.0 || vs != 2.0) return false;
     const char *e2 = tune_env("MIPX_REDUCE2");  // 0: leave 2 x 2 to the generic reduce (A/B)
@@ -763,41 +523,6 @@ bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
     }
     static const bool shape_ok = [] { float c[4]; return reduce2_taps(c); }();
     return shape_ok;
-}
-
-// k_reduce2c over the output region [x0, x1) x [y0, y1) (same tiles as k_reduce2x2<B, 66>)
-static int reduce2c_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x0, int y0, int x1, int y1,
-                                  hipStream_t st) {
-    Reduce2cArgs a{};
-    if (!reduce2c_taps(a.t)) return MIPX_EINVAL;
-    for (float &t : a.t) t /= 4096.0f;
-    a.bias = 1.0f / 8192.0f;
-    a.in = in;
-    a.out = out;
-    a.w = w;
-    a.h = h;
-    a.ow = out_size_reduce(w, 2.0);
-    a.oh = out_size_reduce(h, 2.0);
-    if (x0 < 0 || y0 < 0 || x1 > a.ow || y1 > a.oh || x0 >= x1 || y0 >= y1) return MIPX_EINVAL;
-    const int tw = b == 3 ? R2C<3>::TW : R2C<4>::TW;
-    a.s_base = x0 / tw;
-    a.x_end = x1;
-    a.y_base = y0 / kR * kR;
-    a.y_end = y1;
-    a.n_strips = (x1 + tw - 1) / tw - a.s_base;
-    const int chunks = (y1 - a.y_base + kR - 1) / kR;
-    const char *eb = tune_env("MIPX_R2C_BAND");  // 12-row chunks per band (A/B)
-    const int cpb = (eb && *eb) ? std::max(1, std::atoi(eb)) : 2;
-    a.band_rows = std::max(1, std::min(chunks, cpb)) * kR;
-    a.n_bands = (y1 - a.y_base + a.band_rows - 1) / a.band_rows;
-    a.in_img = img_bytes(w, h, b);
-    a.out_img = img_bytes(a.ow, a.oh, b);
-    const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
-    if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
-    const dim3 grid(static_cast<unsigned>(tiles)), blk(256);
-    if (b == 3) hipLaunchKernelGGL((k_reduce2c<3>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((k_reduce2c<4>), grid, blk, 0, st, a);
-    return launch_check("k_reduce2c");
 }
 
 // k_reduce2x2 build variant.  Only the shipped one (66) is compiled now; the r01 / r02
@@ -823,18 +548,12 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
 // Every computed pixel is the same sum as in the full launch.
 int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x0, int y0, int x1, int y1,
                           hipStream_t st) {
-    if (reduce_centre()) {
-        // k_reduce2m (vertical products on the matrix cores) by default; MIPX_R2M=0 keeps
-        // the all-VALU k_reduce2c (A/B)
-        const char *em = tune_env("MIPX_R2M");
+    if (reduce_centre()) {  // k_reduce2m: both passes on the matrix cores
         float tf[6];
-        if (!(em && *em == '0') && reduce2c_taps(tf)) {
-            int taps[12];
-            for (int i = 0; i < 6; ++i) taps[i] = taps[11 - i] = static_cast<int>(tf[i]);
-            const int e = reduce2m_window_launch(in, out, n, w, h, b, x0, y0, x1, y1, taps, st);
-            if (e != MIPX_EUNSUPPORTED) return e;
-        }
-        return reduce2c_window_launch(in, out, n, w, h, b, x0, y0, x1, y1, st);
+        if (!reduce2c_taps(tf)) return MIPX_EINVAL;
+        int taps[12];
+        for (int i = 0; i < 6; ++i) taps[i] = taps[11 - i] = static_cast<int>(tf[i]);
+        return reduce2m_window_launch(in, out, n, w, h, b, x0, y0, x1, y1, taps, st);
     }
     float c[4];
     if (!reduce2_taps(c)) return MIPX_EINVAL;

@@ -45,7 +45,7 @@ for s in ${STEPS:-tests smoke bench configs}; do
             done
             ALG_BYTES=7962624000 run 60 python3 scripts/traffic_json.py "$O/pmc_c2_corner" "k_reduce2x2<3, 66>" "$O/traffic.json" \
               "C2 bench.py --steps 3, 256 x 4K RGB -> 1080p, corner sampling"
-            ALG_BYTES=7962624000 run 60 python3 scripts/traffic_json.py "$O/pmc_c2_centre" "k_reduce2c<3>" "$O/traffic.json" \
+            ALG_BYTES=7962624000 run 60 python3 scripts/traffic_json.py "$O/pmc_c2_centre" "k_reduce2m<3>" "$O/traffic.json" \
               "C2 bench.py --steps 3 --sampling centre, 256 x 4K RGB -> 1080p" ;;
     pmc_c3) pmc2 "$O/pmc_c3" python3 bench_configs.py --configs C3 --steps 3 --warmup 1 --warm-ms 0
             run 60 python3 scripts/traffic_json.py "$O/pmc_c3" "" "$O/traffic_c3.json" "C3 bench_configs.py --steps 3: every kernel" --per-kernel ;;

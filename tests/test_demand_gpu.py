@@ -9,7 +9,7 @@ import pytest
 
 import imaginary_amd as ia
 
-# every case under both reduce sampling conventions (the centre one runs k_reduce2c)
+# every case under both reduce sampling conventions (the centre one runs k_reduce2m)
 pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("convention")]
 
 

@@ -70,15 +70,14 @@ def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
 
 
-@pytest.mark.parametrize("r2m", ["1", "h0", "0"])
-def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, r2m, monkeypatch):
+@pytest.mark.parametrize("band", ["", "1", "16"])
+def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, band, monkeypatch):
     """The fused 2x2 kernels (corner: k_reduce2x2 variant 66, the r01/r02 A/B builds are
-    recorded under profiles/ and no longer compiled; centre: k_reduce2m with the vertical
-    pass on the matrix cores, and k_reduce2c behind MIPX_R2M=0) are bit-exact, including
-    strips that end at the image edge, images shorter than a band and the smallest
-    eligible sizes."""
-    monkeypatch.setenv("MIPX_R2M", r2m[-1])
-    monkeypatch.setenv("MIPX_R2M_H", "0" if r2m == "h0" else "1")
+    recorded under profiles/ and no longer compiled; centre: k_reduce2m, both passes on
+    the matrix cores, at its default band and at 1 / 16 steps per band) are bit-exact,
+    including strips that end at the image edge, images shorter than a band and the
+    smallest eligible sizes."""
+    monkeypatch.setenv("MIPX_R2M_BAND", band)
     for h, w, b in ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1001 * 4 // 4 - 1, 4), (200, 646, 3),
                     (8, 8, 4), (9, 12, 3), (25, 164, 3), (131, 1000, 4), (1081, 324, 3), (16, 3840, 3)):
         if (w * b) % 4:
@@ -86,7 +85,7 @@ def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, r2m, monkeypatch
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
         got = gpu.run_op("reduce", imgs, hshrink=2.0, vshrink=2.0)
         for i in range(2):
-            assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"{convention} r2m={r2m} {h}x{w}x{b} img{i}")
+            assert_same(got[i], oracle.reduce(imgs[i], 2.0, 2.0), f"{convention} band={band} {h}x{w}x{b} img{i}")
 
 
 @pytest.mark.parametrize("fused", ["0", "1"])

@@ -105,7 +105,7 @@ def centre(oracle, gpu):
 
 
 def test_reduce_centre_c2_c1_shapes(gpu, oracle, rng, centre):
-    """C2 (4K RGB -> 1080p, shrink 2: every output sits at phase 64, k_reduce2c) and
+    """C2 (4K RGB -> 1080p, shrink 2: every output sits at phase 64, k_reduce2m) and
     C1's 480x270 -> 300x169, plus the kernels behind k_rcol (unaligned
     rows: k_rmf2; one axis: the separable passes) and a windowed plan."""
     for h, w, b, hs, vs in ((2160, 3840, 3, 2.0, 2.0), (270, 480, 3, 1.6, 1.5976331360946747),
