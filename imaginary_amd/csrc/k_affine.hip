@@ -124,15 +124,11 @@ __device__ __forceinline__ int af_ix(int o, double scale, int *phase) {
     return static_cast<int>(X);
 }
 
-// P2 (r04): H as row-pair dwords, P[r][i] = (H[r][i], H[r + 1][i]) int16 x 2, so the
-// vertical pass reads two 16-byte pieces per output dword and feeds them to v_dot2
-// as they are (no v_perm); twice the H bytes in LDS.
-template <int B, bool P2>
+template <int B>
 __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t afs[];
     u8 *stg = reinterpret_cast<u8 *>(afs);                                       // [nr_max][ncb]
     int16_t *hrow = reinterpret_cast<int16_t *>(stg + ((a.nr_max * a.ncb + 15) & ~15));  // [nr_max][hs]
-    uint32_t *hpair = reinterpret_cast<uint32_t *>(hrow);                                 // P2: [nr_max][hs]
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int x0 = blockIdx.x * kAfTX, y0 = blockIdx.y * a.ty;
@@ -199,7 +195,6 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
         const int sb = (ix - 2 - c0) * B;  // staged byte of tap 0, channel 0
         const int sh = sb & 3;
         constexpr int ND = B + 1;          // dwords covering 4 B bytes from any alignment
-        int16_t prev[B];
         for (int rr = 0; rr < nr; ++rr) {
             const uint32_t *sp = reinterpret_cast<const uint32_t *>(stg + rr * a.ncb + (sb & ~3));
             uint32_t v[ND], t[B];
@@ -223,25 +218,14 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
                 acc = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, p23), __builtin_bit_cast(af_s2, c23), acc, false);
                 hv[c] = static_cast<int16_t>(acc >> 12);
             }
-            if (P2) {
-                if (rr > 0) {
-                    uint32_t *pq = hpair + (rr - 1) * a.hs + tid * B;
+            int16_t *hq = hrow + rr * a.hs + tid * B;
 #pragma unroll
-                    for (int c = 0; c < B; ++c)
-                        pq[c] = (static_cast<uint32_t>(prev[c]) & 0xffffu) | (static_cast<uint32_t>(hv[c]) << 16);
-                }
-#pragma unroll
-                for (int c = 0; c < B; ++c) prev[c] = hv[c];
-            } else {
-                int16_t *hq = hrow + rr * a.hs + tid * B;
-#pragma unroll
-                for (int c = 0; c < B; ++c) hq[c] = hv[c];
-            }
+            for (int c = 0; c < B; ++c) hq[c] = hv[c];
         }
     }
     // the tile's output-row positions, once per block (fp64 as affine_pos): first H row
     // and the packed int16 tap pairs, read back by every lane of the row's wave
-    uint32_t *vpos = P2 ? hpair + a.nr_max * a.hs : reinterpret_cast<uint32_t *>(hrow + a.nr_max * a.hs);  // [ty][3]
+    uint32_t *vpos = reinterpret_cast<uint32_t *>(hrow + a.nr_max * a.hs);  // [ty][3]
     if (tid < a.ty && y0 + tid <= y_last) {
         int ty;
         const int iy = af_ix(y0 + tid, a.yscale, &ty);
@@ -262,20 +246,10 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
         for (int k = 0; k < B; ++k) {
             const int d = lane + 64 * k;
             if (4 * d >= vbytes) continue;
-            int acc[4];
-            if (P2) {  // pairs (t, t + 1) and (t + 2, t + 3) of bytes 4 d .. 4 d + 3
-                const uint4 p01 = *reinterpret_cast<const uint4 *>(hpair + vp[0] + 4 * d);
-                const uint4 p23 = *reinterpret_cast<const uint4 *>(hpair + vp[0] + 2 * a.hs + 4 * d);
-                const uint32_t u01[4] = {p01.x, p01.y, p01.z, p01.w}, u23[4] = {p23.x, p23.y, p23.z, p23.w};
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int s0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, u01[b]), __builtin_bit_cast(af_s2, y01), 2048, false);
-                    acc[b] = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, u23[b]), __builtin_bit_cast(af_s2, y23), s0, false);
-                }
-            } else {
             uint2 q[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) q[j] = *reinterpret_cast<const uint2 *>(h0 + j * a.hs + 4 * d);
+            int acc[4];
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const uint32_t lo0 = b < 2 ? q[0].x : q[0].y, lo1 = b < 2 ? q[1].x : q[1].y;
@@ -284,7 +258,6 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
                 const uint32_t r01 = __builtin_amdgcn_perm(lo1, lo0, sel), r23 = __builtin_amdgcn_perm(lo3, lo2, sel);
                 int s0 = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, r01), __builtin_bit_cast(af_s2, y01), 2048, false);
                 acc[b] = __builtin_amdgcn_sdot2(__builtin_bit_cast(af_s2, r23), __builtin_bit_cast(af_s2, y23), s0, false);
-            }
             }
             uint32_t lo, hi;
             asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(acc[0]), "v"(acc[1]));
@@ -382,10 +355,11 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
     const char *es = tune_env("MIPX_AFFINE_SEP");  // 0: the per-pixel gather kernel (A/B)
     if (!(es && *es == '0') && n <= 65535) {
         auto ixh = [](int o, double s) { return static_cast<int>((o + 0.5) / s - 0.5 + 1.0); };
-        const char *et = tune_env("MIPX_AFFINE_TY");  // first tile height tried: 32 / 16 / 8 (A/B)
-        const int ty0 = (et && *et) ? std::atoi(et) : 32;
-        const char *ep = tune_env("MIPX_AFFINE_P2");  // 1: row-pair H (A/B)
-        const bool p2 = ep && *ep == '1';
+        // first tile height tried: 16 (RGB, grey) / 8 (RGBA), measured best
+        // (profiles/r04/affine/affine_ty_ab.jsonl: 1080p RGB x2 +2 %, 550x740 x2 +5 %, 1024x768
+        // RGBA x1.5 +6 % against 32); MIPX_AFFINE_TY overrides (A/B)
+        const char *et = tune_env("MIPX_AFFINE_TY");
+        const int ty0 = (et && *et) ? std::atoi(et) : (b == 4 ? 8 : 16);
         for (const int ty : {32, 16, 8}) {
             if (ty > ty0) continue;
             int ncols = 0, nrows = 0;
@@ -402,16 +376,12 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
             g.hs = kAfTX * b;
             g.out_aligned = (a.ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
             const size_t lds = ((static_cast<size_t>(g.nr_max) * g.ncb + 15) & ~size_t(15)) +
-                               static_cast<size_t>(g.nr_max) * g.hs * (p2 ? 4 : 2) + 12 * static_cast<size_t>(ty);
+                               static_cast<size_t>(g.nr_max) * g.hs * 2 + 12 * static_cast<size_t>(ty);
             if (lds > 40 * 1024 || ncols * b > 4 * 4096) continue;
             const long long ytiles = (a.oh + ty - 1) / ty;
             if (ytiles > 65535) continue;
             const dim3 grid((a.ow + kAfTX - 1) / kAfTX, static_cast<unsigned>(ytiles), n);
-            if (p2) {
-                MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_affine_sep<B_, true>), grid, dim3(256), lds, st, g));
-            } else {
-                MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_affine_sep<B_, false>), grid, dim3(256), lds, st, g));
-            }
+            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_affine_sep<B_>, grid, dim3(256), lds, st, g));
             return launch_check("k_affine_sep");
         }
     }

@@ -23,11 +23,10 @@ CASES = [  # h, w, b, xs, ys, extend
 ]
 
 
-@pytest.mark.parametrize("sep", ["1", "p2", "0"])
+@pytest.mark.parametrize("sep", ["1", "0"])
 @pytest.mark.parametrize("h,w,b,xs,ys,extend", CASES)
 def test_affine_tiles_match_oracle(gpu, oracle, rng, monkeypatch, sep, h, w, b, xs, ys, extend):
-    monkeypatch.setenv("MIPX_AFFINE_SEP", "1" if sep == "p2" else sep)
-    monkeypatch.setenv("MIPX_AFFINE_P2", "1" if sep == "p2" else "0")
+    monkeypatch.setenv("MIPX_AFFINE_SEP", sep)
     imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
     got = gpu.run_op("affine", imgs, xscale=xs, yscale=ys, extend=extend)
     for i in range(2):
