@@ -580,7 +580,7 @@ __global__ void __launch_bounds__(256) k_extract_rows(const u8 *__restrict__ in,
     const int img = blockIdx.z;
     const u8 *src = in + img * in_img + static_cast<size_t>(top + y) * in_row_bytes + left_bytes;
     u8 *dst = out + img * out_img + static_cast<size_t>(y) * out_row_bytes;
-    if (dword == 2) {  // non-temporal stores (MIPX_EXTRACT_NT, A/B)
+    if (dword == 2) {  // non-temporal stores (the default; MIPX_EXTRACT_NT=0: plain, A/B)
         const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
         uint32_t *d = reinterpret_cast<uint32_t *>(dst);
         for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < out_row_bytes / 4; j += gridDim.x * blockDim.x)
@@ -853,8 +853,10 @@ int extract_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, 
     if (!dword && (b != 4 || (aligned4(in) && aligned4(out))))
         return embed_launch(in, out, n, w, h, b, -left, -top, ow, oh, MIPX_EXTEND_COPY, nullptr, nullptr, st);
     dim3 grid(std::max(1, std::min((out_row / (dword ? 4 : 1) + 255) / 256, 64)), oh, n);
+    // non-temporal stores by default: 4K RGB -> 2000x1500 +11 %, 1080p -> 1000x700 +57 %, 12 MP
+    // RGBA -> 3001x2000 +9 % (profiles/r04/extract_nt_ab.jsonl); MIPX_EXTRACT_NT=0 keeps plain stores (A/B)
     const char *en = tune_env("MIPX_EXTRACT_NT");
-    const int mode = dword && en && *en == '1' ? 2 : dword;
+    const int mode = dword && !(en && *en == '0') ? 2 : dword;
     hipLaunchKernelGGL(k_extract_rows, grid, dim3(256), 0, st, in, out, in_row, out_row, lb, top, img_bytes(w, h, b),
                        img_bytes(ow, oh, b), mode);
     return launch_check("k_extract_rows");

@@ -58,8 +58,14 @@ struct R2M {
     static constexpr int CPR = (OFF + B * (2 * kMTW + 10) + 15) / 16;  // 16-byte chunks per staged row
     static constexpr int RS = B == 3 ? 432 : 592;            // row stride: (RS / 4 mod 64) / 4 odd
     static constexpr int KM = (32 * CPR + kMNT - 1) / kMNT;  // chunks per lane per step (32 rows)
-    static constexpr int OS = B == 3 ? 208 : 272;            // output tile row stride (conflict-free)
-    static_assert(RS >= 16 * CPR + ISH, "row stride");
+    // intermediate rows IS and output tile rows OS at (dwords mod 32) = 2 x odd, so the 16
+    // rows x 2 dwords of a half-wave's ds_write_b32 hit 32 distinct banks (writes map banks
+    // mod 32), read back with ds_read_b64 pairs (ds_read2_b64 costs 16 LDS cycles, two
+    // ds_read_b64 4): bank-conflict cycles halved against IS = RS / 16-aligned OS, C2 -0.4 %,
+    // RGBA -1.5 % (profiles/r04/reduce2m/f_lds_layout_ab.jsonl, f_pmc_layout.txt)
+    static constexpr int IS = B == 3 ? 424 : 584, OS = B == 3 ? 200 : 264;
+    static_assert(RS >= 16 * CPR + ISH && IS >= 16 * CPR + ISH, "row stride");
+    static_assert((IS / 4) % 32 % 4 == 2 && (OS / 4) % 32 % 4 == 2 && IS % 8 == 0 && OS % 8 == 0, "write banks");
     static_assert(((RS / 4) % 64 / 4) % 2 == 1, "conflict-free transposed reads");
 };
 
@@ -78,11 +84,11 @@ struct R2mArgs {
 template <int B>
 __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     using G = R2M<B>;
-    constexpr int RS = G::RS, CPR = G::CPR, KM = G::KM, RG = kMRing;
-    __shared__ __attribute__((aligned(16))) u8 smem[(RG + kMN) * RS + kMN * G::OS];
+    constexpr int RS = G::RS, CPR = G::CPR, KM = G::KM, RG = kMRing, IS = G::IS, OS = G::OS;
+    __shared__ __attribute__((aligned(16))) u8 smem[RG * RS + kMN * IS + kMN * OS];
     const uint32_t ring_l = rc_lds(smem), inter_l = ring_l + RG * RS;
     u8 *inter = smem + RG * RS;
-    const uint32_t otile_l = inter_l + kMN * RS;  // [16 rows][OS]; wave w owns bytes 16 B w ..
+    const uint32_t otile_l = inter_l + kMN * IS;  // [16 rows][OS]; wave w owns bytes 16 B w ..
     auto slot = [](int r) { return static_cast<uint32_t>(r + 2 * RG) % static_cast<uint32_t>(RG); };  // r >= -5
 
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
@@ -168,7 +174,7 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
             const int r1 = bk + 8 * kg + (n >> 1);
             const uint32_t a1 = ring_l + slot(r1) * RS + 8 * (n & 1);
             const uint32_t a2 = ring_l + slot(r1 + 32) * RS + 8 * (n & 1);
-            const uint32_t iq = inter_l + static_cast<uint32_t>(n * RS + 4 * kg + G::ISH);
+            const uint32_t iq = inter_l + static_cast<uint32_t>(n * IS + 4 * kg + G::ISH);
             auto tile = [&](int c, rc_v2i u1, rc_v2i u2) {
                 const rc_v4i av = rc_v4i{u1.x, u1.y, u2.x, u2.y};
                 rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
@@ -214,7 +220,7 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                 const int f = rem / B, c = rem - f * B;
                 const int d = f < nl ? f : fr + (f - nl);
                 const int sp = f < nl ? nl : fr - 1;
-                inter[u * RS + ib0 + B * d + c] = inter[u * RS + ib0 + B * sp + c];
+                inter[u * IS + ib0 + B * d + c] = inter[u * IS + ib0 + B * sp + c];
             }
             rc_barrier();
         }
@@ -231,7 +237,8 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const uint32_t ws = static_cast<uint32_t>((ib0 & ~7) + 2 * B * GP * (GPW * wave + gb + i));
-                bv[i] = __builtin_bit_cast(rc_v4i, lds_rd2x64(inter_l + static_cast<uint32_t>(n * RS) + ws + 16 * kg));
+                const uint32_t ad = inter_l + static_cast<uint32_t>(n * IS) + ws + 16 * kg;
+                bv[i] = __builtin_bit_cast(rc_v4i, lds_rd64x2(ad));
             }
             lgkm_wait_for<0>(bv[0], bv[1], bv[2], bv[3]);
 #pragma unroll
@@ -245,7 +252,7 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                 asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(s0), "v"(s1));
                 asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(s2), "v"(s3));
                 if (4 * kg < B * GP)
-                    lds_wr32(otile_l + static_cast<uint32_t>(n * G::OS + 16 * B * wave + B * GP * (gb + i) + 4 * kg),
+                    lds_wr32(otile_l + static_cast<uint32_t>(n * OS + 16 * B * wave + B * GP * (gb + i) + 4 * kg),
                              __builtin_amdgcn_perm(hi, lo, 0x05040100u));
             }
         }
@@ -254,7 +261,8 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
             const int u = lane / LPR, c = lane - u * LPR;
             lgkm_wait();
             if (u < kMN) {
-                const rc_u4 v = lds_rd128(otile_l + static_cast<uint32_t>(u * G::OS + 16 * B * wave + 16 * c));
+                const uint32_t ad = otile_l + static_cast<uint32_t>(u * OS + 16 * B * wave + 16 * c);
+                const rc_u4 v = lds_rd64x2(ad);
                 lgkm_wait();
                 const int y = kMN * k + u;
                 const int xb = (x0 + 16 * wave) * B + 16 * c;
