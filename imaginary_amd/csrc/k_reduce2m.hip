@@ -262,8 +262,8 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
             lgkm_wait();
             if (u < kMN) {
                 const uint32_t ad = otile_l + static_cast<uint32_t>(u * OS + 16 * B * wave + 16 * c);
-                const rc_u4 v = lds_rd64x2(ad);
-                lgkm_wait();
+                rc_u4 v = lds_rd64x2(ad);
+                lgkm_wait_for<0>(v);
                 const int y = kMN * k + u;
                 const int xb = (x0 + 16 * wave) * B + 16 * c;
                 const int rowb = a.ow * B;

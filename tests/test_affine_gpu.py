@@ -45,3 +45,22 @@ def test_enlarge_plans(gpu, oracle, rng):
         got = gpu.execute(p, imgs)
         for i in range(2):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"enlarge plan {iw}x{ih}x{b} {opts}")
+
+
+E2_CASES = [  # h, w, b, extend: k_enlarge2 (exactly 2 x 2) at every band count and edge
+    (740, 550, 3, 1), (33, 1201, 4, 0), (97, 203, 1, 2), (61, 130, 2, 3), (64, 640, 3, 4),
+    (5, 7, 3, 5), (1, 1, 4, 1), (2, 3, 3, 0), (70, 129, 4, 1), (129, 128, 3, 3),
+]
+
+
+@pytest.mark.parametrize("e2", ["1", "0"])
+@pytest.mark.parametrize("h,w,b,extend", E2_CASES)
+def test_enlarge2_matches_oracle(gpu, oracle, rng, monkeypatch, e2, h, w, b, extend):
+    """vips_affine at exactly 2 x 2 on k_enlarge2 (the fixed phase-96 / phase-32 pattern,
+    MIPX_ENLARGE2=1, default) and on k_affine_sep (0): strips and bands that end at the
+    image edges, images narrower than the 6-pixel window, every extend mode, all bands."""
+    monkeypatch.setenv("MIPX_ENLARGE2", e2)
+    imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+    got = gpu.run_op("affine", imgs, xscale=2.0, yscale=2.0, extend=extend)
+    for i in range(2):
+        assert_same(got[i], oracle.affine(imgs[i], 2.0, 2.0, extend), f"enlarge2 e2={e2} {h}x{w}x{b} e{extend} img{i}")
