@@ -396,7 +396,9 @@ __global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
             const uint32_t ir = inter_l + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg);
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                q[i][ks] = lds_rd2x64(ir + 64 * ks);  // one 16-byte read: 4 lanes per bank quad, not 2 x (4 per pair)
+                // two ds_read_b64 (2 LDS cycles each) rather than one ds_read2_b64 (16): -0.3 to -2 %
+                // (profiles/r04/small/rcol_rd64_ab.jsonl)
+                q[i][ks] = lds_rd64x2(ir + 64 * ks);
             }
         }
 #pragma unroll

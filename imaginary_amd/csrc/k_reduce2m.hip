@@ -16,7 +16,7 @@
 //    2n + i of output row n.  The result (byte - 128) goes to an LDS intermediate.
 //  * horizontal: D[output byte][row] = W[output byte][window byte] x inter[window][row];
 //    a group of 4 (RGB) / 2 (RGBA) output pixels of all 16 rows reads a 64-byte window
-//    (8-byte aligned) of each intermediate row as its B operand (one ds_read2_b64);
+//    (8-byte aligned) of each intermediate row as its B operand (two ds_read_b64);
 //    W, the taps at byte SH + B (2 (j / B) + i) + j % B of output byte j, is constant.
 //    D dwords go to an LDS output tile, then out as 16-byte row pieces.
 // The tap operands are built on the host (r2m_operands) and read once per block.
