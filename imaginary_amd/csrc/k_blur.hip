@@ -285,300 +285,11 @@ __global__ void __launch_bounds__(256) k_blur2d(Blur2DArgs a) {
 }
 
 
-// ===========================================================================
-// k_bmf<B>: both convsep passes on the i8 matrix cores (v_mfma_i32_16x16x64_i8),
-// one launch per 128 output pixels x 16 output rows.  The mask (rint(20 e^...),
-// 0..20) fits i8, so each pass is one banded product per 16 x 16 tile:
-//   * horizontal first (convsep's order), on the interleaved bytes themselves:
-//     output byte o = B x + c needs input bytes o + delta + B k, so the tap
-//     operand A[o][K] holds tap k at K = o + delta + B k and every channel comes
-//     out of the same product -- no deinterleave.  B operand = 16 staged rows'
-//     bytes, pixels entering as p - 128 (XOR), offset returned by the seed
-//     128 scale + rounding.  Results: (sum + rnd) / scale by a magic multiply,
-//     packed, kept as T - 128 for the vertical product;
-//   * vertical as k_rmf2's: two ds_read_b64_tr_b8 give a lane one byte column
-//     of 16 intermediate rows, B operand = taps shifted per output row; the
-//     lane ends with 4 consecutive output bytes of one row, gathered into an
-//     output tile in LDS and stored as whole rows.
-// Staged rows (DMA) and the intermediate alias one LDS region (the horizontal
-// results wait in registers across the barrier).  Exact integer arithmetic:
-// bit-identical to convi (oracle/vips_ref.c convi_pass).
-// ===========================================================================
-typedef int bm_v4i __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void bm_lds_void;
-__device__ __forceinline__ bm_lds_void *bm_lds(void *p) { return (bm_lds_void *)p; }
-constexpr int kBmXW = 128, kBmMaxKs = 3, kBmMaxCt = 8;
+// k_bmf (r02: both convsep passes on the matrix cores, 128-pixel blocks) was removed in
+// r04: k_bcol (k_bcol.hip) takes every image k_bmf could (RGB / RGBA, <= 33 taps, dword
+// rows) and is faster there (profiles/r03/bcol_*); its records stay under profiles/r02-r03.
 
-struct BmArgs {
-    const u8 *in;
-    u8 *out;
-    long long in_base;  // byte offset of the window origin in an image
-    int in_pitch;
-    long long in_img, out_img;
-    int w, h;           // window = output size (COPY clamp range)
-    int x_blocks, y_blocks;
-    int taps, half;
-    int sx0;            // staged rows start at window pixel x0 - sx0 (4-pixel aligned for RGB)
-    int e;              // byte of pixel x0 - half in a staged row: B (sx0 - half)
-    int nks;            // horizontal K steps
-    int rsd;            // staged row stride (dwords), (rsd mod 64) / 4 odd
-    int tw;             // intermediate row stride (bytes), (tw / 4 mod 64) / 4 odd
-    uint32_t mag;       // floor(x / scale) == mulhi(x, mag) for the sums here
-    int seed;           // 128 scale + (scale + 1) / 2
-    int al16;           // output rows 16-byte aligned (dwordx4 row stores)
-    const signed char *ops;  // device_blur_ops
-};
-
-__device__ __forceinline__ uint32_t bm_pack(const bm_v4i &d, uint32_t mag) {
-    const int t0 = __umulhi(static_cast<uint32_t>(d[0]), mag), t1 = __umulhi(static_cast<uint32_t>(d[1]), mag);
-    const int t2 = __umulhi(static_cast<uint32_t>(d[2]), mag), t3 = __umulhi(static_cast<uint32_t>(d[3]), mag);
-    uint32_t lo, hi;
-    asm("v_ashr_pk_u8_i32 %0, %1, %2, 0" : "=v"(lo) : "v"(t0), "v"(t1));
-    asm("v_ashr_pk_u8_i32 %0, %1, %2, 0" : "=v"(hi) : "v"(t2), "v"(t3));
-    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-}
-
-// RG: 16-row output groups per block (2: 32 output rows from 31 + taps staged rows, so
-// the horizontal products and the row loads per output row drop from (16 + taps - 1) / 16
-// to (32 + taps - 1) / 32)
-template <int B, int RG>
-__global__ void __launch_bounds__(256) k_bmf(BmArgs a) {
-    constexpr int ROWS = 16 * RG, MAXRG = RG + 2;
-    extern __shared__ __attribute__((aligned(16))) uint32_t bsm[];
-    uint32_t *raw = bsm;                   // [L][rsd] staged rows
-    u8 *rawb = reinterpret_cast<u8 *>(bsm);
-    u8 *tm = rawb;                         // [L][tw] intermediate (T - 128), after the horizontal products
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int xb = t % a.x_blocks;
-    const int rest = t / a.x_blocks;
-    const int yb = rest % a.y_blocks;
-    const int img = rest / a.y_blocks;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int x0 = xb * kBmXW, xw = min(kBmXW, a.w - x0);
-    const int y0 = yb * ROWS, nr = min(ROWS, a.h - y0);
-    const int L = nr + a.taps - 1;
-    const int sx = x0 - a.sx0;                       // first staged window pixel
-    const int spx = xw + a.taps - 1 + (a.sx0 - a.half);  // staged pixels per row
-    {
-        const __amdgpu_buffer_rsrc_t rs = image_rsrc(a.in + img * a.in_img, a.in_img);
-        const int chunks = (B * spx + 255) >> 8;
-        for (int l = wave; l < L; l += 4) {
-            const int r = clampi(y0 - a.half + l, 0, a.h - 1);
-            for (int c = 0; c < chunks; ++c)
-                if (c * 64 + lane < a.rsd)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, bm_lds(raw + l * a.rsd + c * 64), 4,
-                                                             static_cast<int>(a.in_base + static_cast<long long>(r) * a.in_pitch) +
-                                                                 B * sx + 4 * (c * 64 + lane),
-                                                             0, 0, 0);
-        }
-    }
-    __syncthreads();
-    // ---- COPY edge: staged pixels outside the window repeat its edge pixel ----
-    if (sx < 0 || sx + spx > a.w) {
-        for (int i = tid; i < L * spx; i += 256) {
-            const int l = i / spx, pq = i - l * spx, p = sx + pq;
-            if (p >= 0 && p < a.w) continue;
-            const int src = clampi(p, 0, a.w - 1) - sx;
-#pragma unroll
-            for (int z = 0; z < B; ++z) rawb[l * a.rsd * 4 + pq * B + z] = rawb[l * a.rsd * 4 + src * B + z];
-        }
-        __syncthreads();
-    }
-    const int n = lane & 15, kg = lane >> 4;
-    // ---- horizontal products: unit = (16-row group, 16 output bytes) ----
-    {
-        bm_v4i ta[kBmMaxKs];
-#pragma unroll
-        for (int ks = 0; ks < kBmMaxKs; ++ks)
-            if (ks < a.nks) ta[ks] = *reinterpret_cast<const bm_v4i *>(a.ops + (ks * 64 + lane) * 16);
-        const int ngr = (xw * B + 15) >> 4, nrg = (L + 15) >> 4;
-        const int kb0 = a.e & ~3;
-        // unit (row group rg, 16-byte group g = wave + 4 j): no divisions, static register slots
-        uint32_t res[MAXRG][kBmMaxCt];
-#pragma unroll
-        for (int rg = 0; rg < MAXRG; ++rg) {
-            if (rg >= nrg) break;  // uniform
-            const int row = min(16 * rg + n, L - 1);
-            const u8 *rrow = rawb + row * a.rsd * 4 + kb0 + 16 * kg;
-#pragma unroll
-            for (int j = 0; j < kBmMaxCt; ++j) {
-                const int g = wave + 4 * j;
-                if (g >= ngr) continue;  // uniform
-                const uint32_t *src = reinterpret_cast<const uint32_t *>(rrow + 16 * g);
-                bm_v4i acc = bm_v4i{a.seed, a.seed, a.seed, a.seed};
-#pragma unroll
-                for (int ks = 0; ks < kBmMaxKs; ++ks) {
-                    if (ks >= a.nks) break;
-                    const bm_v4i bv = bm_v4i{static_cast<int>(src[16 * ks] ^ 0x80808080u), static_cast<int>(src[16 * ks + 1] ^ 0x80808080u),
-                                             static_cast<int>(src[16 * ks + 2] ^ 0x80808080u), static_cast<int>(src[16 * ks + 3] ^ 0x80808080u)};
-                    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(ta[ks], bv, acc, 0, 0, 0);
-                }
-                res[rg][j] = bm_pack(acc, a.mag) ^ 0x80808080u;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int rg = 0; rg < MAXRG; ++rg) {
-            if (rg >= nrg) break;
-            if (16 * rg + n >= L) continue;
-            u8 *trow = tm + (16 * rg + n) * a.tw + 4 * kg;
-#pragma unroll
-            for (int j = 0; j < kBmMaxCt; ++j) {
-                const int g = wave + 4 * j;
-                if (g >= ngr) continue;
-                *reinterpret_cast<uint32_t *>(trow + 16 * g) = res[rg][j];
-            }
-        }
-    }
-    __syncthreads();
-    // ---- vertical products per 16-byte column tile -> output tile in LDS -> whole rows ----
-    {
-        const bm_v4i tb = *reinterpret_cast<const bm_v4i *>(a.ops + (a.nks * 64 + lane) * 16);
-        const int nct = (xw * B + 15) >> 4;
-        typedef int v2i_t __attribute__((ext_vector_type(2)));
-        uint32_t res[RG][kBmMaxCt];
-#pragma unroll
-        for (int g = 0; g < RG; ++g) {  // output rows 16 g .. 16 g + 15 from intermediate rows 16 g ..
-            const int r1 = min(16 * g + 16 * kg + (n >> 1), L - 1), r2 = min(16 * g + 16 * kg + 8 + (n >> 1), L - 1);
-#pragma unroll
-            for (int i = 0; i < kBmMaxCt; ++i) {
-                const int ct = wave + 4 * i;
-                if (ct >= nct) continue;
-                const int cb = 16 * ct + 8 * (n & 1);
-                const v2i_t t1 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                    (__attribute__((address_space(3))) v2i_t *)(bm_lds(tm + r1 * a.tw + cb)));
-                const v2i_t t2 = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
-                    (__attribute__((address_space(3))) v2i_t *)(bm_lds(tm + r2 * a.tw + cb)));
-                const bm_v4i av = bm_v4i{t1.x, t1.y, t2.x, t2.y};
-                const bm_v4i d =
-                    __builtin_amdgcn_mfma_i32_16x16x64_i8(av, tb, bm_v4i{a.seed, a.seed, a.seed, a.seed}, 0, 0, 0);
-                res[g][i] = bm_pack(d, a.mag);
-            }
-        }
-        __syncthreads();  // every wave is done with the intermediate: the output tile goes over it
-#pragma unroll
-        for (int g = 0; g < RG; ++g)
-#pragma unroll
-            for (int i = 0; i < kBmMaxCt; ++i) {
-                const int ct = wave + 4 * i;
-                if (ct >= nct) continue;
-                *reinterpret_cast<uint32_t *>(tm + (16 * g + n) * a.tw + 16 * ct + 4 * kg) = res[g][i];
-            }
-    }
-    __syncthreads();
-    {
-        // a store instruction covers whole output rows (a 16-row column of dwords per
-        // instruction would touch 16 cache lines)
-        u8 *ob = a.out + img * a.out_img;
-        const __amdgpu_buffer_rsrc_t os = __builtin_amdgcn_make_buffer_rsrc(ob, 0, static_cast<int>(a.out_img), 0x00020000);
-        const int rowb = xw * B;
-        if (a.al16 && (rowb & 15) == 0) {
-            const int nq = rowb >> 4;
-            for (int i = tid; i < nr * nq; i += 256) {
-                const int r = i / nq, q = i - r * nq;
-                __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const bm_v4i *>(tm + r * a.tw + 16 * q), os,
-                                                       ((y0 + r) * a.w + x0) * B + 16 * q, 0, 0);
-            }
-        } else {
-            const int nd = (rowb + 3) >> 2;
-            for (int i = tid; i < nr * nd; i += 256) {
-                const int r = i / nd, q = i - r * nd;
-                const uint32_t wv = *reinterpret_cast<const uint32_t *>(tm + r * a.tw + 4 * q);
-                const int qo = ((y0 + r) * a.w + x0) * B + 4 * q;
-                if (4 * q + 4 <= rowb) {
-                    __builtin_amdgcn_raw_buffer_store_b32(wv, os, qo, 0, 0);
-                } else {
-                    for (int k = 0; 4 * q + k < rowb; ++k)
-                        __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(wv >> (8 * k)), os, qo + k, 0, 0);
-                }
-            }
-        }
-    }
-}
 }  // namespace
-
-
-// k_bmf for the (left, top, ow x oh) window: RGB (RGBA when forced) with dword-aligned
-// rows and window start, masks up to 33 taps, scale < 4096 (the magic divide is exact
-// there); MIPX_EUNSUPPORTED otherwise.  MIPX_BMF=0 disables it, =1 forces it (A/B).
-int blur_mfma_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left, int top, int ow, int oh,
-                     const std::vector<int> &mask, int scale, hipStream_t st) {
-    // default RGB only: RGBA's tap window spans 16 + 4 (taps - 1) bytes, two K steps from
-    // 13 taps on, and k_blur2d's dot4 path stays ahead there (blur_ab.jsonl); MIPX_BMF=1 forces
-    const char *ef = tune_env("MIPX_BMF");
-    if (ef && *ef == '0') return MIPX_EUNSUPPORTED;
-    const bool forced = ef && *ef == '1';
-    const int taps = static_cast<int>(mask.size());
-    if ((b != 3 && !(b == 4 && forced)) || taps < 1 || taps > 33 || scale <= 0 || scale >= 4096) return MIPX_EUNSUPPORTED;
-    for (int m : mask)
-        if (m < 0 || m > 127) return MIPX_EUNSUPPORTED;
-    if ((w * b) % 4 || (left * b) % 4 || reinterpret_cast<uintptr_t>(in) % 4 || (ow * b) % 4 ||
-        reinterpret_cast<uintptr_t>(out) % 4)
-        return MIPX_EUNSUPPORTED;
-    BmArgs a{};
-    a.in = in;
-    a.out = out;
-    a.in_pitch = w * b;
-    a.in_base = (static_cast<long long>(top) * w + left) * b;
-    a.in_img = img_bytes(w, h, b);
-    a.out_img = img_bytes(ow, oh, b);
-    if (a.in_img >= 0x7fffffffLL - 1024 || a.out_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
-    a.w = ow;
-    a.h = oh;
-    // output rows per block: 32 where the image has them, 48 for short masks (the staged
-    // halo is taps - 1 rows per block, so taller blocks redo less of the horizontal pass
-    // and reload fewer rows; bmf_rg_ab.jsonl / bmf_rg3_ab.jsonl: 32 rows -17 to -21 % on
-    // RGB at sigma 1-5, 48 rows a further -7 % at sigma 1 and +1-5 % at sigma 3-5);
-    // MIPX_BMF_RG=1/2/3 forces 16 / 32 / 48
-    const char *eg = tune_env("MIPX_BMF_RG");
-    const int rg = (eg && *eg) ? std::min(3, std::max(1, std::atoi(eg)))
-                               : (oh >= 48 && taps <= 7) ? 3 : (oh >= 32 ? 2 : 1);
-    const int rows = 16 * rg;
-    a.x_blocks = (ow + kBmXW - 1) / kBmXW;
-    a.y_blocks = (oh + rows - 1) / rows;
-    a.taps = taps;
-    a.half = taps / 2;
-    a.sx0 = b == 3 ? (a.half + 3) & ~3 : a.half;  // RGB: staged rows start on a 4-pixel (3-dword) boundary
-    a.e = b * (a.sx0 - a.half);
-    const int delta = a.e & 3;
-    a.nks = (16 + delta + b * (taps - 1) + 63) / 64;
-    if (a.nks > kBmMaxKs) return MIPX_EUNSUPPORTED;
-    const int spx = kBmXW + taps - 1 + (a.sx0 - a.half);
-    int rsd = (b * spx + 3) / 4;
-    rsd = (rsd + 3) & ~3;
-    while (((rsd & 63) >> 2) % 2 == 0) rsd += 4;
-    a.rsd = rsd;
-    int twd = (kBmXW * b) / 4;
-    twd = (twd + 3) & ~3;
-    while (((twd & 63) >> 2) % 2 == 0) twd += 4;
-    a.tw = 4 * twd;
-    const int lmax = rows + taps - 1;
-    if ((lmax + 15) / 16 > rg + 2 || (kBmXW * b + 15) / 16 > 4 * kBmMaxCt)
-        return MIPX_EUNSUPPORTED;
-    // horizontal B reads run up to 64 nks bytes past a group's start: slack after the last row
-    const size_t lds = std::max(static_cast<size_t>(lmax) * rsd * 4, static_cast<size_t>(lmax) * a.tw) + 64 * a.nks + 64;
-    if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
-    a.mag = static_cast<uint32_t>(((1ULL << 32) + scale - 1) / scale);
-    a.seed = 128 * scale + (scale + 1) / 2;
-    a.al16 = (ow * b) % 16 == 0 && reinterpret_cast<uintptr_t>(out) % 16 == 0;
-    a.ops = device_blur_ops(mask, b, delta, a.nks);
-    if (!a.ops) return MIPX_EDEVICE;
-    const long long blocks = static_cast<long long>(a.x_blocks) * a.y_blocks * n;
-    if (!grid_ok(blocks)) return MIPX_EINVAL;
-    const dim3 grid(static_cast<unsigned>(blocks)), blk(256);
-    if (rg == 3) {
-        if (b == 3) hipLaunchKernelGGL((k_bmf<3, 3>), grid, blk, lds, st, a);
-        else hipLaunchKernelGGL((k_bmf<4, 3>), grid, blk, lds, st, a);
-    } else if (rg == 2) {
-        if (b == 3) hipLaunchKernelGGL((k_bmf<3, 2>), grid, blk, lds, st, a);
-        else hipLaunchKernelGGL((k_bmf<4, 2>), grid, blk, lds, st, a);
-    } else {
-        if (b == 3) hipLaunchKernelGGL((k_bmf<3, 1>), grid, blk, lds, st, a);
-        else hipLaunchKernelGGL((k_bmf<4, 1>), grid, blk, lds, st, a);
-    }
-    return launch_check("k_bmf");
-}
 
 // Fused blur of the (left, top, ow x oh) window; MIPX_EUNSUPPORTED when the
 // mask is too tall for the register ring (the caller runs the two passes).
@@ -668,8 +379,6 @@ int blur_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int le
     if (gaussmat(sigma, min_ampl, mask, scale) < 0) return MIPX_EINVAL;
     const int ec = blur_col_launch(in, out, n, w, h, b, left, top, ow, oh, mask, scale, st);
     if (ec != MIPX_EUNSUPPORTED) return ec;
-    const int em = blur_mfma_launch(in, out, n, w, h, b, left, top, ow, oh, mask, scale, st);
-    if (em != MIPX_EUNSUPPORTED) return em;
     const int ef = blur2d_launch(in, out, n, w, h, b, left, top, ow, oh, mask, scale, st);
     if (ef != MIPX_EUNSUPPORTED) return ef;
     if (!sep_spec_gauss(sigma, min_ampl, &spec)) return MIPX_EDEVICE;

@@ -5,7 +5,7 @@ taps: one to three horizontal K steps, 32- and 64-row rings), images narrower th
 strip and shorter than a step, strips at both window edges, segment boundaries in
 tall images, windows (resize -> crop -> blur) at every gravity, output rows that are
 not a multiple of 16 bytes.  Every case also through the kernels behind it
-(MIPX_BCOL=0: k_bmf / k_blur2d)."""
+(MIPX_BCOL=0: k_blur2d, then the separable passes)."""
 import numpy as np
 import pytest
 
@@ -19,7 +19,7 @@ def route(request, monkeypatch):
     """k_bcol (the default: 256-byte strips, RGB ones starting mid-pixel, 16-byte-aligned
     horizontal operands), RGB on 64-pixel strips (MIPX_BCOL_RGB192=1), the same with the
     dword-aligned operands (+ MIPX_BCOL_A16=0; RGBA too) and the kernels behind it
-    (MIPX_BCOL=0: k_bmf / k_blur2d)."""
+    (MIPX_BCOL=0: k_blur2d, then the separable passes)."""
     monkeypatch.setenv("MIPX_BCOL", "0" if request.param == "nobcol" else "")
     monkeypatch.setenv("MIPX_BCOL_RGB192", "1" if request.param.startswith("bcol192") else "")
     monkeypatch.setenv("MIPX_BCOL_A16", "0" if request.param == "bcol192_dw" else "")

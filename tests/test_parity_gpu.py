@@ -362,7 +362,6 @@ def test_gaussblur_dot4_and_float_paths(gpu, oracle, rng, monkeypatch, dot, sigm
     (3 images of an odd byte size: the DMA=0 vertical staging)."""
     monkeypatch.setenv("MIPX_SEP_DOT", dot)
     monkeypatch.setenv("MIPX_BLUR2D", "0")  # the two separable passes, not the fused kernels
-    monkeypatch.setenv("MIPX_BMF", "0")
     for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
         got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
@@ -382,7 +381,6 @@ def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma,
     monkeypatch.setenv("MIPX_BLUR2D_ROWS", rows)
     monkeypatch.setenv("MIPX_BLUR2D_FROUND", fround)
     monkeypatch.setenv("MIPX_BCOL", "0")
-    monkeypatch.setenv("MIPX_BMF", "0")  # k_blur2d, not the matrix-core kernels
     for h, w, b in ((37, 53, 1), (29, 41, 2), (64, 77, 3), (50, 260, 4), (33, 19, 3), (9, 600, 4), (130, 513, 3),
                     (3, 5, 4), (70, 257, 2)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b), rand_img(rng, h, w, b)])
@@ -391,26 +389,20 @@ def test_blur2d_fused_matches_oracle(gpu, oracle, rng, monkeypatch, rows, sigma,
             assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"blur2d {sigma} {h}x{w}x{b} rows={rows} fr={fround} img{i}")
 
 
-@pytest.mark.parametrize("on", ["1", "1r", "1t", "0"])
 @pytest.mark.parametrize("sigma", [0.3, 1.0, 2.2, 5.0, 7.5, 9.0, 12.5])
-def test_blur_mfma_matches_oracle(gpu, oracle, rng, monkeypatch, on, sigma):
-    """k_bmf (both convsep passes on the i8 matrix cores: horizontal on the
-    interleaved bytes with the taps at byte stride B, vertical through transposed
-    LDS reads) against the oracle: RGB / RGBA, images narrower than a block and
-    shorter than the mask, several column and row blocks, both edges of every
-    window, windowed plans (resize -> crop -> blur) at every gravity, and the
-    cases it leaves to k_blur2d (unaligned rows, 1-2 bands, > 33 taps).  "0" runs
-    k_blur2d on the same cases; "1" uses 32-row blocks where the image has 32 rows,
-    "1r" the 16-row blocks, "1t" 48-row blocks."""
-    monkeypatch.setenv("MIPX_BCOL", "0")  # k_bmf / k_blur2d (the column walker: tests/test_bcol_gpu.py)
-    monkeypatch.setenv("MIPX_BMF", on[:1])
-    monkeypatch.setenv("MIPX_BMF_RG", {"1r": "1", "1t": "3"}.get(on, ""))
+def test_blur_fallback_matches_oracle(gpu, oracle, rng, monkeypatch, sigma):
+    """The gaussblur chain behind the column walker (MIPX_BCOL=0: k_blur2d, then the two
+    separable passes; r02's k_bmf was removed in r04, k_bcol serves every image it could)
+    against the oracle: RGB / RGBA, images narrower than a block and shorter than the
+    mask, both edges of every window, windowed plans (resize -> crop -> blur) at every
+    gravity, unaligned rows, 1-2 bands, > 33 taps."""
+    monkeypatch.setenv("MIPX_BCOL", "0")  # the column walker itself: tests/test_bcol_gpu.py
     for h, w, b in ((64, 76, 3), (130, 516, 3), (9, 600, 4), (50, 260, 4), (3, 8, 4), (33, 20, 3), (17, 132, 3),
                     (200, 388, 4), (33, 19, 3), (29, 41, 2), (41, 57, 1), (47, 140, 3), (95, 300, 4)):
         imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
         got = gpu.run_op("gaussblur", imgs, sigma=sigma, min_ampl=0.2)
         for i in range(2):
-            assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"bmf={on} {sigma} {h}x{w}x{b} img{i}")
+            assert_same(got[i], oracle.gaussblur(imgs[i], sigma, 0.2), f"fallback {sigma} {h}x{w}x{b} img{i}")
     if sigma in (1.0, 5.0):
         for g, b in ((0, 3), (2, 3), (3, 4), (1, 4)):
             opts = dict(width=300, height=200, crop=1, gravity=g, sigma=sigma)
@@ -420,7 +412,7 @@ def test_blur_mfma_matches_oracle(gpu, oracle, rng, monkeypatch, on, sigma):
             imgs = rng.integers(0, 256, (2, 700, 1200, b), dtype=np.uint8)
             got = gpu.execute(p, imgs)
             for i in range(2):
-                assert_same(got[i], oracle.execute(rp, imgs[i]), f"bmf={on} window gravity {g} bands {b}")
+                assert_same(got[i], oracle.execute(rp, imgs[i]), f"fallback window gravity {g} bands {b}")
 
 
 @pytest.mark.parametrize("hdma", ["16", "4"])
@@ -431,7 +423,6 @@ def test_hpass_dma_widths(gpu, oracle, rng, monkeypatch, hdma):
     16-byte grid), each against the oracle, with both image edges inside a block."""
     monkeypatch.setenv("MIPX_HP_DMA", hdma)
     monkeypatch.setenv("MIPX_BLUR2D", "0")
-    monkeypatch.setenv("MIPX_BMF", "0")
     for h, w, s in ((23, 256, 1.3333333333333333), (19, 300, 2.5), (11, 1028, 1.1), (9, 64, 3.0)):
         imgs = np.stack([rand_img(rng, h, w, 4), smooth_img(rng, h, w, 4)])
         got = gpu.run_op("reduceh", imgs, hshrink=s)
