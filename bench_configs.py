@@ -54,6 +54,24 @@ class Group:
                                    self.wsb, sp), "mipx_execute_dev")
 
 
+def stream_runner(groups, nstreams, dev, sp, stream):
+    """run_all over plan groups dealt round-robin over nstreams HIP streams (the request
+    path's queues_per_device > 1 does the same: independent batches overlap their kernels'
+    ramp-up and tail).  Each side stream waits for the timed stream at the start and the
+    timed stream waits for all of them at the end, so a step is bracketed as before."""
+    side = [torch.cuda.Stream(device=dev) for _ in range(max(0, nstreams - 1))]
+    sps = [sp] + [C.c_void_p(x.cuda_stream) for x in side]
+
+    def run_all():
+        for x in side:
+            x.wait_stream(stream)
+        for i, (g, _) in enumerate(groups):
+            g.run(sps[i % len(sps)])
+        for x in side:
+            stream.wait_stream(x)
+    return run_all, len(sps)
+
+
 def plan_for(opts, w, h, b, typ="png", wm_shape=None):
     inp = ia.make_input(w, h, b, typ)
     if wm_shape is not None:
@@ -150,17 +168,15 @@ def c4(args, dev, sp, stream):
             p = plan_for(opts, w, h, 3, wm_shape=workloads.C4_WM_SHAPE if opts.get("wm_enable") else None)
             groups.append((Group(p, n, dev, 4 + len(groups), wm if opts.get("wm_enable") else None), opts))
 
-    def run_all():
-        for g, _ in groups:
-            g.run(sp)
-
+    run_all, nst = stream_runner(groups, args.streams, dev, sp, stream)
     run_all()
     torch.cuda.synchronize()
     ok = all(verify(g, opts, wm if opts.get("wm_enable") else None) for g, opts in groups)
     wall, dev_ms = time_groups(run_all, args.steps, args.warmup, stream)
     alg = sum(g.in_bytes + g.out_bytes + (wm.nbytes if g.wm is not None else 0) for g, _ in groups)
     line("C4", "smartcrop 256^2 + thumbnail 256^2 + watermark, 12 MP 4000x3000 / 3000x4000",
-         2 * n * 2, wall, dev_ms, alg, ok, {"requests": 4 * n, "plans": [g.plan.describe() for g, _ in groups]})
+         2 * n * 2, wall, dev_ms, alg, ok, {"requests": 4 * n, "streams": nst,
+                                            "plans": [g.plan.describe() for g, _ in groups]})
 
 
 def c5_requests(count, seed=5):
@@ -185,9 +201,7 @@ def c5(args, dev, sp, stream):
     for (w, h), opts, cnt in shard:
         groups.append((Group(plan_for(opts, w, h, 3), cnt, dev, 5 + len(groups)), opts))
 
-    def run_all():
-        for g, _ in groups:
-            g.run(sp)
+    run_all, nst = stream_runner(groups, args.streams, dev, sp, stream)
 
     run_all()
     torch.cuda.synchronize()
@@ -195,7 +209,7 @@ def c5(args, dev, sp, stream):
     wall, dev_ms = time_groups(run_all, args.steps, args.warmup, stream)
     alg = sum(g.in_bytes + g.out_bytes for g, _ in groups)
     line("C5", f"mixed stream {len(reqs)} requests (rank {rank}/{world}), {len(groups)} plan groups",
-         len(reqs), wall, dev_ms, alg, ok, {"groups": len(groups)})
+         len(reqs), wall, dev_ms, alg, ok, {"groups": len(groups), "streams": nst})
 
 
 def e2e(args, dev, sp, stream):
@@ -267,6 +281,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--warm-ms", type=float, default=200.0, help="device-time warm-up after --warmup steps; 0: none")
     ap.add_argument("--c3-batch", type=int, default=512)
+    ap.add_argument("--streams", type=int, default=4,
+                    help="HIP streams the C4 / C5 plan groups are dealt over (1: one stream, r03's lines; "
+                         "4: measured best for C5, profiles/r04/c5_streams.jsonl)")
     ap.add_argument("--c4-batch", type=int, default=64)
     ap.add_argument("--e2e-requests", type=int, default=256)
     ap.add_argument("--e2e-batch", type=int, default=16)
