@@ -141,10 +141,12 @@ def c3(args, dev, sp, stream):
     for opts in stages:
         plans.append(plan_for(opts, w, h, 4))
         w, h = plans[-1].out_w, plans[-1].out_h
-    g = Group(ia.plan_chain(plans), n, dev, 3)
-
-    def run_all():
-        g.run(sp)
+    # --c3-split k: the batch as k sub-batches on k streams (stages of different sub-batches
+    # overlap); 1 = one launch per stage over the whole batch
+    k = max(1, args.c3_split)
+    subs = [Group(ia.plan_chain(plans), n // k + (1 if i < n % k else 0), dev, 3 + i) for i in range(k)]
+    g = subs[0]
+    run_all, _ = stream_runner([(x, None) for x in subs], k, dev, sp, stream)
 
     run_all()
     torch.cuda.synchronize()
@@ -156,7 +158,7 @@ def c3(args, dev, sp, stream):
     ok = bool(np.array_equal(g.y[0].cpu().numpy().reshape(px.shape), px))
     wall, dev_ms = time_groups(run_all, args.steps, args.warmup, stream)
     line("C3", "pipeline resize(w=1024)+crop(768x512)+blur(sigma=5), 2048^2 RGBA", n, wall, dev_ms,
-         g.in_bytes + g.out_bytes, ok, {"batch": n, "fused_plan": g.plan.describe()})
+         sum(x.in_bytes + x.out_bytes for x in subs), ok, {"batch": n, "split": k, "fused_plan": g.plan.describe()})
 
 
 def c4(args, dev, sp, stream):
@@ -281,6 +283,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--warm-ms", type=float, default=200.0, help="device-time warm-up after --warmup steps; 0: none")
     ap.add_argument("--c3-batch", type=int, default=512)
+    ap.add_argument("--c3-split", type=int, default=1, help="C3's batch as k sub-batches on k streams")
     ap.add_argument("--streams", type=int, default=4,
                     help="HIP streams the C4 / C5 plan groups are dealt over (1: one stream, r03's lines; "
                          "4: measured best for C5, profiles/r04/c5_streams.jsonl)")
