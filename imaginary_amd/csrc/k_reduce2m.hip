@@ -18,7 +18,8 @@
 //    a group of 4 (RGB) / 2 (RGBA) output pixels of all 16 rows reads a 64-byte window
 //    (8-byte aligned) of each intermediate row as its B operand (two ds_read_b64);
 //    W, the taps at byte SH + B (2 (j / B) + i) + j % B of output byte j, is constant.
-//    D dwords go to an LDS output tile, then out as 16-byte row pieces.
+//    D dwords go to an output tile in intermediate bytes only the wave's own windows
+//    cover (no LDS of its own: RGBA -1.4 %), then out as 16-byte row pieces.
 // The tap operands are built on the host (r2m_operands) and read once per block.
 //
 // A block (4 waves) owns a strip of 64 output pixels of one image and walks a band of
@@ -58,14 +59,19 @@ struct R2M {
     static constexpr int CPR = (OFF + B * (2 * kMTW + 10) + 15) / 16;  // 16-byte chunks per staged row
     static constexpr int RS = B == 3 ? 432 : 592;            // row stride: (RS / 4 mod 64) / 4 odd
     static constexpr int KM = (32 * CPR + kMNT - 1) / kMNT;  // chunks per lane per step (32 rows)
-    // intermediate rows IS and output tile rows OS at (dwords mod 32) = 2 x odd, so the 16
-    // rows x 2 dwords of a half-wave's ds_write_b32 hit 32 distinct banks (writes map banks
-    // mod 32), read back with ds_read_b64 pairs (ds_read2_b64 costs 16 LDS cycles, two
-    // ds_read_b64 4): bank-conflict cycles halved against IS = RS / 16-aligned OS, C2 -0.4 %,
-    // RGBA -1.5 % (profiles/r04/reduce2m/f_lds_layout_ab.jsonl, f_pmc_layout.txt)
-    static constexpr int IS = B == 3 ? 424 : 584, OS = B == 3 ? 200 : 264;
-    static_assert(RS >= 16 * CPR + ISH && IS >= 16 * CPR + ISH, "row stride");
-    static_assert((IS / 4) % 32 % 4 == 2 && (OS / 4) % 32 % 4 == 2 && IS % 8 == 0 && OS % 8 == 0, "write banks");
+    // intermediate rows IS at (dwords mod 32) = 2 x odd, so the 16 rows x 2 dwords of a
+    // half-wave's ds_write_b32 hit 32 distinct banks (writes map banks mod 32), read back
+    // with ds_read_b64 pairs (ds_read2_b64 costs 16 LDS cycles, two ds_read_b64 4):
+    // bank-conflict cycles halved against IS = RS, C2 -0.4 %, RGBA -1.5 %
+    // (profiles/r04/reduce2m/f_lds_layout_ab.jsonl, f_pmc_layout.txt)
+    static constexpr int IS = B == 3 ? 424 : 584;
+    // the horizontal pass: groups of GP output pixels (a 64-byte window from byte WB + 2 B GP g
+    // of each intermediate row), GPW groups per wave; wave w's windows alone cover the bytes
+    // EXS + EXW w .. + EXN, where its output tile (16 B bytes per row) goes
+    static constexpr int GP = B == 3 ? 4 : 2, GPW = kMTW / GP / 4, WB = (OFF + ISH) & ~7;
+    static constexpr int EXW = 2 * B * GP * GPW, EXS = WB + 64 - 2 * B * GP, EXN = EXW - EXS + WB;
+    static_assert(EXN >= 16 * B && EXS % 8 == 0 && EXS + 3 * EXW + 16 * B <= IS, "output tile in the intermediate");
+    static_assert((IS / 4) % 32 % 4 == 2 && IS % 8 == 0, "write banks");
     static_assert(((RS / 4) % 64 / 4) % 2 == 1, "conflict-free transposed reads");
 };
 
@@ -84,11 +90,10 @@ struct R2mArgs {
 template <int B>
 __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     using G = R2M<B>;
-    constexpr int RS = G::RS, CPR = G::CPR, KM = G::KM, RG = kMRing, IS = G::IS, OS = G::OS;
-    __shared__ __attribute__((aligned(16))) u8 smem[RG * RS + kMN * IS + kMN * OS];
+    constexpr int RS = G::RS, CPR = G::CPR, KM = G::KM, RG = kMRing, IS = G::IS;
+    __shared__ __attribute__((aligned(16))) u8 smem[RG * RS + kMN * IS];
     const uint32_t ring_l = rc_lds(smem), inter_l = ring_l + RG * RS;
     u8 *inter = smem + RG * RS;
-    const uint32_t otile_l = inter_l + kMN * IS;  // [16 rows][OS]; wave w owns bytes 16 B w ..
     auto slot = [](int r) { return static_cast<uint32_t>(r + 2 * RG) % static_cast<uint32_t>(RG); };  // r >= -5
 
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
@@ -110,31 +115,30 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     u8 *dst = a.out + img * a.out_img;
 
     // ---- staging: chunk c = tid + 256 j of a 32-row batch is (row rr, 16-byte column col) ----
-    int rr[KM], cof[KM];
-    uint32_t lof[KM];
+    // packed (row rr << 16 | 16 col), one register per chunk
+    uint32_t sg[KM];
 #pragma unroll
     for (int j = 0; j < KM; ++j) {
         const int c = tid + kMNT * j;
-        rr[j] = c < 32 * CPR ? c / CPR : 64;  // 64: idle
-        const int col = c - (c / CPR) * CPR;
-        cof[j] = org + 16 * col;
-        lof[j] = static_cast<uint32_t>(16 * col);
+        const int r = c < 32 * CPR ? c / CPR : 64;  // 64: idle
+        sg[j] = static_cast<uint32_t>(r << 16 | 16 * (c - (c / CPR) * CPR));
     }
     // a chunk left of the image (negative offset) reads zeros whole: the edge fix-up
     // replaces those pixels; rows clamp to the image (COPY edge)
     auto load = [&](rc_u4 *v, int r0, int nrows) {
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
-            const int r = clampi(r0 + rr[j], 0, a.h - 1);
-            const int off = rr[j] < nrows && cof[j] + 16 > 0 ? r * pitch + cof[j] : 0x7ffffff0;
+            const int rj = static_cast<int>(sg[j] >> 16), cof = org + static_cast<int>(sg[j] & 0xffffu);
+            const int r = clampi(r0 + rj, 0, a.h - 1);
+            const int off = rj < nrows && cof + 16 > 0 ? r * pitch + cof : 0x7ffffff0;
             v[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off, 0, 0));
         }
     };
     auto store_ring = [&](const rc_u4 *v, int r0, int nrows) {
 #pragma unroll
         for (int j = 0; j < KM; ++j)
-            if (rr[j] < nrows)
-                lds_wr128(ring_l + slot(r0 + rr[j]) * RS + lof[j],
+            if (static_cast<int>(sg[j] >> 16) < nrows)
+                lds_wr128(ring_l + slot(r0 + static_cast<int>(sg[j] >> 16)) * RS + (sg[j] & 0xffffu),
                           v[j] ^ 0x80808080u);
     };
 
@@ -188,11 +192,14 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                 // the intermediate is kept as byte - 128 (the horizontal product's B operand)
                 lds_wr32(iq + 16 * c, __builtin_amdgcn_perm(hi, lo, 0x05040100u) ^ 0x80808080u);
             };
-            // four tiles per batch: their reads under one wait, their products interleaved
-            for (int c0 = wave; c0 < CPR; c0 += 16) {
-                rc_v2i p[4][2];
+            // VB tiles per batch: their reads under one wait, their products interleaved (6
+            // waves per SIMD at 80 VGPRs needs VB = HB = 1 for RGB: -1.4 % from the occupancy,
+            // +2 % from the serialised reads, profiles/r04/reduce2m/h_otile_occupancy_ab.jsonl)
+            constexpr int VB = 4;
+            for (int c0 = wave; c0 < CPR; c0 += 4 * VB) {
+                rc_v2i p[VB][2];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
+                for (int i = 0; i < VB; ++i) {
                     const int ct = c0 + 4 * i;
                     if (ct < CPR) {
                         p[i][0] = lds_tr8(a1 + 16 * ct);
@@ -201,9 +208,11 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                         p[i][0] = p[i][1] = rc_v2i{0, 0};
                     }
                 }
-                lgkm_wait_for<0>(p[0][0], p[0][1], p[1][0], p[1][1], p[2][0], p[2][1], p[3][0], p[3][1]);
+                if constexpr (VB == 4) lgkm_wait_for<0>(p[0][0], p[0][1], p[1][0], p[1][1], p[2][0], p[2][1], p[3][0], p[3][1]);
+                else if constexpr (VB == 2) lgkm_wait_for<0>(p[0][0], p[0][1], p[1][0], p[1][1]);
+                else lgkm_wait_for<0>(p[0][0], p[0][1]);
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
+                for (int i = 0; i < VB; ++i)
                     if (c0 + 4 * i < CPR) tile(c0 + 4 * i, p[i][0], p[i][1]);
             }
         }
@@ -226,23 +235,25 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
         }
         // ---- horizontal on the matrix cores: D[out byte j][row u] = W[j][window byte] x
         // inter[window byte][u]; a group = GP output pixels of all 16 rows ----
-        constexpr int GP = B == 3 ? 4 : 2, NG = kMTW / GP;
-        // wave w: groups GPW w .. (16 px); D dwords -> the wave's part of the output tile,
-        // then 16-byte row pieces to HBM
-        constexpr int GPW = NG / 4;
+        constexpr int GP = G::GP, GPW = G::GPW, HB = 4;
+        // wave w: groups GPW w .. (16 px); D dwords -> the wave's output tile, then 16-byte
+        // row pieces to HBM
         if (x0 + 16 * wave >= a.ow) continue;  // (the next step starts with a barrier)
+        uint32_t pk[GPW];  // the packed D dwords of the wave's groups (after all its window reads)
 #pragma unroll
-        for (int gb = 0; gb < GPW; gb += 4) {
-            rc_v4i bv[4];
+        for (int gb = 0; gb < GPW; gb += HB) {
+            rc_v4i bv[HB];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < HB; ++i) {
                 const uint32_t ws = static_cast<uint32_t>((ib0 & ~7) + 2 * B * GP * (GPW * wave + gb + i));
                 const uint32_t ad = inter_l + static_cast<uint32_t>(n * IS) + ws + 16 * kg;
                 bv[i] = __builtin_bit_cast(rc_v4i, lds_rd64x2(ad));
             }
-            lgkm_wait_for<0>(bv[0], bv[1], bv[2], bv[3]);
+            if constexpr (HB == 4) lgkm_wait_for<0>(bv[0], bv[1], bv[2], bv[3]);
+            else if constexpr (HB == 2) lgkm_wait_for<0>(bv[0], bv[1]);
+            else lgkm_wait_for<0>(bv[0]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < HB; ++i) {
                 rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
                 dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(wh, bv[i], dh, 0, 0, 0);
                 dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(wl, bv[i], dl, 0, 0, 0);
@@ -251,17 +262,23 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                 const int s2 = (dh[2] << 6) + dl[2], s3 = (dh[3] << 6) + dl[3];
                 asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(s0), "v"(s1));
                 asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(s2), "v"(s3));
-                if (4 * kg < B * GP)
-                    lds_wr32(otile_l + static_cast<uint32_t>(n * OS + 16 * B * wave + B * GP * (gb + i) + 4 * kg),
-                             __builtin_amdgcn_perm(hi, lo, 0x05040100u));
+                pk[gb + i] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
             }
         }
+        // the output tile: 16 rows x 16 B bytes in the intermediate bytes only this wave's
+        // windows cover (EXS on), written once the wave has read all its windows (a wave's
+        // LDS operations complete in order); the next step's vertical pass overwrites them
+        // only after its barrier
+        const uint32_t otile_w = inter_l + static_cast<uint32_t>(G::EXS + G::EXW * wave);
+#pragma unroll
+        for (int g = 0; g < GPW; ++g)
+            if (4 * kg < B * GP) lds_wr32(otile_w + static_cast<uint32_t>(n * IS + B * GP * g + 4 * kg), pk[g]);
         {
             constexpr int LPR = B;  // 16-byte pieces per tile row of a wave (16 px x B bytes)
             const int u = lane / LPR, c = lane - u * LPR;
             lgkm_wait();
             if (u < kMN) {
-                const uint32_t ad = otile_l + static_cast<uint32_t>(u * OS + 16 * B * wave + 16 * c);
+                const uint32_t ad = otile_w + static_cast<uint32_t>(u * IS + 16 * c);
                 rc_u4 v = lds_rd64x2(ad);
                 lgkm_wait_for<0>(v);
                 const int y = kMN * k + u;

@@ -47,6 +47,8 @@ def main():
     variants = extra or VARIANTS
     dev = torch.device("cuda", 0)
     check(lib.mipx_set_device(0))
+    if os.environ.get("RS_SAMPLING"):  # corner / centre (mipx_set_reduce_sampling)
+        check(lib.mipx_set_reduce_sampling({"corner": 0, "centre": 1}[os.environ["RS_SAMPLING"]]))
     st = torch.cuda.current_stream(dev)
     sp = C.c_void_p(st.cuda_stream)
     for (w, h, b, n, hs, vs) in SHAPES:
