@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <utility>
 #include <vector>
 
 #include "device_common.h"
@@ -140,8 +141,10 @@ __device__ __forceinline__ void rc_edge_frag(const float *tabf, int taps, int pp
 
 // KMAX ring chunks per lane per step (16 bytes each), NKS horizontal K steps (64 bytes
 // each).  Output rows start on a dword (host-checked).
-template <int B, int NKS, int KMAX>
-__global__ void __launch_bounds__(kRcNT) k_rcol(RcArgs a) {
+// WPE: the minimum waves per SIMD the register allocation must allow (1: the compiler's
+// choice; 4 for the one build where that costs only two spilled registers)
+template <int B, int NKS, int KMAX, int WPE>
+__global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_rcol(RcArgs a) {
     constexpr int WV = kRcNT / 64, XW = 16 * WV;
     constexpr int UPW = B;  // horizontal units per wave: XW B / 16 / WV
     extern __shared__ __attribute__((aligned(16))) uint32_t rcs[];
@@ -570,7 +573,7 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     const char *ews = tune_env("MIPX_RCOL_WST");
     a.wst = !(ews && *ews == '0') ? (!out_al ? 3 : (ow * b) % 16 == 0 ? 1 : 2) : 0;
     const void *fn = nullptr;
-#define MIPX_RC_K(B_, NKS_, KM_) fn = reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_>);
+#define MIPX_RC_K(B_, NKS_, KM_) fn = reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, 1>);
 #define MIPX_RC_KM(B_, NKS_) \
     if (kmax == 3) { MIPX_RC_K(B_, NKS_, 3) } else { MIPX_RC_K(B_, NKS_, 6) }
     if (b == 3) {
@@ -585,18 +588,37 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // steps; pick the split that minimises (rounds of resident blocks) x (steps + 2)
     a.strips = (ow + 63) / 64;
     const long long cols = static_cast<long long>(a.strips) * n;
-    const int per_cu = occupancy_per_cu(fn, kRcNT, lds, 2);
-    const long long slots = static_cast<long long>(device_cu_count()) * per_cu;
+    auto plan = [&](const void *f, int *segs_out) {
+        const long long slots = static_cast<long long>(device_cu_count()) * occupancy_per_cu(f, kRcNT, lds, 2);
+        double best = 1e300;
+        int rounds = 0;
+        for (int segs = 1; segs <= a.ksteps; ++segs) {
+            const int ss = (a.ksteps + segs - 1) / segs;
+            if (segs > 1 && ss < 4) break;
+            const long long blocks = cols * ((a.ksteps + ss - 1) / ss);
+            const long long r = (blocks + slots - 1) / slots;
+            const double cost = static_cast<double>(r) * (ss + 2);
+            if (cost < best - 1e-9) {
+                best = cost;
+                *segs_out = segs;
+                rounds = static_cast<int>(r);
+            }
+        }
+        return std::make_pair(best, rounds);
+    };
     int best_segs = 1;
-    double best = 1e300;
-    for (int segs = 1; segs <= a.ksteps; ++segs) {
-        const int ss = (a.ksteps + segs - 1) / segs;
-        if (segs > 1 && ss < 4) break;
-        const long long blocks = cols * ((a.ksteps + ss - 1) / ss);
-        const double cost = static_cast<double>((blocks + slots - 1) / slots) * (ss + 2);
-        if (cost < best - 1e-9) {
-            best = cost;
-            best_segs = segs;
+    const double best = plan(fn, &best_segs).first;
+    // <3, 1, 3> also has a 4-waves-per-SIMD build (128 VGPRs, 2 spilled): it wins only when
+    // the whole launch then fits one round of resident blocks in fewer steps per block
+    // (364x273 RGB, C4's thumbnail reduce: -18 %); with more rounds the spills cost 3-5 %
+    // (480x270, 500x375, 1080p; profiles/r04/small/rcol_w4_ab.jsonl)
+    if (b == 3 && nks == 1 && kmax == 3) {
+        const void *f4 = reinterpret_cast<const void *>(&k_rcol<3, 1, 3, 4>);
+        int segs4 = 1;
+        const auto p4 = plan(f4, &segs4);
+        if (p4.second == 1 && p4.first < best - 1e-9) {
+            fn = f4;
+            best_segs = segs4;
         }
     }
     a.seg_steps = (a.ksteps + best_segs - 1) / best_segs;

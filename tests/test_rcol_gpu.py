@@ -125,3 +125,16 @@ def test_reduce_centre_c2_c1_shapes(gpu, oracle, rng, centre):
         got = gpu.execute(p, imgs)
         for i in range(2):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"centre plan {iw}x{ih}x{b} {opts}")
+
+
+@pytest.mark.parametrize("n", [128, 40, 3])
+def test_rcol_four_wave_build(gpu, oracle, rng, n):
+    """C4's thumbnail reduce (12 MP / 11 = 364x273 -> 256x256): with 40 or 128 images the
+    whole launch fits one round of resident blocks at 4 waves per SIMD, so the launcher
+    takes k_rcol<3, 1, 3>'s 4-wave build (2 segments per strip); 3 images stay on the
+    default build.  Both must give the oracle's bytes."""
+    h, w, hs, vs = 273, 364, 1.421875, 1.06640625
+    imgs = np.stack([rand_img(rng, h, w, 3) if i % 2 else smooth_img(rng, h, w, 3) for i in range(n)])
+    got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+    for i in range(n):
+        assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"4-wave build n={n} img{i}")
