@@ -27,6 +27,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402  (import before libmipx: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
+import launch_ranks  # noqa: E402
+
 W_IN, H_IN, BANDS = 3840, 2160, 3
 W_OUT, H_OUT = 1920, 1080
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -38,7 +40,9 @@ C2_KERNEL = {"corner": "k_reduce2x2<3, 66>", "centre": "k_reduce2m<3>"}
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) to time; without torchrun, N > 1 starts N rank processes "
+                         "(launch_ranks.py); under torchrun it must equal WORLD_SIZE (default: WORLD_SIZE or 1)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU (BASELINE C2: 256)")
@@ -50,6 +54,10 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--sampling", choices=["corner", "centre"], default=None,
                     help="libvips reduce sampling convention (PARITY_ASSUMPTIONS.md row 1); default: the library's")
+    ap.add_argument("--no-centre-leg", action="store_true",
+                    help="skip the second, centre-convention leg (the 'centre' object of the line)")
+    ap.add_argument("--stub-step-ms", type=float, default=0.0,
+                    help="harness test only: each step sleeps (rank + 1) x this many ms, no GPU work")
     return ap.parse_args()
 
 
@@ -205,9 +213,94 @@ def timed_region(step, steps, warmup, sync, world):
     return float(t.item())
 
 
+METRIC = "images/sec (4K RGB->1080p Lanczos3 batch) + achieved HBM GB/s, 1/2/4/8 GPUs"
+
+
+def headline(args, world, n, wall_max, sampling, kernel):
+    """The JSON line's common part: value = every rank's images / the max-over-ranks wall."""
+    return {
+        "metric": METRIC,
+        "value": round(n * world * args.steps / wall_max, 1),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic uniform-random uchar, device-resident (seed 20241220+rank)",
+        "config": {"workload": "C2: batched 3840x2160x3 -> 1920x1080x3 Lanczos3 reduce (bimg "
+                               f"/resize?width=1920&height=1080), {sampling} sampling convention "
+                               f"(PARITY_ASSUMPTIONS.md row 1), {kernel.split('<')[0]}",
+                   "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world} (independent shards)"},
+    }
+
+
+def stub_main(args, world, rank):
+    """The rank harness without a GPU (tests/test_bench_cpu.py): each step sleeps
+    (rank + 1) x --stub-step-ms, so the max-over-ranks timing is the slowest rank's."""
+    delay = args.stub_step_ms * 1e-3 * (rank + 1)
+    wall_max = timed_region(lambda: time.sleep(delay), args.steps, args.warmup, lambda: None, world)
+    if rank == 0:
+        line = headline(args, world, args.batch, wall_max, "corner", C2_KERNEL["corner"])
+        line["data"] = f"STUB: sleep {args.stub_step_ms} ms x (rank + 1) per step, no GPU work (harness test only)"
+        print(json.dumps(line), flush=True)
+
+
+def c2_setup(ia, lib, C, local, rank, n):
+    """Plan, resident batch and workspace of C2 under the current sampling setting."""
+    plan = ia.plan_make(ia.make_opts(width=W_OUT, height=H_OUT, embed=1), ia.make_input(W_IN, H_IN, BANDS, "png"))
+    conv = 1 if ia.reduce_sampling() == "centre" else 0
+    assert plan.describe() == [("reduce", (0,) * 7 + (conv,), (2.0, 2.0, 0.0, 0.0), (W_OUT, H_OUT, BANDS))], \
+        plan.describe()
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device=dev)
+    g.manual_seed(20241220 + rank)
+    d_in = torch.randint(0, 256, (n, W_IN * H_IN * BANDS), dtype=torch.uint8, device=dev, generator=g)
+    d_out = torch.empty((n, W_OUT * H_OUT * BANDS), dtype=torch.uint8, device=dev)
+    wsb = lib.mipx_workspace_bytes(C.byref(plan), n)
+    d_ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    return plan, d_in, d_out, d_ws, wsb
+
+
+def verify_c2(d_in, d_out, n, sampling):
+    """Images 0 and n - 1 byte-compared with the oracle (checker only, after timing)."""
+    from oracle import oracle as o
+    o.set_switch("reduce_centre", int(sampling == "centre"))
+    idx = [0, n - 1]
+    got = d_out[idx].cpu().numpy().reshape(len(idx), H_OUT, W_OUT, BANDS)
+    src = d_in[idx].cpu().numpy().reshape(len(idx), H_IN, W_IN, BANDS)
+    ok = all(np.array_equal(got[i], o.reduce(src[i], 2.0, 2.0)) for i in range(len(idx)))
+    if not ok:
+        raise SystemExit(f"bench: GPU output differs from the oracle ({sampling} convention)")
+    return ok
+
+
+def roofline(kernel, kern_ms, alg_bytes):
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(kernel)
+    return {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+            "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes}
+
+
 def main():
     args = parse()
+    if launch_ranks.needs_spawn(args.gpus):  # plain `python bench.py --gpus N`: N rank processes
+        rc, outs = launch_ranks.run_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+        sys.stdout.write(outs[0])
+        sys.stdout.flush()
+        raise SystemExit(rc)
+    want_world = launch_ranks.resolve_world(args.gpus)
     world, rank, local = dist_env()
+    assert world == want_world, (world, want_world)
+    if args.stub_step_ms > 0:
+        stub_main(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     torch.cuda.set_device(local)
     import imaginary_amd as ia
     from imaginary_amd._abi import check, lib
@@ -219,24 +312,19 @@ def main():
     kernel = C2_KERNEL[sampling]
 
     n = args.batch
-    plan = ia.plan_make(ia.make_opts(width=W_OUT, height=H_OUT, embed=1), ia.make_input(W_IN, H_IN, BANDS, "png"))
-    assert plan.describe() == [("reduce", (0,) * 8, (2.0, 2.0, 0.0, 0.0), (W_OUT, H_OUT, BANDS))], plan.describe()
+    plan, d_in, d_out, d_ws, wsb = c2_setup(ia, lib, C, local, rank, n)
     in_img = W_IN * H_IN * BANDS
     out_img = W_OUT * H_OUT * BANDS
-    dev = torch.device("cuda", local)
-    g = torch.Generator(device=dev)
-    g.manual_seed(20241220 + rank)
-    d_in = torch.randint(0, 256, (n, in_img), dtype=torch.uint8, device=dev, generator=g)
-    d_out = torch.empty((n, out_img), dtype=torch.uint8, device=dev)
-    wsb = lib.mipx_workspace_bytes(C.byref(plan), n)
-    d_ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.current_stream(torch.device("cuda", local))
     sp = C.c_void_p(stream.cuda_stream)
 
-    def step():
-        check(lib.mipx_execute_dev(C.byref(plan), n, d_in.data_ptr(), d_out.data_ptr(), None,
-                                   d_ws.data_ptr(), wsb, sp), "mipx_execute_dev")
+    def make_step(pl, ws, wsz):
+        def step():
+            check(lib.mipx_execute_dev(C.byref(pl), n, d_in.data_ptr(), d_out.data_ptr(), None,
+                                       ws.data_ptr(), wsz, sp), "mipx_execute_dev")
+        return step
 
+    step = make_step(plan, d_ws, wsb)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     count = {"i": 0}
@@ -256,45 +344,44 @@ def main():
 
     verify = None
     if not args.no_verify and rank == 0:
-        from oracle import oracle as o
-        o.set_switch("reduce_centre", int(sampling == "centre"))
-        idx = [0, n - 1]
-        got = d_out[idx].cpu().numpy().reshape(len(idx), H_OUT, W_OUT, BANDS)
-        src = d_in[idx].cpu().numpy().reshape(len(idx), H_IN, W_IN, BANDS)
-        verify = all(np.array_equal(got[i], o.reduce(src[i], 2.0, 2.0)) for i in range(len(idx)))
-        if not verify:
-            raise SystemExit("bench: GPU output differs from the oracle")
+        verify = verify_c2(d_in, d_out, n, sampling)
+
+    # the other reduce sampling convention's kernel on the same batch, same process, after
+    # the headline leg (PARITY_ASSUMPTIONS.md row 1 is unresolved: the line carries both)
+    other = None
+    if not args.no_centre_leg and sampling == "corner":
+        ia.set_reduce_sampling("centre")
+        try:
+            cplan = ia.plan_make(ia.make_opts(width=W_OUT, height=H_OUT, embed=1),
+                                 ia.make_input(W_IN, H_IN, BANDS, "png"))
+        finally:
+            ia.set_reduce_sampling(sampling)  # the plan keeps the centre convention (ABI v6)
+        cws_b = lib.mipx_workspace_bytes(C.byref(cplan), n)
+        cws = torch.empty(max(cws_b, 1), dtype=torch.uint8, device=d_in.device)
+        cstep = make_step(cplan, cws, cws_b)
+        for _ in range(args.warmup):
+            cstep()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            cstep()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        cms = e0.elapsed_time(e1) / args.steps
+        other = {"sampling": "centre", "images_per_sec_per_gpu": round(n / (cms * 1e-3), 1),
+                 "roofline": roofline(C2_KERNEL["centre"], cms, n * (in_img + out_img)),
+                 "verified_vs_oracle": verify_c2(d_in, d_out, n, "centre") if (not args.no_verify and rank == 0)
+                 else None}
+
     if rank == 0:
-        images = n * world * args.steps
-        value = images / wall_max
-        alg_bytes = n * (in_img + out_img)
-        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(kernel)
-        line = {
-            "metric": "images/sec (4K RGB->1080p Lanczos3 batch) + achieved HBM GB/s, 1/2/4/8 GPUs",
-            "value": round(value, 1),
-            "unit": "images/sec",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic uniform-random uchar, device-resident (seed 20241220+rank)",
-            "config": {"workload": "C2: batched 3840x2160x3 -> 1920x1080x3 Lanczos3 reduce (bimg "
-                                   f"/resize?width=1920&height=1080), {sampling} sampling convention "
-                                   f"(PARITY_ASSUMPTIONS.md row 1), {kernel.split('<')[0]}",
-                       "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world} (independent shards)"},
-            "achieved_hbm_gbs": round(achieved, 1),
-            "roofline": {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
-            "verified_vs_oracle": verify,
-        }
+        line = headline(args, world, n, wall_max, sampling, kernel)
+        rl = roofline(kernel, kern_ms, n * (in_img + out_img))
+        line["achieved_hbm_gbs"] = rl["achieved"]
+        line["roofline"] = rl
+        line["verified_vs_oracle"] = verify
+        if other:
+            line["centre"] = other
         if not args.no_cpu and world == 1:  # the CPU figures are N = 1 figures
             line["cpu_baseline"] = cpu_baseline(args)
             line["c1_cpu_reference"] = c1_cpu_reference(args)

@@ -23,7 +23,43 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+import launch_ranks  # noqa: E402
+
+
+def _aggregate(texts, nranks):
+    """One line per config from the ranks' lines: the whole job's images over the
+    slowest rank's step time (the ranks time after a common barrier)."""
+    per = {}
+    for r, t in enumerate(texts):
+        for ln in t.splitlines():
+            if ln.startswith("{"):
+                d = json.loads(ln)
+                per.setdefault(d["config"], []).append(d)
+    for name, ds in per.items():
+        ms = max(d["ms_per_step"] for d in ds)
+        imgs = sum(d["images_per_step"] for d in ds)
+        out = dict(ds[0])
+        out.update({"n_gpus": nranks, "images_per_step": imgs, "ms_per_step": ms,
+                    "images_per_sec": round(imgs / (ms * 1e-3), 1),
+                    "verified_vs_oracle": all(d["verified_vs_oracle"] for d in ds),
+                    "per_rank": [{k: d[k] for k in ("images_per_step", "ms_per_step", "device_ms_per_step",
+                                                    "hbm_frac")} for d in ds]})
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":  # plain `python bench_configs.py --gpus N`: N rank processes, before any GPU call
+    _pre = argparse.ArgumentParser(add_help=False)
+    _pre.add_argument("--gpus", type=int, default=None)
+    _gpus = _pre.parse_known_args()[0].gpus
+    if launch_ranks.needs_spawn(_gpus):
+        _rc, _outs = launch_ranks.run_ranks(_gpus, os.path.abspath(__file__), sys.argv[1:])
+        if _rc == 0:
+            _aggregate(_outs, _gpus)
+        raise SystemExit(_rc)
+    launch_ranks.resolve_world(_gpus)
+
 import torch  # noqa: E402  (before libmipx: one HIP runtime)
+import torch.distributed as dist  # noqa: E402
 
 import imaginary_amd as ia  # noqa: E402
 import workloads  # noqa: E402
@@ -110,17 +146,24 @@ def time_groups(run_all, steps, warmup, stream):
         if w0.elapsed_time(w1) >= WARM_MS:
             break
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    multi = dist.is_initialized() and dist.get_world_size() > 1
+    if multi:  # every rank starts its timed steps together
+        dist.barrier()
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(steps):
         run_all()
     e1.record(stream)
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps, e0.elapsed_time(e1) / steps
+    wall = time.perf_counter() - t0
+    if multi:
+        dist.barrier()
+    return wall / steps, e0.elapsed_time(e1) / steps
 
 
 def line(name, workload, images, wall_s, dev_ms, alg_bytes, verified, extra=None):
     d = {"config": name, "workload": workload, "images_per_sec": round(images / wall_s, 1),
+         "images_per_step": images, "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
          "ms_per_step": round(wall_s * 1e3, 3), "device_ms_per_step": round(dev_ms, 3),
          "achieved_gbs": round(alg_bytes / (dev_ms * 1e-3) / 1e9, 1),
          "hbm_frac": round(alg_bytes / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -279,6 +322,8 @@ def e2e_c(args, dev, sp, stream):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="C3,C4,C5")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks; without torchrun N > 1 starts N processes and prints one aggregate line per config")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--warm-ms", type=float, default=200.0, help="device-time warm-up after --warmup steps; 0: none")
@@ -303,6 +348,10 @@ def main():
         ia.set_reduce_sampling(args.sampling)
         o.set_switch("reduce_centre", int(args.sampling == "centre"))
     globals()["WARM_MS"] = args.warm_ms
+    world = launch_ranks.resolve_world(args.gpus)
+    if world > 1 and not dist.is_initialized():  # barriers around the timed steps only; shards are independent
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=int(os.environ.get("RANK", "0")), world_size=world)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     check(lib.mipx_set_device(local), "mipx_set_device")
@@ -312,6 +361,8 @@ def main():
     for c in args.configs.split(","):
         {"C3": c3, "C4": c4, "C5": c5, "E2E": e2e, "E2EC": e2e_c}[c](args, dev, sp, stream)
         torch.cuda.empty_cache()
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

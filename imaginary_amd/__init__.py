@@ -6,7 +6,7 @@ Importing it fails when libmipx.so has not been built: there is no CPU path.
 """
 from ._abi import lib, MipxError, MipxPlan, MipxOpts, MipxInput, LIB_PATH, TYPES, EXTEND, GRAVITY  # noqa: F401
 from ._abi import (MIPX_OK, MIPX_EINVAL, MIPX_EUNSUPPORTED, MIPX_ENOMEM, MIPX_ENODEV, MIPX_EDEVICE,  # noqa: F401
-                   MIPX_ETIMEOUT, MIPX_ENOTINIT, MIPX_ESTALE)
+                   MIPX_ETIMEOUT, MIPX_ENOTINIT, MIPX_ESTALE, MIPX_EBUSY)
 from .engine import (DeviceBuffer, Engine, device_count, execute, fit_dimension, make_input,  # noqa: F401
                      make_opts, plan_chain, plan_make, reduce_sampling, run_op, set_reduce_sampling,
                      smartcrop_origins, synchronize)

@@ -22,6 +22,7 @@ MIPX_EDEVICE = -5
 MIPX_ETIMEOUT = -6
 MIPX_ENOTINIT = -7
 MIPX_ESTALE = -8
+MIPX_EBUSY = -9
 
 GRAVITY = {"centre": 0, "north": 1, "east": 2, "south": 3, "west": 4, "smart": 5}
 EXTEND = {"black": 0, "copy": 1, "repeat": 2, "mirror": 3, "white": 4, "background": 5, "lastpixel": 6}

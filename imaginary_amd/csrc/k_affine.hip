@@ -349,7 +349,11 @@ __global__ void __launch_bounds__(256) k_enlarge2(Enl2Args a) {
     const int ma = kE2RB * band, mb = min(ma + kE2RB, a.h);
     const int rfirst = ma - 2, rlast = mb + 1;  // H rows this band needs
     const int pitch = a.w * B;
-    const __amdgpu_buffer_rsrc_t src = image_rsrc(a.in + img * a.in_img, a.in_img);
+    // over the dword-aligned-down image base, range rounded up to the dword holding the
+    // last byte: the tail dword of a chunk that ends at the image's last byte is then in
+    // range (with image_rsrc it straddled num_records and read 0 when in_img % 4 != 0)
+    int delta = 0;
+    const __amdgpu_buffer_rsrc_t src = image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &delta);
     u8 *dst = a.out + img * a.out_img;
 
     // ---- staging: chunk q = lane + 64 j of an 8-row batch = (row t, column chunk cc) ----
@@ -372,7 +376,7 @@ __global__ void __launch_bounds__(256) k_enlarge2(Enl2Args a) {
                 const uint32_t f = 0x01010101u * static_cast<uint32_t>(a.fill);
                 v[j] = rc_u4{f, f, f, f};
             } else if (b0 >= 0 && b0 + 16 <= pitch) {
-                const int off = sr * pitch + b0;
+                const int off = sr * pitch + b0 + delta;
                 const rc_u4 p = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off & ~3, 0, 0));
                 const uint32_t e = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
                 const int sh = off & 3;

@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // horizontal pass: units wave + WV i, operands from registers, every unit's LDS
     // reads in flight together
     auto horizontal = [&](uint32_t *res) {
-        rc_u4 q[UPW][NKS];
+        rc_u2x2 q[UPW][NKS];
 #pragma unroll
         for (int i = 0; i < UPW; ++i) {
             const uint32_t ir = inter_l + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg);
@@ -415,7 +415,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
                 rc_pin(q[i][ks]);
-                const rc_v4i bz = __builtin_bit_cast(rc_v4i, q[i][ks]);
+                const rc_v4i bz = __builtin_bit_cast(rc_v4i, rc_join(q[i][ks]));
                 ah = __builtin_amdgcn_mfma_i32_16x16x64_i8(th[i][ks], bz, ah, 0, 0, 0);
                 al = __builtin_amdgcn_mfma_i32_16x16x64_i8(tl[i][ks], bz, al, 0, 0, 0);
             }

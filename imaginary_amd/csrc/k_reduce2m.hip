@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <vector>
 
 #include "device_common.h"
@@ -45,6 +46,7 @@ namespace {
 
 using namespace dev;
 
+constexpr int kMaxDevices = 64;  // operand-table cache slots (HIP device ordinals)
 constexpr int kMTW = 64;    // output pixels per strip
 constexpr int kMN = 16;     // output rows per step (the MFMA N)
 constexpr int kMNT = 256;
@@ -242,16 +244,19 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
         uint32_t pk[GPW];  // the packed D dwords of the wave's groups (after all its window reads)
 #pragma unroll
         for (int gb = 0; gb < GPW; gb += HB) {
-            rc_v4i bv[HB];
+            rc_u2x2 bq[HB];
 #pragma unroll
             for (int i = 0; i < HB; ++i) {
                 const uint32_t ws = static_cast<uint32_t>((ib0 & ~7) + 2 * B * GP * (GPW * wave + gb + i));
                 const uint32_t ad = inter_l + static_cast<uint32_t>(n * IS) + ws + 16 * kg;
-                bv[i] = __builtin_bit_cast(rc_v4i, lds_rd64x2(ad));
+                bq[i] = lds_rd64x2(ad);
             }
-            if constexpr (HB == 4) lgkm_wait_for<0>(bv[0], bv[1], bv[2], bv[3]);
-            else if constexpr (HB == 2) lgkm_wait_for<0>(bv[0], bv[1]);
-            else lgkm_wait_for<0>(bv[0]);
+            if constexpr (HB == 4) lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3]);
+            else if constexpr (HB == 2) lgkm_wait_for<0>(bq[0], bq[1]);
+            else lgkm_wait_for<0>(bq[0]);
+            rc_v4i bv[HB];
+#pragma unroll
+            for (int i = 0; i < HB; ++i) bv[i] = __builtin_bit_cast(rc_v4i, rc_join(bq[i]));
 #pragma unroll
             for (int i = 0; i < HB; ++i) {
                 rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
@@ -279,8 +284,9 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
             lgkm_wait();
             if (u < kMN) {
                 const uint32_t ad = otile_w + static_cast<uint32_t>(u * IS + 16 * c);
-                rc_u4 v = lds_rd64x2(ad);
-                lgkm_wait_for<0>(v);
+                rc_u2x2 vq = lds_rd64x2(ad);
+                lgkm_wait_for<0>(vq);
+                const rc_u4 v = rc_join(vq);
                 const int y = kMN * k + u;
                 const int xb = (x0 + 16 * wave) * B + 16 * c;
                 const int rowb = a.ow * B;
@@ -354,9 +360,29 @@ int reduce2m_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
         sum += taps12[i];
         if (taps12[i] < -128 * 64 || taps12[i] > 127 * 64 + 63) return MIPX_EUNSUPPORTED;  // i8 hi / lo split
     }
-    const std::vector<uint32_t> ops = b == 3 ? r2m_operands<3>(taps12) : r2m_operands<4>(taps12);
-    a.ops = static_cast<const rc_u4 *>(device_blob(ops.data(), ops.size() * sizeof(uint32_t)));
-    if (!a.ops) return MIPX_EDEVICE;
+    // the operand table depends on (device, bands) only (taps12 is always the phase-64 row
+    // of the shrink-2 table): cached lock-free after the first launch (it was
+    // rebuilt and looked up by contents under the table mutex on every launch)
+    struct Cached {
+        const rc_u4 *ops;
+        unsigned gen;
+    };
+    static std::mutex mu;
+    static Cached cache[kMaxDevices][2];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return MIPX_EDEVICE;
+    const unsigned gen = device_tables_generation();
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        Cached *slot = dev < kMaxDevices ? &cache[dev][b - 3] : nullptr;
+        a.ops = slot && slot->gen == gen ? slot->ops : nullptr;
+        if (!a.ops) {
+            const std::vector<uint32_t> ops = b == 3 ? r2m_operands<3>(taps12) : r2m_operands<4>(taps12);
+            a.ops = static_cast<const rc_u4 *>(device_blob(ops.data(), ops.size() * sizeof(uint32_t)));
+            if (!a.ops) return MIPX_EDEVICE;
+            if (slot) *slot = Cached{a.ops, gen};
+        }
+    }
     a.seed = 128 * sum + 2048;
     a.x_end = x1;
     a.y_end = y1;

@@ -26,10 +26,29 @@ int hip_fail(hipError_t e, const char *what);  // records detail, returns MIPX_E
 // mipx_tuning_reload): nullptr when unset.  Launchers call this, never getenv.
 const char *tune_env(const char *name);
 void tune_reload();
-// mipx_set_reduce_sampling(MIPX_SAMPLE_CENTRE): every Lanczos reduce samples output o at
-// (o + 0.5) * shrink - 0.5 (libvips' centre convention) instead of o * shrink
-// (PARITY_ASSUMPTIONS.md row 1)
+// The Lanczos reduce sampling convention (PARITY_ASSUMPTIONS.md row 1): under
+// MIPX_SAMPLE_CENTRE output o samples (o + 0.5) * shrink - 0.5 (libvips' centre
+// convention) instead of o * shrink.  reduce_centre() is what every reduce launcher and
+// the demand-region walk read: the innermost SamplingScope of this thread, else the
+// process setting (mipx_set_reduce_sampling).  execute_plan opens a scope with the
+// convention each reduce / smartcrop step recorded at mipx_plan_make time (step a[7]), and
+// the per-op entry points snapshot the process setting once per call, so one launch never
+// mixes conventions.
 bool reduce_centre();
+int reduce_sampling_now();  // the process setting (what mipx_plan_make records)
+class SamplingScope {
+   public:
+    explicit SamplingScope(int convention);  // this convention until the scope ends
+    SamplingScope();                          // snapshot: the enclosing scope's, else the process setting
+    ~SamplingScope();
+    SamplingScope(const SamplingScope &) = delete;
+    SamplingScope &operator=(const SamplingScope &) = delete;
+
+   private:
+    int prev_;
+};
+// requests submitted through mipx_submit and not yet retired (mipx_runtime.cpp)
+long long requests_in_flight();
 inline double reduce_x_host(int o, double s, bool centre) { return centre ? (o + 0.5) * s - 0.5 : o * s; }
 
 // ---- device properties, cached per device (mipx_tuning.cpp) --------------------
@@ -102,6 +121,9 @@ const float *device_gauss_table(double sigma, double min_ampl, int *n_taps, int 
 // `bytes` of host data on the current device, cached by contents (small constant tables)
 const void *device_blob(const void *data, size_t bytes);
 void free_device_tables();
+// bumped by free_device_tables: a launcher that caches a table pointer outside the maps
+// above keeps the generation it was made in and refetches when it changed
+unsigned device_tables_generation();
 
 // ---- generic separable passes (k_sep.hip) -----------------------------------
 enum { kSepReduce = 0, kSepConv = 1 };

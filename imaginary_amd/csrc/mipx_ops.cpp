@@ -38,6 +38,7 @@ size_t mipx_op_workspace_bytes(int32_t op, int32_t n, int32_t w, int32_t h, int3
 int mipx_op_reducev(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h, int32_t bands,
                     double vshrink, void *stream) {
     if (!d_in || !d_out || !geom_ok(n, w, h, bands) || !(vshrink >= 1.0)) return MIPX_EINVAL;
+    const SamplingScope sampling;  // one convention for the whole call
     if (vshrink == 1.0) {
         return device_copy(d_out, d_in, static_cast<size_t>(n) * w * h * bands, as_stream(stream));
     }
@@ -47,6 +48,7 @@ int mipx_op_reducev(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, i
 int mipx_op_reduceh(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, int32_t h, int32_t bands,
                     double hshrink, void *stream) {
     if (!d_in || !d_out || !geom_ok(n, w, h, bands) || !(hshrink >= 1.0)) return MIPX_EINVAL;
+    const SamplingScope sampling;  // one convention for the whole call
     if (hshrink == 1.0) {
         return device_copy(d_out, d_in, static_cast<size_t>(n) * w * h * bands, as_stream(stream));
     }
@@ -57,6 +59,7 @@ int mipx_op_reduce(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32_t w, in
                    double hshrink, double vshrink, void *d_ws, size_t ws_bytes, void *stream) {
     if (!d_in || !d_out || !geom_ok(n, w, h, bands) || !(hshrink >= 1.0) || !(vshrink >= 1.0))
         return MIPX_EINVAL;
+    const SamplingScope sampling;  // one convention for the whole call (the enclosing plan step's, if any)
     hipStream_t st = as_stream(stream);
     if (reduce2_eligible(d_in, w, h, bands, hshrink, vshrink)) return reduce2_launch(d_in, d_out, n, w, h, bands, st);
     if (vshrink == 1.0) return mipx_op_reduceh(d_in, d_out, n, w, h, bands, hshrink, stream);
@@ -153,6 +156,7 @@ int mipx_op_colourspace_bw(const uint8_t *d_in, uint8_t *d_out, int32_t n, int32
 int mipx_op_smartcrop_origin(const uint8_t *d_in, int32_t *d_origins, int32_t n, int32_t w, int32_t h, int32_t bands,
                              int32_t cw, int32_t ch, void *d_ws, size_t ws_bytes, void *stream) {
     if (!d_in || !d_origins || !geom_ok(n, w, h, bands)) return MIPX_EINVAL;
+    const SamplingScope sampling;  // one convention for the whole call
     return smartcrop_origins(d_in, d_origins, n, w, h, bands, cw, ch, d_ws, ws_bytes, as_stream(stream));
 }
 

@@ -389,6 +389,7 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
                 pb.push(MIPX_OP_REDUCE);
                 pb.last().d[0] = 1.0 / rx;
                 pb.last().d[1] = 1.0 / ry;
+                pb.last().a[7] = mipx::reduce_sampling_now();  // the plan keeps its convention (ABI v6)
                 pb.geom(out_size_reduce(pb.w(), 1.0 / rx), out_size_reduce(pb.h(), 1.0 / ry),
                         pb.b());
             } else if (!(rx == 1.0 && ry == 1.0)) {
@@ -418,6 +419,7 @@ extern "C" int mipx_plan_make(const mipx_opts *opts, const mipx_input *in, mipx_
                 const int w = std::min(cw, o.width), h = std::min(ch, o.height);
                 pb.last().a[0] = w;
                 pb.last().a[1] = h;
+                pb.last().a[7] = mipx::reduce_sampling_now();  // its scorer's downsize reduces
                 pb.geom(w, h, pb.b());
             }
         } else if (o.crop) {

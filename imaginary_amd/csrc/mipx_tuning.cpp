@@ -61,9 +61,23 @@ const char *tune_env(const char *name) {
 
 namespace {
 std::atomic<int> g_sampling{MIPX_SAMPLE_CORNER};  // PARITY_ASSUMPTIONS.md row 1
+thread_local int t_sampling = -1;                 // SamplingScope's convention; -1 = none
 }  // namespace
 
-bool reduce_centre() { return g_sampling.load(std::memory_order_relaxed) == MIPX_SAMPLE_CENTRE; }
+bool reduce_centre() {
+    const int t = t_sampling;
+    return (t >= 0 ? t : g_sampling.load(std::memory_order_relaxed)) == MIPX_SAMPLE_CENTRE;
+}
+
+int reduce_sampling_now() { return g_sampling.load(std::memory_order_relaxed); }
+
+SamplingScope::SamplingScope(int convention) : prev_(t_sampling) {
+    t_sampling = convention == MIPX_SAMPLE_CENTRE ? MIPX_SAMPLE_CENTRE : MIPX_SAMPLE_CORNER;
+}
+SamplingScope::SamplingScope() : prev_(t_sampling) {
+    if (prev_ < 0) t_sampling = g_sampling.load(std::memory_order_relaxed);
+}
+SamplingScope::~SamplingScope() { t_sampling = prev_; }
 
 void tune_reload() {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -111,6 +125,14 @@ int occupancy_per_cu(const void *fn, int threads, size_t lds, int fallback) {
 
 extern "C" int mipx_set_reduce_sampling(int32_t convention) {
     if (convention != MIPX_SAMPLE_CORNER && convention != MIPX_SAMPLE_CENTRE) return MIPX_EINVAL;
+    // plans record the convention they were made under (mipx_plan_make), so queued work
+    // would not change; the setter still refuses while requests are queued or running, so
+    // a caller cannot believe its in-flight requests follow the new setting
+    if (mipx::requests_in_flight() > 0) {
+        mipx::set_error("mipx_set_reduce_sampling: %lld requests queued or running",
+                        static_cast<long long>(mipx::requests_in_flight()));
+        return MIPX_EBUSY;
+    }
     mipx::g_sampling.store(convention, std::memory_order_relaxed);
     return MIPX_OK;
 }

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MIPX_ABI_VERSION 5
+#define MIPX_ABI_VERSION 6
 
 /* ---- error codes ---- */
 #define MIPX_OK 0
@@ -54,6 +54,7 @@ extern "C" {
 #define MIPX_ETIMEOUT (-6)
 #define MIPX_ENOTINIT (-7)
 #define MIPX_ESTALE (-8)         /* unknown or already-waited ticket */
+#define MIPX_EBUSY (-9)          /* refused while requests are queued or running */
 
 /* ---- bimg enums (bimg v1.1.9 options.go / type.go) ---- */
 enum { MIPX_GRAVITY_CENTRE = 0, MIPX_GRAVITY_NORTH, MIPX_GRAVITY_EAST, MIPX_GRAVITY_SOUTH,
@@ -106,10 +107,10 @@ enum {
     MIPX_OP_ROT = 1,     /* a[0] = angle 0/90/180/270 clockwise              (vips_rot) */
     MIPX_OP_FLIP,        /* a[0] = 0 horizontal mirror, 1 vertical           (vips_flip) */
     MIPX_OP_SHRINK,      /* a[0] = hshrink, a[1] = vshrink (integer box)     (vips_shrink) */
-    MIPX_OP_REDUCE,      /* d[0] = hshrink, d[1] = vshrink, Lanczos3         (vips_reduce) */
+    MIPX_OP_REDUCE,      /* d[0] = hshrink, d[1] = vshrink, Lanczos3; a[7] = MIPX_SAMPLE_*  (vips_reduce) */
     MIPX_OP_EXTRACT,     /* a[0..3] = left, top, width, height               (vips_extract_area) */
     MIPX_OP_EMBED,       /* a[0..3] = x, y, w, h; a[4] = extend; a[5..7] bg  (vips_embed) */
-    MIPX_OP_SMARTCROP,   /* a[0..1] = width, height, attention strategy      (vips_smartcrop) */
+    MIPX_OP_SMARTCROP,   /* a[0..1] = width, height, attention; a[7] = MIPX_SAMPLE_*  (vips_smartcrop) */
     MIPX_OP_BLUR,        /* d[0] = sigma, d[1] = min_ampl                    (vips_gaussblur) */
     MIPX_OP_WATERMARK,   /* a[0..1] = left, top; d[0] = opacity  (bimg vips_watermark_image) */
     MIPX_OP_AFFINE,      /* d[0] = xscale, d[1] = yscale, a[0] = extend; bicubic  (vips_affine) */
@@ -251,10 +252,14 @@ size_t mipx_op_workspace_bytes(int32_t op, int32_t n, int32_t w, int32_t h, int3
 /* ---- parity settings (PARITY_ASSUMPTIONS.md) ----
  * The sampling convention of libvips' Lanczos3 reduce (reducev.cpp / reduceh.cpp;
  * PARITY_ASSUMPTIONS.md row 1): MIPX_SAMPLE_CORNER, output o samples X = o * shrink,
- * or MIPX_SAMPLE_CENTRE, X = (o + 0.5) * shrink - 0.5.  Process-wide, read by every
- * reduce kernel and by the demand-driven region walk; output sizes (the planner) do
- * not depend on it.  Set it before the first request or between launches, never while
- * work is in flight.  MIPX_EINVAL for any other value. */
+ * or MIPX_SAMPLE_CENTRE, X = (o + 0.5) * shrink - 0.5.  Output sizes do not depend on it.
+ * ABI v6: mipx_plan_make records the process setting in every REDUCE and SMARTCROP step
+ * (a[7]), and a plan always executes under the convention it recorded (a cached plan
+ * keeps its convention when the setting changes later; a zeroed a[7] is the corner
+ * convention, any value but 0 / 1 is MIPX_EINVAL).  The per-op entry points
+ * (mipx_op_reduce, _reducev, _reduceh, _smartcrop_origin) read the setting once per call.
+ * The setter returns MIPX_EBUSY while requests submitted through mipx_submit are queued
+ * or running, MIPX_EINVAL for any other value. */
 #define MIPX_SAMPLE_CORNER 0
 #define MIPX_SAMPLE_CENTRE 1
 int mipx_set_reduce_sampling(int32_t convention);

@@ -994,6 +994,7 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
                 push(plan, REF_OP_REDUCE, 0, 0, 0);
                 LAST(plan)->d[0] = 1.0 / rx;
                 LAST(plan)->d[1] = 1.0 / ry;
+                LAST(plan)->a[7] = SW("reduce_centre"); /* the engine's plan records the convention (mipx.h ABI v6) */
                 cw = ref_out_size_reduce(cw, 1.0 / rx);
                 ch = ref_out_size_reduce(ch, 1.0 / ry);
                 set_geom(plan, cw, ch, cb);
@@ -1018,6 +1019,7 @@ int ref_plan_make(const ref_opts *oin, const ref_input *in, ref_plan *plan) {
                 push(plan, REF_OP_SMARTCROP, 0, 0, 0);
                 LAST(plan)->a[0] = w;
                 LAST(plan)->a[1] = h;
+                LAST(plan)->a[7] = SW("reduce_centre");
                 cw = w;
                 ch = h;
                 set_geom(plan, cw, ch, cb);

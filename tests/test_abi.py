@@ -33,7 +33,8 @@ def test_library_loads_and_exports_every_declared_symbol():
 
 def test_version_and_errors_without_gpu():
     import imaginary_amd as ia
-    assert ia.lib.mipx_abi_version() == 5
+    assert ia.lib.mipx_abi_version() == 6
+    assert ia.lib.mipx_strerror(-9) == b"requests in flight"
     assert b"gfx950" in ia.lib.mipx_version()
     assert ia.lib.mipx_strerror(-2).startswith(b"operation not supported")
 
@@ -238,6 +239,9 @@ def test_inconsistent_plans_are_rejected_before_any_device_work():
     p.steps[0].a[0], p.steps[0].a[1] = 400, 100
     p.steps[0].out_w, p.steps[0].out_h = p.out_w, p.out_h = 400, 100
     cases.append(p)
+    p = _abi.MipxPlan.from_buffer_copy(good)          # reduce with no such sampling convention
+    p.steps[0].a[7] = 2
+    cases.append(p)
     p = _abi.MipxPlan.from_buffer_copy(good)          # extract outside the image
     p.n_steps = 1
     p.steps[0].op = _abi.OP_EXTRACT
@@ -274,3 +278,25 @@ def test_watermark_image_must_match_the_plan():
         assert L.mipx_submit(-1, C.byref(p), C.byref(_img(src)), C.byref(_img(wm)), C.byref(_img(dst)),
                              C.byref(t)) == -1
     assert L.mipx_submit(-1, C.byref(p), C.byref(_img(src)), None, C.byref(_img(dst)), C.byref(t)) == -1
+
+
+def test_plan_records_the_sampling_convention():
+    """ABI v6: mipx_plan_make stores the process's reduce sampling
+    convention in every REDUCE / SMARTCROP step (a[7]); flipping the setting later does
+    not change a plan already made, and the setter works with nothing in flight."""
+    import imaginary_amd as ia
+    prev = ia.reduce_sampling()
+    try:
+        ia.set_reduce_sampling("corner")
+        corner = _plan_reduce_2x(ia)
+        smart_c = ia.plan_make(ia.make_opts(width=64, height=64, crop=1, gravity=5), ia.make_input(320, 240, 3, "png"))
+        ia.set_reduce_sampling("centre")
+        centre = _plan_reduce_2x(ia)
+        smart_m = ia.plan_make(ia.make_opts(width=64, height=64, crop=1, gravity=5), ia.make_input(320, 240, 3, "png"))
+        assert corner.steps[0].a[7] == 0 and centre.steps[0].a[7] == 1
+        assert [s[0] for s in smart_m.describe()][-1] == "smartcrop"
+        assert smart_c.steps[smart_c.n_steps - 1].a[7] == 0 and smart_m.steps[smart_m.n_steps - 1].a[7] == 1
+        assert corner.steps[0].a[7] == 0                      # the earlier plan kept its convention
+        assert ia.lib.mipx_set_reduce_sampling(5) == -1
+    finally:
+        ia.set_reduce_sampling(prev)

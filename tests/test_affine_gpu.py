@@ -50,6 +50,9 @@ def test_enlarge_plans(gpu, oracle, rng):
 E2_CASES = [  # h, w, b, extend: k_enlarge2 (exactly 2 x 2) at every band count and edge
     (740, 550, 3, 1), (33, 1201, 4, 0), (97, 203, 1, 2), (61, 130, 2, 3), (64, 640, 3, 4),
     (5, 7, 3, 5), (1, 1, 4, 1), (2, 3, 3, 0), (70, 129, 4, 1), (129, 128, 3, 3),
+    # a 16-byte chunk ending exactly at the image's last byte with in_img % 4 != 0
+    # (w = 14 mod 16 pixels for B = 1, odd h): its tail dword straddled the descriptor's range and read 0
+    (1151, 1150, 3, 1), (31, 30, 1, 1), (31, 30, 1, 3),
 ]
 
 
