@@ -508,6 +508,20 @@ bool reduce2c_taps(float t[6]) {
     return true;
 }
 
+// The 2 x 2 reduce's 12 taps from 2x - 5 under the current sampling convention (corner:
+// phase 0, whose taps 11 and 12 are zero; centre: phase 64, whose tap 12 is zero), for
+// the chained kernel (k_rchain); false when tap 12 is not zero.
+bool reduce2_front_taps(int taps[12]) {
+    std::vector<int> tab;
+    reduce_table(2.0, tab);
+    const int n = reduce_points(2.0);
+    if (n != 13) return false;
+    const int *r = tab.data() + (reduce_centre() ? 64 : 0) * n;
+    if (r[12] != 0) return false;
+    for (int i = 0; i < 12; ++i) taps[i] = r[i];
+    return true;
+}
+
 // Fused path applies to shrink exactly 2 x 2 on 3- or 4-band images whose rows
 // are dword aligned: k_reduce2x2 at the corner convention, k_reduce2m at the centre one.
 bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
