@@ -43,6 +43,7 @@
 
 #include "device_common.h"
 #include "lds_ops.h"
+#include "r2front.h"
 
 namespace mipx {
 namespace {
@@ -96,23 +97,6 @@ __device__ __forceinline__ rc_v4i rc_frag16(const signed char *row, int o) {
                   static_cast<int>(__builtin_amdgcn_alignbyte(d.z, d.y, sh)),
                   static_cast<int>(__builtin_amdgcn_alignbyte(d.w, d.z, sh)),
                   static_cast<int>(__builtin_amdgcn_alignbyte(e, d.w, sh))};
-}
-
-// (a0..3 + 2048) >> 12 clamped to 0..255 and packed (accumulators seeded with the
-// rounding); v_ashr_pk_u8_i32 writes 16 bits, so the halves are joined by a perm.
-// rc_round4s: the same minus 128 as signed bytes (seeds carry - 128 << 12): the
-// intermediate in the pixel - 128 form the next pass multiplies
-__device__ __forceinline__ uint32_t rc_round4(int a0, int a1, int a2, int a3) {
-    uint32_t lo, hi;
-    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(a0), "v"(a1));
-    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(a2), "v"(a3));
-    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-}
-__device__ __forceinline__ uint32_t rc_round4s(int a0, int a1, int a2, int a3) {
-    uint32_t lo, hi;
-    asm("v_ashr_pk_i8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(a0), "v"(a1));
-    asm("v_ashr_pk_i8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(a2), "v"(a3));
-    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
 }
 
 // Horizontal operand rows of one output byte o = B x + c (x's first tap sp, phase pp)
@@ -491,15 +475,7 @@ struct RchArgs {
     const rc_u4 *fops;        // [64 lanes][vh, vl, wh, wl]: the front's MFMA operands (rch_operands)
     int vseed, hseed;         // front seeds: 128 sum(T) + 2048 - (128 << 12) (results in - 128 form)
     int fis;                  // front intermediate row stride (bytes)
-};
-
-template <int B>
-struct RCH {
-    static constexpr int GP = B == 3 ? 4 : 3;    // front output pixels per horizontal group (<= 64-byte window)
-    static constexpr int LOFF = B == 3 ? 0 : 4;  // LDS byte of the front intermediate's tile origin
-    // (B (2 org - 5) - 64-byte aligned base + LOFF) mod 8, the same for every strip: the
-    // 12-tap window of GP pixels then fits 64 bytes (RGBA: 0 + 4 x 15 + 4; RGB: 1 + 3 x 17 + 3)
-    static constexpr int SH = B == 3 ? 1 : 0;
+    const u8 *dbg_mid;        // debug (MIPX_CHAIN_DBG=1): ring rows loaded from this 2 x 2 output instead
 };
 
 template <int B, int NKS>
@@ -608,6 +584,16 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
     // ---- front step: 2 x 2-output rows P .. P + 14 into the ring ----
     auto front = [&](int P) {
         const int hh = a.h;  // rows of the 2 x 2 output
+        if (c.dbg_mid) {  // debug: the back end alone, on rows of a 2 x 2 output made by k_reduce2x2
+            const u8 *mid = c.dbg_mid + img * a.in_img;
+            for (int i = tid; i < kChFR * (16 * cpr); i += kRcNT) {
+                const int u = i / (16 * cpr), j = i - u * (16 * cpr);
+                const int R = clampi(P + u, 0, hh - 1), px = org * B + j;
+                ring[((P + u) & (kChRing - 1)) * a.rs + j] =
+                    static_cast<u8>((px >= 0 && px < a.w * B ? mid[static_cast<long long>(R) * a.w * B + px] : 0) ^ 0x80);
+            }
+            return;
+        }
         if (P < hh) {
             // vertical: wave-dealt 64-byte column tiles; 5 groups of 3 rows, 20 loads per lane in flight
             for (int tl_ = wave; tl_ < ntile; tl_ += WV) {
@@ -788,34 +774,6 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
     }
 }
 
-// The front's per-lane MFMA operands, [lane][vh, vl, wh, wl] x 16 bytes (taps = the 12
-// taps from 2x - 5 of the 2 x 2 reduce at the sampling convention's phase):
-//   vertical A, lane (m, kg): M = (row r = m / 4 < 3, byte c = m % 4), K = 16 kg + e =
-//     (block row 4 kg + e / 4, byte e % 4): tap (block row - 2 r) where the bytes match;
-//   horizontal A (k_reduce2m's W): output byte j = m < B GP takes tap i at window byte
-//     SH + B (2 (j / B) + i) + j % B.
-// Every tap T = 64 hi + lo (lo in [0, 63]).
-template <int B>
-std::vector<uint32_t> rch_operands(const int *tap) {
-    using G = RCH<B>;
-    std::vector<uint32_t> v(64 * 16, 0);
-    for (int lane = 0; lane < 64; ++lane) {
-        const int m = lane & 15, kg = lane >> 4;
-        for (int e = 0; e < 16; ++e) {
-            const int r = m >> 2, cm = m & 3;
-            const int i = 4 * kg + (e >> 2) - 2 * r;
-            const int tv = (r < 3 && (e & 3) == cm && i >= 0 && i < 12) ? tap[i] : 0;
-            const int k = 16 * kg + e - G::SH - m % B;
-            const int ih = k >= 0 && k % B == 0 ? k / B - 2 * (m / B) : -1;
-            const int th = (m < B * G::GP && ih >= 0 && ih < 12) ? tap[ih] : 0;
-            const int t4[4] = {tv >> 6, tv - 64 * (tv >> 6), th >> 6, th - 64 * (th >> 6)};
-            for (int o = 0; o < 4; ++o)
-                v[16 * lane + 4 * o + e / 4] |= (static_cast<uint32_t>(t4[o]) & 0xffu) << (8 * (e % 4));
-        }
-    }
-    return v;
-}
-
 }  // namespace
 
 // The column walker for both shrinks in (1, ~2.5] (<= 16 taps) on 3- / 4-band images
@@ -983,6 +941,12 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
     const long long blocks = cols * a.segs;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
+    {
+        const char *edb = tune_env("MIPX_CHAIN_DBG");
+        if (edb && *edb == '2')
+            fprintf(stderr, "k_rcol b%d %dx%d win %d,%d %dx%d: nks %d kmax %d cpr_max %d rs %d iw %d lds %zu ring %d segs %d steps %d wst %d\n",
+                    b, w, h, ox0, oy0, ow, oh, nks, kmax, cpr_max, a.rs, a.iw, lds, ring, a.segs, a.seg_steps, a.wst);
+    }
     hipLaunchKernelGGL(reinterpret_cast<void (*)(RcArgs)>(const_cast<void *>(fn)), dim3(static_cast<unsigned>(blocks)),
                        dim3(kRcNT), lds, st, a);
     return launch_check("k_rcol");
@@ -1058,7 +1022,9 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
         }
     }
     if (nks > 2) return MIPX_EUNSUPPORTED;
-    int rs = std::max(4 * cpr_max, (b * ni_max + 3) / 4);  // dwords: the vertical tiles and the front's pixels
+    // dwords, a multiple of 4 (the transposed reads need 8-byte rows; the vertical tiles are 16
+    // bytes): the column tiles and every pixel the front writes
+    int rs = 4 * std::max(cpr_max, (b * ni_max + 15) / 16);
     while (((rs & 63) >> 2) % 2 == 0) rs += 4;
     a.rs = 4 * rs;
     int iw = (std::max(16 * cpr_max, kbmax + 64 * nks) + 16 + 15) & ~15;
@@ -1098,6 +1064,14 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     c.fops = static_cast<const rc_u4 *>(device_blob(ops.data(), ops.size() * sizeof(uint32_t)));
     if (!c.fops) return MIPX_EDEVICE;
     c.vseed = c.hseed = 128 * sum + 2048 - (128 << 12);
+    const char *edb = tune_env("MIPX_CHAIN_DBG");
+    if (edb && *edb == '1') {  // debug: 2 x 2 output by k_reduce2x2 / k_reduce2m, back end reads it (leaks)
+        u8 *mid = nullptr;
+        if (hipMalloc(&mid, static_cast<size_t>(n) * a.in_img) != hipSuccess) return MIPX_ENOMEM;
+        const int e2 = reduce2_launch(in, mid, n, w, h, b, st);
+        if (e2) return e2;
+        c.dbg_mid = mid;
+    }
 
     const void *fn = nullptr;
     if (b == 3) fn = nks == 1 ? reinterpret_cast<const void *>(&k_rchain<3, 1>) : reinterpret_cast<const void *>(&k_rchain<3, 2>);
@@ -1116,6 +1090,10 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
     const long long blocks = cols * a.segs;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
+    if (edb && *edb == '2')
+        fprintf(stderr, "k_rchain b%d %dx%d -> %dx%d win %d,%d %dx%d: nks %d cpr_max %d ni_max %d rs %d iw %d fis %d lds %zu strips %d segs %d steps %d k0 %d\n",
+                b, w2, h2, out_size_reduce(w2, hs), out_size_reduce(h2, vs), ox0, oy0, ow, oh, nks, cpr_max, ni_max, a.rs,
+                a.iw, c.fis, lds, a.strips, a.segs, a.seg_steps, a.k0);
     hipLaunchKernelGGL(reinterpret_cast<void (*)(RcArgs, RchArgs)>(const_cast<void *>(fn)),
                        dim3(static_cast<unsigned>(blocks)), dim3(kRcNT), lds, st, a, c);
     return launch_check("k_rchain");

@@ -87,5 +87,22 @@ __device__ __forceinline__ void lgkm_wait_for(T &...v) {
     (rc_pin(v), ...);  // every later use reads the copy made after the wait
 }
 
+// (a0..3 + 2048) >> 12 clamped to 0..255 and packed (accumulators seeded with the
+// rounding); v_ashr_pk_u8_i32 writes 16 bits, so the halves are joined by a perm.
+// rc_round4s: the same minus 128 as signed bytes (seeds carry - 128 << 12): the
+// intermediate in the pixel - 128 form the next pass multiplies
+__device__ __forceinline__ uint32_t rc_round4(int a0, int a1, int a2, int a3) {
+    uint32_t lo, hi;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(a0), "v"(a1));
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(a2), "v"(a3));
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+__device__ __forceinline__ uint32_t rc_round4s(int a0, int a1, int a2, int a3) {
+    uint32_t lo, hi;
+    asm("v_ashr_pk_i8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(a0), "v"(a1));
+    asm("v_ashr_pk_i8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(a2), "v"(a3));
+    return __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+}
+
 }  // namespace dev
 }  // namespace mipx
