@@ -3,7 +3,7 @@
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 O="$R/gpurun_out/${OUT:-r05}"; mkdir -p "$O"
-timeout -k 10 300 python3 -u -m pytest tests/test_chain_gpu.py tests/test_sampling_gpu.py -x -q -p no:cacheprovider \
+timeout -k 10 400 python3 -u -m pytest tests/test_chain_gpu.py tests/test_sampling_gpu.py -q -p no:cacheprovider \
   --timeout 120 --timeout-method thread > "$O/pytest_chain.log" 2>&1; rc=$?
 tail -30 "$O/pytest_chain.log"
 [ $rc -eq 0 ] || exit $rc

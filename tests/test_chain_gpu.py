@@ -79,3 +79,47 @@ def test_chain_smooth_images_and_extremes(gpu, oracle, convention, monkeypatch):
     monkeypatch.setenv("MIPX_CHAIN", "2")
     got = gpu.execute(plan, px[None])
     assert np.array_equal(got[0], _oracle(oracle, p1, p2, px))
+
+
+# ---------------------------------------------------------------- k_reduce2d (MIPX_R2D=1)
+R2D_SHAPES = ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1000, 4), (200, 648, 3), (8, 8, 4), (9, 12, 3),
+              (25, 164, 3), (131, 1000, 4), (1081, 324, 3), (16, 3840, 3), (47, 226, 4), (2160, 3840, 3))
+
+
+@pytest.mark.parametrize("band", ["1", "8", "40"])
+def test_reduce2d_exact(gpu, oracle, convention, band, monkeypatch):
+    """The ring-less 2 x 2 kernel (k_reduce2d: vertical pass straight from HBM into the
+    matrix cores) at both conventions: strips ending at the image edges, images shorter
+    than a 15-row step, widths past one strip, full 4K."""
+    monkeypatch.setenv("MIPX_R2D", "1")
+    monkeypatch.setenv("MIPX_R2D_BAND", band)
+    r = np.random.default_rng(11)
+    for h, w, b in R2D_SHAPES:
+        if (w * b) % 4 or (h == 2160 and band != "8"):
+            continue
+        imgs = r.integers(0, 256, (2, h, w, b), dtype=np.uint8)
+        got = gpu.run_op("reduce", imgs, hshrink=2.0, vshrink=2.0)
+        for i in range(2):
+            want = oracle.reduce(imgs[i], 2.0, 2.0)
+            d = np.argwhere(got[i] != want)
+            assert len(d) == 0, f"{convention} band={band} {h}x{w}x{b} img{i}: {len(d)} differ, first {d[0]}"
+
+
+def test_reduce2d_windows(gpu, oracle, convention, monkeypatch):
+    """k_reduce2d computing only a 2 x 2 reduce's demanded region (reduce -> crop plans)."""
+    monkeypatch.setenv("MIPX_R2D", "1")
+    r = np.random.default_rng(12)
+    for (w, h, b), (left, top, cw, ch) in (((1200, 800, 3), (150, 100, 300, 200)), ((1200, 800, 4), (0, 280, 500, 120)),
+                                           ((640, 960, 3), (0, 0, 320, 100)), ((640, 960, 4), (219, 0, 100, 480))):
+        px = r.integers(0, 256, (1, h, w, b), dtype=np.uint8)
+        opts = dict(width=w // 2, height=h // 2, embed=1)
+        p1 = gpu.plan_make(gpu.make_opts(**opts), gpu.make_input(w, h, b, "png"))
+        p2 = gpu.plan_make(gpu.make_opts(left=left, top=top, area_width=cw, area_height=ch),
+                           gpu.make_input(p1.out_w, p1.out_h, b, "png"))
+        plan = gpu.plan_chain([p1, p2])
+        got = gpu.execute(plan, px)[0]
+        mid = oracle.reduce(px[0], 2.0, 2.0)
+        (op, a, _d, _o), = p2.describe()
+        assert op == "extract"
+        want = mid[a[1]:a[1] + a[3], a[0]:a[0] + a[2]]
+        assert np.array_equal(got, want), (w, h, b, left, top, cw, ch)
