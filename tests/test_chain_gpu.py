@@ -23,8 +23,8 @@ CASES = [
     (1000, 752, 4, dict(width=300, height=200, crop=1, gravity=3)),
     (1000, 752, 3, dict(width=300, height=200, crop=1, gravity=2)),
     (1000, 752, 3, dict(width=300, height=200, crop=1, gravity=4)),
-    (132, 90, 4, dict(width=40, height=28, embed=1)),        # 66x45 -> 40x28: one strip
-    (132, 90, 3, dict(width=40, height=28, embed=1)),
+    (132, 90, 4, dict(width=40, height=27, embed=1)),        # 66x45 -> 40x27: one strip
+    (132, 90, 3, dict(width=40, height=27, embed=1)),
     (200, 40, 4, dict(width=60, height=12, embed=1)),        # fewer 2 x 2 rows than a front step
     (2048, 2048, 4, dict(width=768, height=512, crop=1)),    # C3's own geometry
     (1540, 300, 3, dict(width=481, height=94, embed=1)),     # shrink 1.6: 16 taps
