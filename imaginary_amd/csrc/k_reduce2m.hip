@@ -338,6 +338,7 @@ struct R2dArgs {
     long long in_img, out_img;
     int seed;               // 128 sum(T) + 2048 - (128 << 12) (results in the - 128 form)
     const rc_u4 *ops;       // rch_operands: [64 lanes][vh, vl, wh, wl]
+    int soff;               // 1: interior steps put the row offset in the buffer SGPR offset (no per-load VALU)
 };
 
 template <int B>
@@ -380,8 +381,27 @@ __global__ void __launch_bounds__(256) k_reduce2d(R2dArgs a) {
         cofs[i] = (wave + 4 * i < NT && cb >= 0 && cb < pitch) ? cb : -1;
     }
     uint32_t v[TPW][5][4];
+    // per-lane part of an interior load's offset: rows 4 kg .. of the 16-row block at this
+    // lane's column (out-of-row columns: an offset past the image, read as 0)
+    int vo[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) vo[i] = cofs[i] >= 0 ? 4 * kg * pitch + cofs[i] : 0x7ffffff0;
     auto load = [&](int f) {
         const int P = FR * f;
+        const int r0 = 2 * P - 5;  // first input row of the step's blocks
+        if (a.soff && r0 >= 0 && r0 + 2 * (FR - 1) + 12 <= a.h - 1) {
+            // interior: row 6 g + j of the step in the SGPR offset (uniform), 4 kg rows and the
+            // column in the VGPR offset (range-checked; the whole address stays in the image)
+#pragma unroll
+            for (int i = 0; i < TPW; ++i)
+#pragma unroll
+                for (int g = 0; g < 5; ++g)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        v[i][g][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(
+                            src, vo[i], __builtin_amdgcn_readfirstlane((r0 + 6 * g + j) * pitch), 0));
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < TPW; ++i)
 #pragma unroll
@@ -610,6 +630,8 @@ int reduce2d_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
     a.ops = static_cast<const rc_u4 *>(device_blob(ops.data(), ops.size() * sizeof(uint32_t)));
     if (!a.ops) return MIPX_EDEVICE;
     a.seed = 128 * sum + 2048 - (128 << 12);
+    const char *eso = tune_env("MIPX_R2D_SOFF");
+    a.soff = !(eso && *eso == '0');
     const int spx = b == 3 ? R2D<3>::SPX : R2D<4>::SPX, fr = R2D<3>::FR;
     a.x_end = x1;
     a.y_end = y1;
