@@ -959,8 +959,11 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
 int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
                          int ow, int oh, const int *taps12, hipStream_t st) {
     if ((b != 3 && b != 4) || !(hs > 1.0) || !(vs > 1.0)) return MIPX_EUNSUPPORTED;
-    const char *ech = tune_env("MIPX_CHAIN");  // 0: run the two reduces (A/B)
-    if (ech && *ech == '0') return MIPX_EUNSUPPORTED;
+    // MIPX_CHAIN=1 / 2 (tests: 2 = the chained kernel or an error); unset or 0: the two
+    // reduces.  Off by default: on C3 the chain measures 3.90 ms per step against 2.43 ms
+    // for k_reduce2x2 + k_rcol (profiles/r05/c3_chain_ab.jsonl)
+    const char *ech = tune_env("MIPX_CHAIN");
+    if (!(ech && (*ech == '1' || *ech == '2'))) return MIPX_EUNSUPPORTED;
     const int w2 = out_size_reduce(w, 2.0), h2 = out_size_reduce(h, 2.0);
     const long long src_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
     if (src_img >= 0x7fffffffLL - 64 || out_img >= (1LL << 29)) return MIPX_EUNSUPPORTED;
