@@ -476,11 +476,17 @@ struct RchArgs {
     int vseed, hseed;         // front seeds: 128 sum(T) + 2048 - (128 << 12) (results in - 128 form)
     int fis;                  // front intermediate row stride (bytes)
     const u8 *dbg_mid;        // debug (MIPX_CHAIN_DBG=1): ring rows loaded from this 2 x 2 output instead
+    float c0, c1, c3, c5, bias;  // FRONT 1: k_reduce2x2's corner taps / 4096 and its 2^-13 bias
 };
 
-template <int B, int NKS>
+// FRONT 0: the vertical pass straight from HBM into the matrix cores (r05 first build,
+// 15-row steps); FRONT 1: the vertical pass on the VALU as k_reduce2x2 makes it (corner
+// convention: every input row loaded once into a register ring of its odd rows, the next
+// 12-row chunk prefetched while this one is consumed), the horizontal on the matrix cores
+template <int B, int NKS, int FRONT>
 __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
     using G = RCH<B>;
+    constexpr int FR = FRONT ? 12 : kChFR;  // 2 x 2-output rows per front step
     constexpr int WV = kRcNT / 64, XW = 16 * WV, GP = G::GP;
     constexpr int UPW = B;
     extern __shared__ __attribute__((aligned(16))) uint32_t rcs[];
@@ -488,7 +494,7 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
     const uint32_t inter_l = ring_l + static_cast<uint32_t>(kChRing * a.rs);     // [16][iw] + wave tiles
     constexpr int WSR = 16 * UPW + (UPW == 4 ? 16 : 0);
     const uint32_t wst_l = inter_l + static_cast<uint32_t>(kRcRows * a.iw);
-    const uint32_t fint_l = wst_l + static_cast<uint32_t>(WV * kRcRows * WSR);   // [kChFR][fis]
+    const uint32_t fint_l = wst_l + static_cast<uint32_t>(WV * kRcRows * WSR);   // [FR][fis]
     u8 *fint = reinterpret_cast<u8 *>(rcs) + (fint_l - ring_l);
     u8 *ring = reinterpret_cast<u8 *>(rcs);
 
@@ -586,7 +592,7 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
         const int hh = a.h;  // rows of the 2 x 2 output
         if (c.dbg_mid) {  // debug: the back end alone, on rows of a 2 x 2 output made by k_reduce2x2
             const u8 *mid = c.dbg_mid + img * a.in_img;
-            for (int i = tid; i < kChFR * (16 * cpr); i += kRcNT) {
+            for (int i = tid; i < FR * (16 * cpr); i += kRcNT) {
                 const int u = i / (16 * cpr), j = i - u * (16 * cpr);
                 const int R = clampi(P + u, 0, hh - 1), px = org * B + j;
                 ring[((P + u) & (kChRing - 1)) * a.rs + j] =
@@ -594,6 +600,7 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
             }
             return;
         }
+        if constexpr (FRONT == 0) {
         if (P < hh) {
             // vertical: wave-dealt 64-byte column tiles; 5 groups of 3 rows, 20 loads per lane in flight
             for (int tl_ = wave; tl_ < ntile; tl_ += WV) {
@@ -625,7 +632,7 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
             rc_barrier();
             if (fedge) {  // EXTEND_COPY of the input columns, per byte
                 const int nfill = nl + nr;
-                for (int i = tid; i < kChFR * nfill * B; i += kRcNT) {
+                for (int i = tid; i < FR * nfill * B; i += kRcNT) {
                     const int u = i / (nfill * B);
                     const int rem = i - u * nfill * B;
                     const int f = rem / B, ch = rem - f * B;
@@ -637,7 +644,7 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
             }
             // horizontal: groups of GP pixels, 4 groups' windows under one wait
             const uint32_t fb = fint_l + static_cast<uint32_t>(n * c.fis + (ish & ~7) + 16 * kg);
-            const bool wrow = n < kChFR && 4 * kg < B * GP;
+            const bool wrow = n < FR && 4 * kg < B * GP;
             const uint32_t rrow = ring_l + static_cast<uint32_t>(((P + n) & (kChRing - 1)) * a.rs + 4 * kg);
             for (int q0 = wave; q0 < ngr; q0 += 4 * WV) {
                 rc_u2x2 bq[4];
@@ -660,16 +667,125 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
         }
         // rows outside the 2 x 2 output: copies of its first / last row (COPY edge of the
         // second reduce's vertical pass)
-        if (P < 0 || P + kChFR > hh) {
+        if (P < 0 || P + FR > hh) {
             rc_barrier();
             const int rb = a.rs;  // bytes per ring row copied (>= 16 cpr)
-            for (int i = tid; i < kChFR * (rb >> 2); i += kRcNT) {
+            for (int i = tid; i < FR * (rb >> 2); i += kRcNT) {
                 const int u = i / (rb >> 2), d = i - u * (rb >> 2);
                 const int R = P + u;
                 if (R >= 0 && R < hh) continue;
                 const int S = R < 0 ? 0 : hh - 1;
                 reinterpret_cast<uint32_t *>(ring + (R & (kChRing - 1)) * a.rs)[d] =
                     reinterpret_cast<const uint32_t *>(ring + (S & (kChRing - 1)) * a.rs)[d];
+            }
+        }
+        }
+    };
+
+    // ---- FRONT 1: VALU vertical (k_reduce2x2's register ring), matrix-core horizontal ----
+    typedef float f4v_ __attribute__((ext_vector_type(4)));
+    auto cvt4 = [](uint32_t v) { return f4v_{ubyte_once<0>(v), ubyte_once<1>(v), ubyte_once<2>(v), ubyte_once<3>(v)}; };
+    auto tap7 = [&](float e, float m1, float p1, float m3, float p3, float m5, float p5) {
+        float acc = __builtin_fmaf(c.c0, e, c.bias);
+        acc = __builtin_fmaf(c.c1, m1 + p1, acc);
+        acc = __builtin_fmaf(c.c3, m3 + p3, acc);
+        return __builtin_fmaf(c.c5, m5 + p5, acc);
+    };
+    auto pack4 = [](float x, float y, float z, float w) {
+        uint32_t v = __builtin_amdgcn_cvt_pk_u8_f32(x, 0, 0u);
+        v = __builtin_amdgcn_cvt_pk_u8_f32(y, 1, v);
+        v = __builtin_amdgcn_cvt_pk_u8_f32(z, 2, v);
+        return __builtin_amdgcn_cvt_pk_u8_f32(w, 3, v);
+    };
+    const int ib = vb0 + 4 * tid;  // the lane's input dword (front intermediate dword tid)
+    const int nd = (ish - G::LOFF + B * (2 * ni + 10) + 3) >> 2;
+    const bool vlane = tid < nd;
+    const uint32_t voff = vlane && ib >= 0 && ib + 4 <= spitch ? static_cast<uint32_t>(ib) : 0x80000000u;
+    auto load_row = [&](int r) -> uint32_t {
+        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(
+            src, voff, __builtin_amdgcn_readfirstlane(clampi(r, 0, c.sh - 1) * spitch), 0));
+    };
+    f4v_ vring[6];
+    uint32_t podd[12], pevn[12];
+    auto front2_init = [&](int Q) {  // Q: a multiple of 12
+        if constexpr (FRONT == 1) {
+            vring[3] = cvt4(load_row(2 * (Q - 3) + 1));
+            vring[4] = cvt4(load_row(2 * (Q - 2) + 1));
+            vring[5] = cvt4(load_row(2 * (Q - 1) + 1));
+            vring[0] = cvt4(load_row(2 * Q + 1));
+            vring[1] = cvt4(load_row(2 * (Q + 1) + 1));
+            vring[2] = f4v_{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int u = 0; u < 12; ++u) {
+                podd[u] = load_row(2 * (Q + u + 2) + 1);
+                pevn[u] = load_row(2 * (Q + u));
+            }
+        }
+    };
+    auto front2 = [&](int Q) {
+        const int hh = a.h;
+        if constexpr (FRONT == 1) {
+            const uint32_t fw = fint_l + static_cast<uint32_t>(G::LOFF + 4 * tid);
+#pragma unroll
+            for (int u = 0; u < 12; ++u) {
+                vring[(u + 2) % 6] = cvt4(podd[u]);
+                const f4v_ e = cvt4(pevn[u]);
+                podd[u] = load_row(2 * (Q + 12 + u + 2) + 1);  // the next chunk's rows, in flight from here
+                pevn[u] = load_row(2 * (Q + 12 + u));
+                const f4v_ m5 = vring[(u + 3) % 6], m3 = vring[(u + 4) % 6], m1 = vring[(u + 5) % 6];
+                const f4v_ p1 = vring[u % 6], p3 = vring[(u + 1) % 6], p5 = vring[(u + 2) % 6];
+                const uint32_t d = pack4(tap7(e.x, m1.x, p1.x, m3.x, p3.x, m5.x, p5.x),
+                                         tap7(e.y, m1.y, p1.y, m3.y, p3.y, m5.y, p5.y),
+                                         tap7(e.z, m1.z, p1.z, m3.z, p3.z, m5.z, p5.z),
+                                         tap7(e.w, m1.w, p1.w, m3.w, p3.w, m5.w, p5.w));
+                if (vlane) lds_wr32(fw + static_cast<uint32_t>(u * c.fis), d ^ 0x80808080u);
+            }
+            rc_barrier();
+            if (fedge) {  // EXTEND_COPY of the input columns, per byte
+                const int nfill = nl + nr;
+                for (int i = tid; i < FR * nfill * B; i += kRcNT) {
+                    const int u = i / (nfill * B);
+                    const int rem = i - u * nfill * B;
+                    const int f = rem / B, ch = rem - f * B;
+                    const int d = f < nl ? f : fr + (f - nl);
+                    const int sp = f < nl ? nl : fr - 1;
+                    fint[u * c.fis + ish + B * d + ch] = fint[u * c.fis + ish + B * sp + ch];
+                }
+                rc_barrier();
+            }
+            const uint32_t fb = fint_l + static_cast<uint32_t>(n * c.fis + (ish & ~7) + 16 * kg);
+            const bool wrow = n < FR && 4 * kg < B * GP;
+            const uint32_t rrow = ring_l + static_cast<uint32_t>(((Q + n) & (kChRing - 1)) * a.rs + 4 * kg);
+            for (int q0 = wave; q0 < ngr; q0 += 4 * WV) {
+                rc_u2x2 bq[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) bq[i] = lds_rd64x2(fb + static_cast<uint32_t>(2 * B * GP * min(q0 + WV * i, ngr - 1)));
+                lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3]);
+                rc_v4i dh[4], dl[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const rc_v4i bv = __builtin_bit_cast(rc_v4i, rc_join(bq[i]));
+                    dh[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwh, bv, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
+                    dl[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwl, bv, rc_v4i{hsd, hsd, hsd, hsd}, 0, 0, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (wrow && q0 + WV * i < ngr)
+                        lds_wr32(rrow + static_cast<uint32_t>(B * GP * (q0 + WV * i)),
+                                 rc_round4s((dh[i][0] << 6) + dl[i][0], (dh[i][1] << 6) + dl[i][1], (dh[i][2] << 6) + dl[i][2],
+                                            (dh[i][3] << 6) + dl[i][3]));
+            }
+            if (Q < 0 || Q + FR > hh) {
+                rc_barrier();
+                const int rb = a.rs;
+                for (int i = tid; i < FR * (rb >> 2); i += kRcNT) {
+                    const int u = i / (rb >> 2), d = i - u * (rb >> 2);
+                    const int R = Q + u;
+                    if (R >= 0 && R < hh) continue;
+                    const int S = R < 0 ? 0 : hh - 1;
+                    reinterpret_cast<uint32_t *>(ring + (R & (kChRing - 1)) * a.rs)[d] =
+                        reinterpret_cast<const uint32_t *>(ring + (S & (kChRing - 1)) * a.rs)[d];
+                }
             }
         }
     };
@@ -680,6 +796,10 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
     const int we = 16 * (UPW * wave + wch);
     const uint32_t wst_w = wst_l + static_cast<uint32_t>(wave * kRcRows * WSR);
     int P = srow[2 * ka];  // next ring row to produce
+    if constexpr (FRONT == 1) {  // chunks on multiples of 12 (the register ring's slot map)
+        P = (P >= 0 ? P / 12 : -((-P + 11) / 12)) * 12;
+        if (!c.dbg_mid) front2_init(P);
+    }
     for (int k = ka; k < ka + steps; ++k) {
         const int o = k * (kRcRows * kRcolPlanRow);
         const rc_v4i bh = __builtin_bit_cast(rc_v4i, __builtin_amdgcn_raw_buffer_load_b128(prs, toff + o, 0, 0));
@@ -689,8 +809,9 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
         bool first = true;
         while (P < ek) {
             if (!first) rc_barrier();  // the front intermediate is free again
-            front(P);
-            P += kChFR;
+            if (FRONT == 1 && !c.dbg_mid) front2(P);
+            else front(P);
+            P += FR;
             first = false;
         }
         rc_barrier();  // ring rows of step k complete; the back intermediate free
@@ -993,11 +1114,16 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     a.ksteps = k1 - a.k0 + 1;
     auto gb = [&](int k) { return rc_start(kRcRows * k, vs, vpad, centre); };
     auto ge = [&](int k) { return rc_start(kRcRows * k + kRcRows - 1, vs, vpad, centre) + vtaps; };
+    // the front: FRONT 1 (VALU vertical, corner convention only) unless forced
+    // (MIPX_CHAIN_FRONT=0 / 1, A/B); FRONT 0 for the centre convention
+    const char *efr = tune_env("MIPX_CHAIN_FRONT");
+    const int front = (efr && *efr) ? (*efr == '1' && !centre ? 1 : 0) : (centre ? 0 : 1);
+    const int fr = front ? 12 : kChFR, falign = front ? 11 : 0;
     for (int k = a.k0; k <= k1; ++k) {
         if (ge(k) - gb(k) > 64) return MIPX_EUNSUPPORTED;  // the MFMA K
-        // the ring holds the step's rows plus one front step past its end; rows below the
-        // first 2 x 2 row are produced from row gb(k0) on, at most kChFR - 1 past ge(k)
-        if (ge(k) + kChFR - 1 - gb(k) > kChRing) return MIPX_EUNSUPPORTED;
+        // the ring holds the step's rows plus one front step past its end (and, FRONT 1, the
+        // rows a 12-aligned chunk makes above the step's first)
+        if (ge(k) + fr - 1 + falign - gb(k) > kChRing) return MIPX_EUNSUPPORTED;
     }
     int cpr_max = 0, nks = 0, kbmax = 0, fbytes_max = 0, ni_max = 0;
     const int gp = b == 3 ? RCH<3>::GP : RCH<4>::GP;
@@ -1013,6 +1139,7 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
         const int vst = 2 * org - 5, vb0 = (b * vst) & ~63, ish = b * vst - vb0 + loff;
         if ((ish & 7) != (b == 3 ? RCH<3>::SH : RCH<4>::SH)) return MIPX_EINVAL;  // the operand's window shift
         const int ntile = (ish - loff + b * (2 * ni + 10) + 63) >> 6;
+        if ((ish - loff + b * (2 * ni + 10) + 3) / 4 > kRcNT) return MIPX_EUNSUPPORTED;  // FRONT 1: a dword per lane
         fbytes_max = std::max({fbytes_max, 64 * ntile + loff, (ish & ~7) + 2 * b * gp * (ni / gp - 1) + 64});
         for (int u = 0; u < 64 * b / 16; ++u) {
             const int o0 = 16 * u, o1 = 16 * u + 15;
@@ -1076,9 +1203,21 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
         c.dbg_mid = mid;
     }
 
+    if (front) {
+        float cc[4];
+        if (!reduce2_taps(cc)) return MIPX_EUNSUPPORTED;
+        c.c0 = cc[0] / 4096.0f, c.c1 = cc[1] / 4096.0f, c.c3 = cc[2] / 4096.0f, c.c5 = cc[3] / 4096.0f;
+        c.bias = 1.0f / 8192.0f;
+    }
     const void *fn = nullptr;
-    if (b == 3) fn = nks == 1 ? reinterpret_cast<const void *>(&k_rchain<3, 1>) : reinterpret_cast<const void *>(&k_rchain<3, 2>);
-    else fn = nks == 1 ? reinterpret_cast<const void *>(&k_rchain<4, 1>) : reinterpret_cast<const void *>(&k_rchain<4, 2>);
+#define MIPX_RCH(B_, NKS_)                                                                        \
+    fn = front ? reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 1>) : reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 0>);
+    if (b == 3) {
+        if (nks == 1) { MIPX_RCH(3, 1) } else { MIPX_RCH(3, 2) }
+    } else {
+        if (nks == 1) { MIPX_RCH(4, 1) } else { MIPX_RCH(4, 2) }
+    }
+#undef MIPX_RCH
     // segments: one per strip unless the grid would not fill the device (a segment's first
     // front steps re-make the rows above its first step)
     a.strips = (ow + 63) / 64;

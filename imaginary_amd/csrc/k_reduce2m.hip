@@ -431,22 +431,17 @@ __global__ void __launch_bounds__(256) k_reduce2d(R2dArgs a) {
         for (int i = 0; i < TPW; ++i) {
             if (wave + 4 * i >= NT) break;
             const uint32_t fw = fint_l + static_cast<uint32_t>(kg * FIS + 64 * (wave + 4 * i) + 4 * n + G::LOFF);
-            // all ten products of the tile issued back to back, then the results (no MFMA ->
-            // VALU dependency stall per group: 39 % of wave cycles were issue stalls, PMC r05)
-            rc_v4i dh[5], dl[5];
 #pragma unroll
             for (int g = 0; g < 5; ++g) {
                 const rc_v4i bv = rc_v4i{static_cast<int>(v[i][g][0] ^ 0x80808080u), static_cast<int>(v[i][g][1] ^ 0x80808080u),
                                          static_cast<int>(v[i][g][2] ^ 0x80808080u), static_cast<int>(v[i][g][3] ^ 0x80808080u)};
-                dh[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fvh, bv, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
-                dl[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fvl, bv, rc_v4i{sd, sd, sd, sd}, 0, 0, 0);
-            }
-#pragma unroll
-            for (int g = 0; g < 5; ++g)
+                rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
+                dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(fvh, bv, dh, 0, 0, 0);
+                dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(fvl, bv, dl, 0, 0, 0);
                 if (kg < 3)
                     lds_wr32(fw + static_cast<uint32_t>(3 * g * FIS),
-                             rc_round4s((dh[g][0] << 6) + dl[g][0], (dh[g][1] << 6) + dl[g][1], (dh[g][2] << 6) + dl[g][2],
-                                        (dh[g][3] << 6) + dl[g][3]));
+                             rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
+            }
         }
         if (f + 1 < fb) load(f + 1);  // the next step's rows, in flight during the rest of this one
         rc_barrier();
@@ -474,20 +469,17 @@ __global__ void __launch_bounds__(256) k_reduce2d(R2dArgs a) {
             if constexpr (QPW == 7) lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3], bq[4], bq[5], bq[6]);
             else if constexpr (QPW == 6) lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3], bq[4], bq[5]);
             else static_assert(QPW == 6 || QPW == 7, "groups per wave");
-            rc_v4i dh[QPW], dl[QPW];
-#pragma unroll
-            for (int i = 0; i < QPW; ++i) {
-                const rc_v4i bv = __builtin_bit_cast(rc_v4i, rc_join(bq[i]));
-                dh[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwh, bv, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
-                dl[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwl, bv, rc_v4i{sd, sd, sd, sd}, 0, 0, 0);
-            }
 #pragma unroll
             for (int i = 0; i < QPW; ++i) {
                 const int q = wave + 4 * i;
+                const rc_v4i bv = __builtin_bit_cast(rc_v4i, rc_join(bq[i]));
+                rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
+                dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwh, bv, dh, 0, 0, 0);
+                dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwl, bv, dl, 0, 0, 0);
                 if (n < FR && 4 * kg < B * GP && q < G::NGR)
                     lds_wr32(ow_l + static_cast<uint32_t>(B * GP * q),
-                             rc_round4s((dh[i][0] << 6) + dl[i][0], (dh[i][1] << 6) + dl[i][1], (dh[i][2] << 6) + dl[i][2],
-                                        (dh[i][3] << 6) + dl[i][3]) ^ 0x80808080u);
+                             rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]) ^
+                                 0x80808080u);
             }
         }
         rc_barrier();

@@ -182,6 +182,8 @@ int reduce2m_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h,
 // k_reduce2m.hip: the 2 x 2 reduce with no input ring (k_rchain's front), either convention
 int reduce2d_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int x0, int y0, int x1,
                            int y1, const int *taps12, hipStream_t st);
+// the corner convention's 2 x 2 mask as k_reduce2x2 uses it: c0, c1, c3, c5 (k_reduce.hip)
+bool reduce2_taps(float c[4]);
 // the 2 x 2 reduce's 12 taps from 2x - 5 at the current convention (k_reduce.hip)
 bool reduce2_front_taps(int taps[12]);
 // k_rcol.hip: reduce 2 x 2 then reduce (hs, vs) over the second's output window, one launch
