@@ -761,25 +761,23 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
 #pragma unroll
                 for (int i = 0; i < 4; ++i) bq[i] = lds_rd64x2(fb + static_cast<uint32_t>(2 * B * GP * min(q0 + WV * i, ngr - 1)));
                 lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3]);
-                rc_v4i dh[4], dl[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const rc_v4i bv = __builtin_bit_cast(rc_v4i, rc_join(bq[i]));
-                    dh[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwh, bv, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
-                    dl[i] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwl, bv, rc_v4i{hsd, hsd, hsd, hsd}, 0, 0, 0);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
+                    const rc_v4i dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwh, bv, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
+                    const rc_v4i dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwl, bv, rc_v4i{hsd, hsd, hsd, hsd}, 0, 0, 0);
                     if (wrow && q0 + WV * i < ngr)
                         lds_wr32(rrow + static_cast<uint32_t>(B * GP * (q0 + WV * i)),
-                                 rc_round4s((dh[i][0] << 6) + dl[i][0], (dh[i][1] << 6) + dl[i][1], (dh[i][2] << 6) + dl[i][2],
-                                            (dh[i][3] << 6) + dl[i][3]));
+                                 rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
+                }
             }
-            if (Q < 0 || Q + FR > hh) {
+            // rows outside the 2 x 2 output: those past its last row in this chunk, and with
+            // the first chunk (chunks start at row 0, never above it) the up to 11 rows above row 0
+            if (Q == 0 || Q + FR > hh) {
                 rc_barrier();
-                const int rb = a.rs;
-                for (int i = tid; i < FR * (rb >> 2); i += kRcNT) {
-                    const int u = i / (rb >> 2), d = i - u * (rb >> 2);
+                const int rb = a.rs, u0 = Q == 0 ? -11 : 0;
+                for (int i = tid; i < (FR - u0) * (rb >> 2); i += kRcNT) {
+                    const int u = u0 + i / (rb >> 2), d = i - (u - u0) * (rb >> 2);
                     const int R = Q + u;
                     if (R >= 0 && R < hh) continue;
                     const int S = R < 0 ? 0 : hh - 1;
@@ -797,7 +795,7 @@ __global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
     const uint32_t wst_w = wst_l + static_cast<uint32_t>(wave * kRcRows * WSR);
     int P = srow[2 * ka];  // next ring row to produce
     if constexpr (FRONT == 1) {  // chunks on multiples of 12 (the register ring's slot map)
-        P = (P >= 0 ? P / 12 : -((-P + 11) / 12)) * 12;
+        P = P >= 0 ? P / 12 * 12 : 0;  // rows above row 0 are copies of it, filled with chunk 0
         if (!c.dbg_mid) front2_init(P);
     }
     for (int k = ka; k < ka + steps; ++k) {
