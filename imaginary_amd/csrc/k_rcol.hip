@@ -1115,7 +1115,19 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     // the front: FRONT 1 (VALU vertical, corner convention only) unless forced
     // (MIPX_CHAIN_FRONT=0 / 1, A/B); FRONT 0 for the centre convention
     const char *efr = tune_env("MIPX_CHAIN_FRONT");
-    const int front = (efr && *efr) ? (*efr == '1' && !centre ? 1 : 0) : (centre ? 0 : 1);
+    int front = (efr && *efr) ? (*efr == '1' && !centre ? 1 : 0) : (centre ? 0 : 1);
+    // FRONT 1 holds a strip's input row in one dword per lane: wider strips (shrinks past
+    // ~1.55 on RGBA) take FRONT 0
+    for (int x0 = 0; front && x0 < ow; x0 += 64) {
+        const int xl = std::min(x0 + 63, ow - 1);
+        const int lo = rc_start(ox0 + x0, hs, a.hpad, centre), hi = rc_start(ox0 + xl, hs, a.hpad, centre) + htaps - 1;
+        const int org = lo & (lo < 0 && b == 3 ? ~15 : ~3);
+        const int cpr = (b * (hi - org + 1) + 15) >> 4;
+        const int gpf = b == 3 ? RCH<3>::GP : RCH<4>::GP;
+        const int ni = (((16 * cpr + b - 1) / b + gpf - 1) / gpf) * gpf;
+        const int vst = 2 * org - 5, ish = b * vst - ((b * vst) & ~63);  // (LOFF cancels)
+        if ((ish + b * (2 * ni + 10) + 3) / 4 > kRcNT) front = 0;
+    }
     const int fr = front ? 12 : kChFR, falign = front ? 11 : 0;
     for (int k = a.k0; k <= k1; ++k) {
         if (ge(k) - gb(k) > 64) return MIPX_EUNSUPPORTED;  // the MFMA K
@@ -1137,7 +1149,6 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
         const int vst = 2 * org - 5, vb0 = (b * vst) & ~63, ish = b * vst - vb0 + loff;
         if ((ish & 7) != (b == 3 ? RCH<3>::SH : RCH<4>::SH)) return MIPX_EINVAL;  // the operand's window shift
         const int ntile = (ish - loff + b * (2 * ni + 10) + 63) >> 6;
-        if ((ish - loff + b * (2 * ni + 10) + 3) / 4 > kRcNT) return MIPX_EUNSUPPORTED;  // FRONT 1: a dword per lane
         fbytes_max = std::max({fbytes_max, 64 * ntile + loff, (ish & ~7) + 2 * b * gp * (ni / gp - 1) + 64});
         for (int u = 0; u < 64 * b / 16; ++u) {
             const int o0 = 16 * u, o1 = 16 * u + 15;
