@@ -77,6 +77,7 @@ struct RcArgs {
     const signed char *tabhf; // device_reduce_i8s_fold(hs, B): the COPY edge folded in
     int centre;               // centre sampling convention (mipx_set_reduce_sampling)
     int wst;                  // each wave's 16 rows x 16 UPW bytes go out as 16-byte row pieces
+    int prime_ov;             // the prime's loads overlapped with the pipeline's first (MIPX_RCOL_PRIME, A/B)
 };
 
 // libvips reduce position (reducev.cpp / reduceh.cpp): X = reduce_x (o * shrink, or
@@ -236,37 +237,6 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         lcol[j] = ring_l + static_cast<uint32_t>(16 * col);
     }
     const int lkf = (kRcNT * KMAX) / cpr;  // rows one load batch covers completely
-
-    // ---- prime: group ka's rows straight into the ring (exact rows only) ----
-    const int bka = srow[2 * ka], eka = srow[2 * ka + 1];
-    for (int r = bka; r < eka; r += lkf) {
-        rc_u4 tv[KMAX];
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  src, clampi(r + rr[j], 0, a.h - 1) * pitch + cof[j], 0, 0));
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            if (rr[j] < lkf && r + rr[j] < eka)
-                lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j], tv[j] ^ 0x80808080u);
-    }
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) {
-        if (both[i]) continue;
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            const int sh = qsh[i][ks];
-            const uint4 d = qh[i][ks], e = ql[i][ks];
-            th[i][ks] = rc_v4i{static_cast<int>(__builtin_amdgcn_alignbyte(d.y, d.x, sh)),
-                               static_cast<int>(__builtin_amdgcn_alignbyte(d.z, d.y, sh)),
-                               static_cast<int>(__builtin_amdgcn_alignbyte(d.w, d.z, sh)),
-                               static_cast<int>(__builtin_amdgcn_alignbyte(eh[i][ks], d.w, sh))};
-            tl[i][ks] = rc_v4i{static_cast<int>(__builtin_amdgcn_alignbyte(e.y, e.x, sh)),
-                               static_cast<int>(__builtin_amdgcn_alignbyte(e.z, e.y, sh)),
-                               static_cast<int>(__builtin_amdgcn_alignbyte(e.w, e.z, sh)),
-                               static_cast<int>(__builtin_amdgcn_alignbyte(el[i][ks], e.w, sh))};
-        }
-    }
 
     // ---- the step pipeline: register set P = (step - ka) & 1 holds step k + 2's ring
     // chunks and vertical operands from the middle of step k to the top of step k + 2.
@@ -429,11 +399,66 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     const uint32_t zero[UPW] = {};
-    issue_taps(I0{}, ka);
-    store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
-    issue_ring(I1{}, eka);
-    issue_taps(I1{}, ka + 1);
-    store(ka, false, zero);
+    // ---- prime: group ka's rows straight into the ring (exact rows only) ----
+    const int bka = srow[2 * ka], eka = srow[2 * ka + 1];
+    auto prime_write = [&](int r, const rc_u4 *tv) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if (rr[j] < lkf && r + rr[j] < eka)
+                lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j], tv[j] ^ 0x80808080u);
+    };
+    auto prime_load = [&](int r, rc_u4 *tv) {
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  src, clampi(r + rr[j], 0, a.h - 1) * pitch + cof[j], 0, 0));
+    };
+    bool ov = false;
+    if constexpr (KMAX == 3) ov = a.prime_ov != 0;  // the small-image builds; KMAX 6 keeps its register budget
+    if (ov) {
+        // r05: the first prime batch's loads and the pipeline's first loads in flight together
+        // (the separate prime loop paid a whole memory round trip before the pipeline started)
+        rc_u4 tv[KMAX];
+        prime_load(bka, tv);
+        issue_taps(I0{}, ka);
+        store(ka, false, zero);
+        issue_ring(I1{}, eka);
+        issue_taps(I1{}, ka + 1);
+        store(ka, false, zero);
+        prime_write(bka, tv);
+        for (int r = bka + lkf; r < eka; r += lkf) {
+            prime_load(r, tv);
+            prime_write(r, tv);
+        }
+    } else {
+        for (int r = bka; r < eka; r += lkf) {
+            rc_u4 tv[KMAX];
+            prime_load(r, tv);
+            prime_write(r, tv);
+        }
+        issue_taps(I0{}, ka);
+        store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
+        issue_ring(I1{}, eka);
+        issue_taps(I1{}, ka + 1);
+        store(ka, false, zero);
+    }
+#pragma unroll
+    for (int i = 0; i < UPW; ++i) {
+        if (both[i]) continue;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int sh = qsh[i][ks];
+            const uint4 d = qh[i][ks], e = ql[i][ks];
+            th[i][ks] = rc_v4i{static_cast<int>(__builtin_amdgcn_alignbyte(d.y, d.x, sh)),
+                               static_cast<int>(__builtin_amdgcn_alignbyte(d.z, d.y, sh)),
+                               static_cast<int>(__builtin_amdgcn_alignbyte(d.w, d.z, sh)),
+                               static_cast<int>(__builtin_amdgcn_alignbyte(eh[i][ks], d.w, sh))};
+            tl[i][ks] = rc_v4i{static_cast<int>(__builtin_amdgcn_alignbyte(e.y, e.x, sh)),
+                               static_cast<int>(__builtin_amdgcn_alignbyte(e.z, e.y, sh)),
+                               static_cast<int>(__builtin_amdgcn_alignbyte(e.w, e.z, sh)),
+                               static_cast<int>(__builtin_amdgcn_alignbyte(el[i][ks], e.w, sh))};
+        }
+    }
     for (int s = 0; s < steps; s += 2) {
         body(I0{}, ka + s, true, s == 0);
         body(I1{}, ka + s + 1, s + 1 < steps, false);
@@ -483,8 +508,10 @@ struct RchArgs {
 // 15-row steps); FRONT 1: the vertical pass on the VALU as k_reduce2x2 makes it (corner
 // convention: every input row loaded once into a register ring of its odd rows, the next
 // 12-row chunk prefetched while this one is consumed), the horizontal on the matrix cores
-template <int B, int NKS, int FRONT>
-__global__ void __launch_bounds__(kRcNT) k_rchain(RcArgs a, RchArgs c) {
+// W3: a build held to 3 waves per SIMD (168 VGPRs, a few spilled) instead of the
+// compiler's 2 (FRONT 1 only; MIPX_CHAIN_W3, A/B)
+template <int B, int NKS, int FRONT, int W3>
+__global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(W3 ? 3 : 1, 8))) k_rchain(RcArgs a, RchArgs c) {
     using G = RCH<B>;
     constexpr int FR = FRONT ? 12 : kChFR;  // 2 x 2-output rows per front step
     constexpr int WV = kRcNT / 64, XW = 16 * WV, GP = G::GP;
@@ -1007,6 +1034,8 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // -31 %, profiles/r03/rcol_wst_ab.jsonl); MIPX_RCOL_WST=0 keeps the 4-byte stores (A/B)
     const char *ews = tune_env("MIPX_RCOL_WST");
     a.wst = !(ews && *ews == '0') ? (!out_al ? 3 : (ow * b) % 16 == 0 ? 1 : 2) : 0;
+    const char *epr = tune_env("MIPX_RCOL_PRIME");
+    a.prime_ov = !(epr && *epr == '0');
     const void *fn = nullptr;
 #define MIPX_RC_K(B_, NKS_, KM_) fn = reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, 1>);
 #define MIPX_RC_KM(B_, NKS_) \
@@ -1219,8 +1248,12 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
         c.bias = 1.0f / 8192.0f;
     }
     const void *fn = nullptr;
-#define MIPX_RCH(B_, NKS_)                                                                        \
-    fn = front ? reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 1>) : reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 0>);
+    const char *ew3 = tune_env("MIPX_CHAIN_W3");
+    const bool w3 = !(ew3 && *ew3 == '0');
+#define MIPX_RCH(B_, NKS_)                                                                                     \
+    fn = front ? (w3 ? reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 1, 1>)                              \
+                     : reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 1, 0>))                             \
+               : reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 0, 0>);
     if (b == 3) {
         if (nks == 1) { MIPX_RCH(3, 1) } else { MIPX_RCH(3, 2) }
     } else {
