@@ -500,7 +500,6 @@ struct RchArgs {
     const rc_u4 *fops;        // [64 lanes][vh, vl, wh, wl]: the front's MFMA operands (rch_operands)
     int vseed, hseed;         // front seeds: 128 sum(T) + 2048 - (128 << 12) (results in - 128 form)
     int fis;                  // front intermediate row stride (bytes)
-    const u8 *dbg_mid;        // debug (MIPX_CHAIN_DBG=1): ring rows loaded from this 2 x 2 output instead
     float c0, c1, c3, c5, bias;  // FRONT 1: k_reduce2x2's corner taps / 4096 and its 2^-13 bias
 };
 
@@ -617,16 +616,6 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(W3 ?
     // ---- front step: 2 x 2-output rows P .. P + 14 into the ring ----
     auto front = [&](int P) {
         const int hh = a.h;  // rows of the 2 x 2 output
-        if (c.dbg_mid) {  // debug: the back end alone, on rows of a 2 x 2 output made by k_reduce2x2
-            const u8 *mid = c.dbg_mid + img * a.in_img;
-            for (int i = tid; i < FR * (16 * cpr); i += kRcNT) {
-                const int u = i / (16 * cpr), j = i - u * (16 * cpr);
-                const int R = clampi(P + u, 0, hh - 1), px = org * B + j;
-                ring[((P + u) & (kChRing - 1)) * a.rs + j] =
-                    static_cast<u8>((px >= 0 && px < a.w * B ? mid[static_cast<long long>(R) * a.w * B + px] : 0) ^ 0x80);
-            }
-            return;
-        }
         if constexpr (FRONT == 0) {
         if (P < hh) {
             // vertical: wave-dealt 64-byte column tiles; 5 groups of 3 rows, 20 loads per lane in flight
@@ -823,7 +812,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(W3 ?
     int P = srow[2 * ka];  // next ring row to produce
     if constexpr (FRONT == 1) {  // chunks on multiples of 12 (the register ring's slot map)
         P = P >= 0 ? P / 12 * 12 : 0;  // rows above row 0 are copies of it, filled with chunk 0
-        if (!c.dbg_mid) front2_init(P);
+        front2_init(P);
     }
     for (int k = ka; k < ka + steps; ++k) {
         const int o = k * (kRcRows * kRcolPlanRow);
@@ -834,7 +823,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(W3 ?
         bool first = true;
         while (P < ek) {
             if (!first) rc_barrier();  // the front intermediate is free again
-            if (FRONT == 1 && !c.dbg_mid) front2(P);
+            if (FRONT == 1) front2(P);
             else front(P);
             P += FR;
             first = false;
@@ -1089,12 +1078,6 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
     const long long blocks = cols * a.segs;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
-    {
-        const char *edb = tune_env("MIPX_CHAIN_DBG");
-        if (edb && *edb == '2')
-            fprintf(stderr, "k_rcol b%d %dx%d win %d,%d %dx%d: nks %d kmax %d cpr_max %d rs %d iw %d lds %zu ring %d segs %d steps %d wst %d\n",
-                    b, w, h, ox0, oy0, ow, oh, nks, kmax, cpr_max, a.rs, a.iw, lds, ring, a.segs, a.seg_steps, a.wst);
-    }
     hipLaunchKernelGGL(reinterpret_cast<void (*)(RcArgs)>(const_cast<void *>(fn)), dim3(static_cast<unsigned>(blocks)),
                        dim3(kRcNT), lds, st, a);
     return launch_check("k_rcol");
@@ -1232,14 +1215,6 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     c.fops = static_cast<const rc_u4 *>(device_blob(ops.data(), ops.size() * sizeof(uint32_t)));
     if (!c.fops) return MIPX_EDEVICE;
     c.vseed = c.hseed = 128 * sum + 2048 - (128 << 12);
-    const char *edb = tune_env("MIPX_CHAIN_DBG");
-    if (edb && *edb == '1') {  // debug: 2 x 2 output by k_reduce2x2 / k_reduce2m, back end reads it (leaks)
-        u8 *mid = nullptr;
-        if (hipMalloc(&mid, static_cast<size_t>(n) * a.in_img) != hipSuccess) return MIPX_ENOMEM;
-        const int e2 = reduce2_launch(in, mid, n, w, h, b, st);
-        if (e2) return e2;
-        c.dbg_mid = mid;
-    }
 
     if (front) {
         float cc[4];
@@ -1274,10 +1249,6 @@ int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, doub
     a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
     const long long blocks = cols * a.segs;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
-    if (edb && *edb == '2')
-        fprintf(stderr, "k_rchain b%d %dx%d -> %dx%d win %d,%d %dx%d: nks %d cpr_max %d ni_max %d rs %d iw %d fis %d lds %zu strips %d segs %d steps %d k0 %d\n",
-                b, w2, h2, out_size_reduce(w2, hs), out_size_reduce(h2, vs), ox0, oy0, ow, oh, nks, cpr_max, ni_max, a.rs,
-                a.iw, c.fis, lds, a.strips, a.segs, a.seg_steps, a.k0);
     hipLaunchKernelGGL(reinterpret_cast<void (*)(RcArgs, RchArgs)>(const_cast<void *>(fn)),
                        dim3(static_cast<unsigned>(blocks)), dim3(kRcNT), lds, st, a, c);
     return launch_check("k_rchain");
