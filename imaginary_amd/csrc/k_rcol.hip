@@ -77,7 +77,6 @@ struct RcArgs {
     const signed char *tabhf; // device_reduce_i8s_fold(hs, B): the COPY edge folded in
     int centre;               // centre sampling convention (mipx_set_reduce_sampling)
     int wst;                  // each wave's 16 rows x 16 UPW bytes go out as 16-byte row pieces
-    int prime_ov;             // the prime's loads overlapped with the pipeline's first (MIPX_RCOL_PRIME, A/B)
 };
 
 // libvips reduce position (reducev.cpp / reduceh.cpp): X = reduce_x (o * shrink, or
@@ -399,49 +398,27 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     const uint32_t zero[UPW] = {};
-    // ---- prime: group ka's rows straight into the ring (exact rows only) ----
+    // ---- prime: group ka's rows straight into the ring (exact rows only), then the
+    // pipeline's first loads (r05: issuing those before the prime's ring writes measured
+    // within +-1 %, and the extra live registers spilled in the 4-wave build,
+    // profiles/r05/prime_ab.jsonl) ----
     const int bka = srow[2 * ka], eka = srow[2 * ka + 1];
-    auto prime_write = [&](int r, const rc_u4 *tv) {
-#pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            if (rr[j] < lkf && r + rr[j] < eka)
-                lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j], tv[j] ^ 0x80808080u);
-    };
-    auto prime_load = [&](int r, rc_u4 *tv) {
+    for (int r = bka; r < eka; r += lkf) {
+        rc_u4 tv[KMAX];
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
                                                   src, clampi(r + rr[j], 0, a.h - 1) * pitch + cof[j], 0, 0));
-    };
-    bool ov = false;
-    if constexpr (KMAX == 3) ov = a.prime_ov != 0;  // the small-image builds; KMAX 6 keeps its register budget
-    if (ov) {
-        // r05: the first prime batch's loads and the pipeline's first loads in flight together
-        // (the separate prime loop paid a whole memory round trip before the pipeline started)
-        rc_u4 tv[KMAX];
-        prime_load(bka, tv);
-        issue_taps(I0{}, ka);
-        store(ka, false, zero);
-        issue_ring(I1{}, eka);
-        issue_taps(I1{}, ka + 1);
-        store(ka, false, zero);
-        prime_write(bka, tv);
-        for (int r = bka + lkf; r < eka; r += lkf) {
-            prime_load(r, tv);
-            prime_write(r, tv);
-        }
-    } else {
-        for (int r = bka; r < eka; r += lkf) {
-            rc_u4 tv[KMAX];
-            prime_load(r, tv);
-            prime_write(r, tv);
-        }
-        issue_taps(I0{}, ka);
-        store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
-        issue_ring(I1{}, eka);
-        issue_taps(I1{}, ka + 1);
-        store(ka, false, zero);
+#pragma unroll
+        for (int j = 0; j < KMAX; ++j)
+            if (rr[j] < lkf && r + rr[j] < eka)
+                lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j], tv[j] ^ 0x80808080u);
     }
+    issue_taps(I0{}, ka);
+    store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
+    issue_ring(I1{}, eka);
+    issue_taps(I1{}, ka + 1);
+    store(ka, false, zero);
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
         if (both[i]) continue;
@@ -1023,8 +1000,6 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // -31 %, profiles/r03/rcol_wst_ab.jsonl); MIPX_RCOL_WST=0 keeps the 4-byte stores (A/B)
     const char *ews = tune_env("MIPX_RCOL_WST");
     a.wst = !(ews && *ews == '0') ? (!out_al ? 3 : (ow * b) % 16 == 0 ? 1 : 2) : 0;
-    const char *epr = tune_env("MIPX_RCOL_PRIME");
-    a.prime_ov = !(epr && *epr == '0');
     const void *fn = nullptr;
 #define MIPX_RC_K(B_, NKS_, KM_) fn = reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, 1>);
 #define MIPX_RC_KM(B_, NKS_) \
