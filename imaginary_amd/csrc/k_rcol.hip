@@ -1040,11 +1040,15 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // the whole launch then fits one round of resident blocks in fewer steps per block
     // (364x273 RGB x 128 -> 256^2: -18 %); with more rounds the spills cost 3-5 %
     // (480x270, 500x375, 1080p; profiles/r04/small/rcol_w4_ab.jsonl)
-    if (b == 3 && nks == 1 && kmax == 3) {
-        const void *f4 = reinterpret_cast<const void *>(&k_rcol<3, 1, 3, 4>);
+    // MIPX_RCOL_W4=1 (A/B): the 4-wave build whatever the plan says (RGBA too)
+    const char *ew4 = tune_env("MIPX_RCOL_W4");
+    const bool force4 = ew4 && *ew4 == '1';
+    if (nks == 1 && kmax == 3 && (b == 3 || force4)) {
+        const void *f4 = b == 3 ? reinterpret_cast<const void *>(&k_rcol<3, 1, 3, 4>)
+                                : reinterpret_cast<const void *>(&k_rcol<4, 1, 3, 4>);
         int segs4 = 1;
         const auto p4 = plan(f4, &segs4);
-        if (p4.second == 1 && p4.first < best - 1e-9) {
+        if (force4 || (p4.second == 1 && p4.first < best - 1e-9)) {
             fn = f4;
             best_segs = segs4;
         }
