@@ -77,6 +77,7 @@ struct RcArgs {
     const signed char *tabhf; // device_reduce_i8s_fold(hs, B): the COPY edge folded in
     int centre;               // centre sampling convention (mipx_set_reduce_sampling)
     int wst;                  // each wave's 16 rows x 16 UPW bytes go out as 16-byte row pieces
+    int swz;                  // horizontal reads: odd K blocks read their second 8 bytes first
 };
 
 // libvips reduce position (reducev.cpp / reduceh.cpp): X = reduce_x (o * shrink, or
@@ -344,17 +345,23 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
             }
     };
     // horizontal pass: units wave + WV i, operands from registers, every unit's LDS
-    // reads in flight together
+    // reads in flight together.  r05: a lane of an odd K block reads bytes 8..15 of its
+    // 16 first (hsw = 8) and the operands' halves are swapped to match: with kg = 0 / 1
+    // lanes in one 32-lane half on banks 0-1 / 2-3 (mod 4) each read is conflict-free
+    // (both halves of one K block at once were 2-way); MIPX_RCOL_SWZ=0 keeps the old order
+    const int hsw = a.swz && (kg & 1) ? 8 : 0, hsd = 8 - 2 * hsw;
     auto horizontal = [&](uint32_t *res) {
         rc_u2x2 q[UPW][NKS];
 #pragma unroll
         for (int i = 0; i < UPW; ++i) {
-            const uint32_t ir = inter_l + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg);
+            const uint32_t ir = inter_l + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg + hsw);
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
                 // two ds_read_b64 (2 LDS cycles each) rather than one ds_read2_b64 (16): -0.3 to -2 %
-                // (profiles/r04/small/rcol_rd64_ab.jsonl)
-                q[i][ks] = lds_rd64x2(ir + 64 * ks);
+                // (profiles/r04/small/rcol_rd64_ab.jsonl); lanes of odd K blocks read their
+                // second half first (hsw), so each read's 32-lane half covers all 64 banks
+                q[i][ks].lo = lds_rd64(ir + 64 * ks);
+                q[i][ks].hi = lds_rd64(ir + 64 * ks + hsd);
             }
         }
 #pragma unroll
@@ -435,6 +442,15 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
                                static_cast<int>(__builtin_amdgcn_alignbyte(e.w, e.z, sh)),
                                static_cast<int>(__builtin_amdgcn_alignbyte(el[i][ks], e.w, sh))};
         }
+    }
+    if (hsw) {  // the K halves of odd blocks, in the order their data is read
+#pragma unroll
+        for (int i = 0; i < UPW; ++i)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                th[i][ks] = rc_v4i{th[i][ks][2], th[i][ks][3], th[i][ks][0], th[i][ks][1]};
+                tl[i][ks] = rc_v4i{tl[i][ks][2], tl[i][ks][3], tl[i][ks][0], tl[i][ks][1]};
+            }
     }
     for (int s = 0; s < steps; s += 2) {
         body(I0{}, ka + s, true, s == 0);
@@ -1000,6 +1016,8 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // -31 %, profiles/r03/rcol_wst_ab.jsonl); MIPX_RCOL_WST=0 keeps the 4-byte stores (A/B)
     const char *ews = tune_env("MIPX_RCOL_WST");
     a.wst = !(ews && *ews == '0') ? (!out_al ? 3 : (ow * b) % 16 == 0 ? 1 : 2) : 0;
+    const char *esz = tune_env("MIPX_RCOL_SWZ");
+    a.swz = !(esz && *esz == '0');
     const void *fn = nullptr;
 #define MIPX_RC_K(B_, NKS_, KM_) fn = reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, 1>);
 #define MIPX_RC_KM(B_, NKS_) \

@@ -52,6 +52,11 @@ __device__ __forceinline__ rc_u2x2 lds_rd64x2(uint32_t a) {
     asm volatile("ds_read_b64 %0, %1 offset:8" : "=v"(v.hi) : "v"(a));
     return v;
 }
+__device__ __forceinline__ rc_u2 lds_rd64(uint32_t a) {
+    rc_u2 v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
 __device__ __forceinline__ rc_u4 rc_join(const rc_u2x2 &v) { return rc_u4{v.lo.x, v.lo.y, v.hi.x, v.hi.y}; }
 __device__ __forceinline__ rc_u4 lds_rd128(uint32_t a) {
     rc_u4 v;

@@ -41,6 +41,8 @@ flip --w 3840 --h 2160 --b 3 --n 32 --s 1
 affine --w 1920 --h 1080 --b 3 --n 16 --s 2
 affine --w 550 --h 740 --b 3 --n 64 --s 2
 affine --w 1024 --h 768 --b 4 --n 16 --s 1.5
+affine --w 1280 --h 720 --b 3 --n 16 --s 3
+affine --w 960 --h 540 --b 3 --n 16 --s 4
 zoom --w 1920 --h 1080 --b 3 --n 16 --s 2
 LIST
 python3 - "$F" <<'PY'
