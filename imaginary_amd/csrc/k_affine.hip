@@ -14,6 +14,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
 
 #include "device_common.h"
 #include "lds_ops.h"
@@ -507,6 +511,288 @@ __global__ void __launch_bounds__(256) k_enlarge2(Enl2Args a) {
     }
 }
 
+// ===========================================================================
+// k_enlm<B, NK>: vips_affine at any enlargement whose windows fit the tiles below
+// (2 x, 3 x, 4 x, 1.5 x, per-axis mixes; the host checks), both passes on the matrix
+// cores in f16 with f32 accumulation — every product and partial sum is an exact f32
+// (bounds below), so the result is bicubic.cpp's integer arithmetic bit for bit.
+//
+// A block owns 64 output bytes of a row (4 units of 16 bytes) in 4 bands of output rows,
+// one per wave; the horizontal operands depend on the columns only and live in LDS, built
+// once per block.  A wave walks its band's input rows in tiles of 16:
+//  * staging: the tile's 16 rows x the wave's input window (<= 128 bytes, extend modes per
+//    byte only in chunks that cross an image edge), loaded two tiles ahead, into a
+//    wave-private LDS tile;
+//  * horizontal, per unit: D[m = input row][n = output byte] = v_mfma_f32_16x16x32_f16 of
+//    A = 8 staged bytes per lane (row m, bytes kb + 8 kg ..) as f16 1024 + p (one v_perm per
+//    two bytes: 0x64 high bytes) and B = the taps of output byte n at those bytes, split
+//    T = 64 Th + Tl into Th / 64 and Tl / 4096 (both exact in f16; two MFMAs).  Seed
+//    1200 + 2^-13 - sum(T) / 4: D = sum(T p) / 4096 + 2^-13 + 1200, so v_cvt_pk_f16_f32
+//    (round to nearest even, spacing 1 in [1024, 2048)) gives H + 1200 with H =
+//    (sum(T p) + 2048) >> 12, bicubic.cpp's rounded row sum — and lane (n, kg) now holds
+//    rows 4 kg .. 4 kg + 3 of column n: an A operand over rows, so H never leaves registers;
+//  * vertical, per 16 output rows once the tile holding their last H row is done:
+//    D[m = column][n = output row] = v_mfma_f32_16x16x32_f16 with K = (the lane's 4 H rows
+//    of the previous tile, its 4 of this tile) and B = the rows' taps placed at their H
+//    rows' K slots (a 64-bit shift of the 4 taps per part), split Ch / 64 and Cl / 4096;
+//    seed 2^-13 - 1200 sum(C) / 4096: D = sum(C H) / 4096 + 2^-13, and v_cvt_pk_u8_f32
+//    (round to nearest even, clamped) is (sum(C H) + 2048) >> 12 clamped; the 16 rows x 64
+//    bytes go out as 16-byte pieces through a wave tile.
+// Exactness: every partial sum of either product is a multiple of 2^-13 below 2^11 in
+// magnitude (24 bits), and f16 products are exact in f32.
+// ===========================================================================
+typedef _Float16 em_h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 em_h4 __attribute__((ext_vector_type(4)));
+typedef float em_f4 __attribute__((ext_vector_type(4)));
+constexpr int kEmNU = 4;           // 16-byte output units per wave
+constexpr int kEmOS = 80;          // output tile row stride (bytes)
+constexpr float kEmMagic = 1200.0f;
+constexpr int kEmRec = 8;       // ints per axis record: {pos, tap sum, taps 0 1, taps 2 3 (int16)}, {pos, tap sum, Ch + 64, Cl (u8 x 4)}
+
+struct EnlmArgs {
+    const u8 *in;
+    u8 *out;
+    int w, h, ow, oh, extend, fill;
+    const int4 *cols;  // [ow][2] em_axis records of output column x
+    const int4 *rows;  // [oh][2] the same of output row y
+    long long in_img, out_img;
+    int groups, bands, br;  // column groups of 64 output bytes; bands of br output rows
+    int bquads;             // blocks per column group and image: (bands + 3) / 4
+    int rs;                 // staged row stride (bytes, 16 x odd: conflict-free operand reads)
+    int ncr;                // 16-byte chunks staged per row (<= 8)
+    long long blocks;
+};
+
+// 8 bytes -> 8 f16 of value 1024 + p
+__device__ __forceinline__ em_h8 em_cvt8(uint32_t lo, uint32_t hi) {
+    const uint32_t k = 0x64646464u;
+    return __builtin_bit_cast(em_h8, rc_u4{__builtin_amdgcn_perm(k, lo, 0x04010400u), __builtin_amdgcn_perm(k, lo, 0x04030402u),
+                                           __builtin_amdgcn_perm(k, hi, 0x04010400u), __builtin_amdgcn_perm(k, hi, 0x04030402u)});
+}
+// tap i (0..3; anything else: 0) of an axis record
+__device__ __forceinline__ int em_tap(const int4 &r, int i) {
+    const int v = i < 2 ? r.z : r.w;
+    const int t = (i & 1) ? (v >> 16) : static_cast<int>(static_cast<int16_t>(v & 0xffff));
+    return (i >= 0 && i < 4) ? t : 0;
+}
+
+template <int B, int NK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) k_enlm(EnlmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t ems[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // a block = one column group x 4 consecutive bands (wave w: band 4 q + w), so the
+    // horizontal operands, which depend on the columns only, are built once per block
+    const long long blk = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring groups (shared halo) on one L2
+    const int grp = static_cast<int>(blk % a.groups);
+    const long long rest = blk / a.groups;
+    const int band = 4 * static_cast<int>(rest % a.bquads) + wave;
+    const int img = static_cast<int>(rest / a.bquads);
+    u8 *opl = reinterpret_cast<u8 *>(ems);  // [unit][ks][hi, lo][64 lanes] x 16 bytes
+    u8 *stg = opl + kEmNU * NK * 2 * 1024 + wave * (16 * a.rs + 16 * kEmOS + 16 * a.br);
+    u8 *otl = stg + 16 * a.rs;
+    int4 *rrec = reinterpret_cast<int4 *>(otl + 16 * kEmOS);  // [br] the band's row records
+    const int n = lane & 15, kg = lane >> 4;
+    const int rowb = a.ow * B, pitch = a.w * B;
+    const int x0b = 64 * grp;
+    const int ws = B * (a.cols[2 * (x0b / B)].x - 2);  // input byte of staged column 0
+
+    // ---- horizontal operands: wave w builds unit w's into LDS; K origins and seeds per wave ----
+    int kb[kEmNU];
+    float hseed[kEmNU];
+#pragma unroll
+    for (int u = 0; u < kEmNU; ++u) {
+        // K origin: channel 0 of the unit's first pixel (a later pixel with the same first
+        // tap, e.g. at 3 x, starts its channel 0 there), 8-byte aligned for ds_read_b64
+        const int xf = min(x0b + 16 * u, rowb - 1) / B;
+        kb[u] = __builtin_amdgcn_readfirstlane((B * (a.cols[2 * xf].x - 2) - ws) & ~7);
+        const int ob = min(x0b + 16 * u + n, rowb - 1);
+        const int x = ob / B, c = ob - B * x;
+        const int4 cr = a.cols[2 * x];
+        hseed[u] = kEmMagic + 1.0f / 8192.0f - 0.25f * static_cast<float>(cr.y);
+        if (u != wave) continue;
+        const int first = B * (cr.x - 2) + c - ws;
+#pragma unroll
+        for (int ks = 0; ks < NK; ++ks) {
+            em_h8 th, tl;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int e = kb[u] + 32 * ks + 8 * kg + j - first;
+                const int i = e / B;
+                const int T = (e >= 0 && e - B * i == 0) ? em_tap(cr, i) : 0;
+                th[j] = static_cast<_Float16>(static_cast<float>(T >> 6) * (1.0f / 64.0f));
+                tl[j] = static_cast<_Float16>(static_cast<float>(T & 63) * (1.0f / 4096.0f));
+            }
+            *reinterpret_cast<em_h8 *>(opl + ((u * NK + ks) * 2) * 1024 + 16 * lane) = th;
+            *reinterpret_cast<em_h8 *>(opl + ((u * NK + ks) * 2 + 1) * 1024 + 16 * lane) = tl;
+        }
+    }
+    __syncthreads();
+    if (band >= a.bands) return;  // after the barrier: whole waves, no barrier follows
+
+    // ---- staging: chunk q = lane + 64 j of a tile = (row q / ncr, column chunk q % ncr),
+    // loaded one tile ahead ----
+    const int ya = band * a.br, yb = min(ya + a.br, a.oh);
+    const int ra = a.rows[2 * ya].x - 2, rb = a.rows[2 * (yb - 1)].x + 1;
+    const int ntile = (rb - ra + 16) >> 4;
+    int delta = 0;
+    const __amdgpu_buffer_rsrc_t src = image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &delta);
+    const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
+    int crow[2], ccol[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int q = lane + 64 * j;
+        crow[j] = q / a.ncr;
+        ccol[j] = q - crow[j] * a.ncr;
+    }
+    // a tile's chunks in flight: the raw 20 bytes from the dword-aligned-down offset and the
+    // byte shift, realigned (v_alignbyte) only when the tile is written to LDS, so the loads
+    // are not waited for when they are issued
+    rc_u4 pq[2];
+    uint32_t pe[2], psh[2];
+    auto load = [&](int r0) {
+        const bool redge = r0 < 0 || r0 + 16 > a.h;  // uniform: rows through the extend mode
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            pq[j] = rc_u4{0u, 0u, 0u, 0u};
+            pe[j] = 0u;
+            psh[j] = 0u;
+            if (crow[j] >= 16) continue;
+            int sr = r0 + crow[j];
+            if (redge) sr = extend_idx(sr, a.h, a.extend);
+            const int b0 = ws + 16 * ccol[j];
+            if (sr < 0) {
+                const uint32_t f = 0x01010101u * static_cast<uint32_t>(a.fill);
+                pq[j] = rc_u4{f, f, f, f};
+            } else if (b0 >= 0 && b0 + 16 <= pitch) {
+                const int off = sr * pitch + b0 + delta;
+                pq[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off & ~3, 0, 0));
+                pe[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
+                psh[j] = static_cast<uint32_t>(off & 3);
+            } else {  // a chunk across an image edge: per byte through the extend mode
+                uint32_t d[4] = {0u, 0u, 0u, 0u};
+                for (int e = 0; e < 16; ++e) {
+                    const int ib = b0 + e;
+                    const int col = ib >= 0 ? ib / B : -((-ib + B - 1) / B);
+                    const int ch = ib - col * B;
+                    const int sc = extend_idx(col, a.w, a.extend);
+                    const uint32_t byte = sc < 0 ? static_cast<uint32_t>(a.fill)
+                                                 : static_cast<uint32_t>(a.in[img * a.in_img + static_cast<long long>(sr) * pitch + sc * B + ch]);
+                    d[e >> 2] |= byte << (8 * (e & 3));
+                }
+                pq[j] = rc_u4{d[0], d[1], d[2], d[3]};
+            }
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (crow[j] < 16) {
+                const rc_u4 p = pq[j];
+                const uint32_t sh = psh[j];
+                *reinterpret_cast<rc_u4 *>(stg + crow[j] * a.rs + 16 * ccol[j]) =
+                    rc_u4{__builtin_amdgcn_alignbyte(p.y, p.x, sh), __builtin_amdgcn_alignbyte(p.z, p.y, sh),
+                          __builtin_amdgcn_alignbyte(p.w, p.z, sh), __builtin_amdgcn_alignbyte(pe[j], p.w, sh)};
+            }
+    };
+
+    em_h8 hh[kEmNU];  // H + 1200: the lane's 4 rows of the previous tile, then of this tile
+#pragma unroll
+    for (int u = 0; u < kEmNU; ++u) hh[u] = em_h8{0, 0, 0, 0, 0, 0, 0, 0};
+    int oy = ya;  // the next 16 output rows
+    // row records of the lane's output row in the next two groups of 16 (clipped to the
+    // band), each loaded two groups before it is used
+    // the band's row records into the wave's LDS once: read per 16 output rows from there
+    // (a record in registers loaded ahead across the variable-length emission loop would
+    // make the compiler wait for every load in flight, the staging ones included)
+    for (int i = lane; i < yb - ya; i += 64) rrec[i] = a.rows[2 * (ya + i) + 1];
+    load(ra);
+    for (int t = 0; t < ntile; ++t) {
+        const int r0 = ra + 16 * t;
+        put();
+        if (t + 1 < ntile) load(r0 + 16);
+        // horizontal: H + 1200 of rows r0 .. r0 + 15 for the wave's 64 output bytes
+#pragma unroll
+        for (int u = 0; u < kEmNU; ++u) {
+            em_f4 d = em_f4{hseed[u], hseed[u], hseed[u], hseed[u]};
+#pragma unroll
+            for (int ks = 0; ks < NK; ++ks) {
+                const uint2 v = *reinterpret_cast<const uint2 *>(stg + n * a.rs + kb[u] + 32 * ks + 8 * kg);
+                const em_h8 th = *reinterpret_cast<const em_h8 *>(opl + ((u * NK + ks) * 2) * 1024 + 16 * lane);
+                const em_h8 tl = *reinterpret_cast<const em_h8 *>(opl + ((u * NK + ks) * 2 + 1) * 1024 + 16 * lane);
+                const em_h8 av = em_cvt8(v.x, v.y);
+                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, th, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, tl, d, 0, 0, 0);
+            }
+            hh[u] = em_h8{hh[u][4], hh[u][5], hh[u][6], hh[u][7], static_cast<_Float16>(d[0]), static_cast<_Float16>(d[1]),
+                          static_cast<_Float16>(d[2]), static_cast<_Float16>(d[3])};
+        }
+        // vertical: every 16 output rows whose last H row is in this tile
+        while (oy < yb) {
+            const int yl = min(oy + 15, yb - 1);
+            // the lane's output row record (clipped to the band); lane 15 holds row yl
+            const int4 c0 = rrec[min(oy + n, yl) - ya];
+            if (__builtin_amdgcn_readlane(c0.x, 15) + 1 > r0 + 15) break;
+            // the row's taps as f16 operands: Ch / 64 from the byte Ch + 64 (f16 1024 + byte
+            // by v_perm, then x / 64 - 17) and Cl / 4096 (1024 + Cl, then x / 4096 - 1 / 4),
+            // every step exact in f16
+            typedef _Float16 em_h2 __attribute__((ext_vector_type(2)));
+            const uint32_t k64 = 0x64646464u;
+            auto cvt2 = [&](uint32_t w, uint32_t sel, float sc, float off) {
+                const em_h2 x = __builtin_bit_cast(em_h2, __builtin_amdgcn_perm(k64, w, sel));
+                const em_h2 r = x * em_h2{static_cast<_Float16>(sc), static_cast<_Float16>(sc)} +
+                                em_h2{static_cast<_Float16>(off), static_cast<_Float16>(off)};
+                return __builtin_bit_cast(uint32_t, r);
+            };
+            const uint32_t uh = static_cast<uint32_t>(c0.z), ul = static_cast<uint32_t>(c0.w);
+            const uint64_t th64 = (static_cast<uint64_t>(cvt2(uh, 0x04030402u, 1.0f / 64.0f, -17.0f)) << 32) |
+                                  cvt2(uh, 0x04010400u, 1.0f / 64.0f, -17.0f);
+            const uint64_t tl64 = (static_cast<uint64_t>(cvt2(ul, 0x04030402u, 1.0f / 4096.0f, -0.25f)) << 32) |
+                                  cvt2(ul, 0x04010400u, 1.0f / 4096.0f, -0.25f);
+            // B: the 4 taps moved to the K slots of their H rows: slot j of this tile holds
+            // tap j - s, of the previous tile j - s - 16
+            const int s = c0.x - 2 - (r0 + 4 * kg);
+            auto place = [](uint64_t v, int sh) -> uint64_t {
+                return sh >= 4 || sh <= -4 ? 0ull : sh >= 0 ? v << (16 * sh) : v >> (-16 * sh);
+            };
+            const uint64_t hc = place(th64, s), lc = place(tl64, s), hp = place(th64, s + 16), lp = place(tl64, s + 16);
+            const em_h8 bh = __builtin_bit_cast(em_h8, rc_u4{static_cast<uint32_t>(hp), static_cast<uint32_t>(hp >> 32),
+                                                             static_cast<uint32_t>(hc), static_cast<uint32_t>(hc >> 32)});
+            const em_h8 bl = __builtin_bit_cast(em_h8, rc_u4{static_cast<uint32_t>(lp), static_cast<uint32_t>(lp >> 32),
+                                                             static_cast<uint32_t>(lc), static_cast<uint32_t>(lc >> 32)});
+            const float vseed = 1.0f / 8192.0f - kEmMagic / 4096.0f * static_cast<float>(c0.y);
+#pragma unroll
+            for (int u = 0; u < kEmNU; ++u) {
+                // K = 32 as (the lane's 4 H rows of the previous tile, its 4 of this tile)
+                em_f4 d = em_f4{vseed, vseed, vseed, vseed};
+                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(hh[u], bh, d, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(hh[u], bl, d, 0, 0, 0);
+                // D = sum(C H) / 4096 + 2^-13: v_cvt_pk_u8_f32 (round to nearest even, clamped
+                // to 0..255, profiles/r05/enlm/cvt_pk_u8.txt) gives (sum(C H) + 2048) >> 12 clamped
+                uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(d[0], 0, 0u);
+                q = __builtin_amdgcn_cvt_pk_u8_f32(d[1], 1, q);
+                q = __builtin_amdgcn_cvt_pk_u8_f32(d[2], 2, q);
+                q = __builtin_amdgcn_cvt_pk_u8_f32(d[3], 3, q);
+                *reinterpret_cast<uint32_t *>(otl + n * kEmOS + 16 * u + 4 * kg) = q;
+            }
+            // 16 rows x 64 bytes as 16-byte pieces: lane = (row lane / 4, piece lane % 4)
+            const int rr = lane >> 2, pc2 = lane & 3;
+            const rc_u4 v = *reinterpret_cast<const rc_u4 *>(otl + rr * kEmOS + 16 * pc2);
+            const int yy = oy + rr, bo = x0b + 16 * pc2;
+            if (yy <= yl && bo < rowb) {
+                const int off = yy * rowb + bo;
+                if (bo + 16 <= rowb) {
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, v), dst, off, 0, 0);
+                } else {
+                    for (int e = 0; e < rowb - bo; ++e)
+                        __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(v[e >> 2] >> (8 * (e & 3))), dst, off + e, 0, 0);
+                }
+            }
+            oy += 16;
+        }
+    }
+}
+
 // vips_zoom: output row Y = source row Y / yf, output pixel x = source pixel x / xf.
 // r03: a block makes one 4 KiB chunk of the output rows of ONE source row: the source
 // bytes the chunk needs are staged in LDS with 16-byte loads (from the dword-aligned-
@@ -563,6 +849,188 @@ __global__ void __launch_bounds__(256) k_zoom_rows(const u8 *__restrict__ in, u8
     }
 }
 
+// host restatement of af_ix (the same double expression, so the same rounding)
+int enlm_ix(int o, double s, int *phase) {
+    const double X = (o + 0.5) / s - 0.5 + 1.0;
+    *phase = ((static_cast<int>(X * 256.0) & 255) + 1) >> 1;
+    return static_cast<int>(X);
+}
+
+// Per-axis records of k_enlm, output positions 0 .. cap - 1 at scale s: {first window
+// pixel + 2 (af_ix), the phase's tap sum, taps 0 1, taps 2 3 as int16 pairs}.  A record
+// depends on (o, s) only, so one table per (device, scale) serves every size; grown by
+// doubling (a replaced table stays allocated: kernels in flight may read it).  Dropped
+// when the engine's device tables are (device_tables_generation).
+struct EmAxis {
+    std::vector<int> host;  // [cap][kEmRec]
+    const int4 *dev;
+    unsigned gen;
+};
+std::mutex g_em_mu;
+std::map<std::pair<int, double>, EmAxis> &em_axes() {
+    static auto *m = new std::map<std::pair<int, double>, EmAxis>();
+    return *m;
+}
+std::vector<int4 *> &em_retired() {
+    static auto *v = new std::vector<int4 *>();
+    return *v;
+}
+
+const EmAxis *em_axis_locked(int dev, double s, int n) {
+    const unsigned gen = device_tables_generation();
+    auto &m = em_axes();
+    auto it = m.find({dev, s});
+    if (it != m.end() && it->second.gen == gen && static_cast<int>(it->second.host.size() / kEmRec) >= n) return &it->second;
+    int cap = 1024;
+    while (cap < n) cap *= 2;
+    int tab[(kTransformScale + 1) * 4];
+    bicubic_table(tab);
+    EmAxis ax;
+    ax.host.resize(static_cast<size_t>(cap) * kEmRec);
+    for (int o = 0; o < cap; ++o) {
+        int ph = 0;
+        const int p = enlm_ix(o, s, &ph);
+        const int *c = tab + 4 * ph;
+        int *r = ax.host.data() + kEmRec * static_cast<size_t>(o);
+        const int sum = c[0] + c[1] + c[2] + c[3];
+        r[0] = p;
+        r[1] = sum;
+        r[2] = static_cast<int>((static_cast<uint32_t>(c[0]) & 0xffffu) | (static_cast<uint32_t>(c[1]) << 16));
+        r[3] = static_cast<int>((static_cast<uint32_t>(c[2]) & 0xffffu) | (static_cast<uint32_t>(c[3]) << 16));
+        // as a row: {pos, tap sum, Ch + 64 (u8 x 4), Cl (u8 x 4)} (C = 64 Ch + Cl)
+        uint32_t hi = 0, lo = 0;
+        for (int k = 0; k < 4; ++k) {
+            hi |= static_cast<uint32_t>((c[k] >> 6) + 64) << (8 * k);
+            lo |= static_cast<uint32_t>(c[k] & 63) << (8 * k);
+        }
+        r[4] = p;
+        r[5] = sum;
+        r[6] = static_cast<int>(hi);
+        r[7] = static_cast<int>(lo);
+    }
+    int4 *d = nullptr;
+    if (hipMalloc(&d, ax.host.size() * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, ax.host.data(), ax.host.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    if (it != m.end() && it->second.gen == gen) em_retired().push_back(const_cast<int4 *>(it->second.dev));
+    ax.dev = d;
+    ax.gen = gen;
+    m[{dev, s}] = std::move(ax);
+    return &m[{dev, s}];
+}
+
+// k_enlm's geometry, or false when the scale is outside its tiles: every unit's taps within
+// 32 NK staged bytes of its K origin (NK <= 2, window <= 128 bytes), every 16 output rows'
+// H rows within 17 consecutive rows (so within two 16-row tiles).  Plans are cached per
+// (device, n, w, h, b, xs, ys) (the checks walk every column and row).
+struct EmPlan {
+    bool ok;
+    int nk;
+    EnlmArgs g;
+    unsigned gen;
+};
+bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys, EnlmArgs *out, int *nk_out) {
+    if (!(xs >= 1.0) || !(ys >= 1.0) || n <= 0) return false;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    std::lock_guard<std::mutex> lk(g_em_mu);
+    static auto *plans = new std::map<std::tuple<int, int, int, int, int, double, double>, EmPlan>();
+    const unsigned gen = device_tables_generation();
+    const auto key = std::make_tuple(dev, n, w, h, b, xs, ys);
+    auto pit = plans->find(key);
+    if (pit != plans->end() && pit->second.gen == gen) {
+        *out = pit->second.g;
+        *nk_out = pit->second.nk;
+        return pit->second.ok;
+    }
+    if (plans->size() > 1024) plans->clear();
+    EmPlan pl{false, 0, EnlmArgs{}, gen};
+    const EmAxis *cx = em_axis_locked(dev, xs, ow);
+    const int4 *cols = cx ? cx->dev : nullptr;
+    const std::vector<int> xh = cx ? cx->host : std::vector<int>();
+    const EmAxis *cy = em_axis_locked(dev, ys, oh);
+    if (!cols || !cy) return false;
+    const int *px = xh.data(), *py = cy->host.data();
+    const int rowb = ow * b;
+    const int groups = (rowb + 63) / 64;
+    int nk = 1, kbmax = 0;
+    bool ok = true;
+    for (int gi = 0; gi < groups && ok; ++gi) {
+        const int x0b = 64 * gi;
+        const int ws = b * (px[kEmRec * (x0b / b)] - 2);
+        for (int u = 0; u < kEmNU; ++u) {
+            const int xf = std::min(x0b + 16 * u, rowb - 1) / b;
+            const int kbu = (b * (px[kEmRec * xf] - 2) - ws) & ~7;
+            int last = 0;
+            for (int l = 0; l < 16; ++l) {
+                const int ob = std::min(x0b + 16 * u + l, rowb - 1);
+                const int x = ob / b;
+                last = std::max(last, b * (px[kEmRec * x] + 1) + (ob - b * x) - ws);
+            }
+            const int need = (last - kbu) / 32 + 1;
+            if (kbu < 0 || need > 2) {
+                ok = false;
+                break;
+            }
+            nk = std::max(nk, need);
+            kbmax = std::max(kbmax, kbu);
+        }
+    }
+    const int iwb = (kbmax + 32 * nk + 15) & ~15;
+    ok = ok && iwb <= 128;
+    int rs = iwb;
+    while ((rs / 16) % 2 == 0) rs += 16;
+    // LDS per block for a band height (the kernel's layout); 5 blocks per CU need <= 32 KB
+    auto lds_of = [&](int c) { return kEmNU * nk * 2 * 1024 + 4 * (16 * rs + 16 * kEmOS + 16 * c); };
+    // band height: the multiple of 16 output rows whose input tiles are best used (input rows
+    // needed / staged) times the share of a block's 4 waves that have a band, among those
+    // that still give >= 8192 waves
+    int br = 64;
+    double best = -1.0;
+    for (int c = 64; c <= 256; c += 16) {
+        const double rows = c / ys;
+        const int nb = (oh + c - 1) / c;
+        const double eff = rows / (16.0 * std::ceil((rows + 4.0) / 16.0)) * nb / (4.0 * ((nb + 3) / 4));
+        const long long tasks = static_cast<long long>(groups) * nb * n;
+        if (tasks < 8192 && c > 64) break;
+        if (lds_of(c) > 32 * 1024 && c > 64) break;
+        if (eff > best + 1e-9) {
+            best = eff;
+            br = c;
+        }
+    }
+    const int bands = (oh + br - 1) / br;
+    for (int band = 0; band < bands && ok; ++band) {
+        const int ya = band * br, yb = std::min(ya + br, oh);
+        for (int oy = ya; oy < yb; oy += 16) {
+            const int yl = std::min(oy + 15, yb - 1);
+            if (py[kEmRec * yl] + 1 - (py[kEmRec * oy] - 2) + 1 > 17) {
+                ok = false;
+                break;
+            }
+        }
+    }
+    if (ok) {
+        pl.g.cols = cols;
+        pl.g.rows = cy->dev;
+        pl.g.groups = groups;
+        pl.g.bands = bands;
+        pl.g.br = br;
+        pl.g.rs = rs;
+        pl.g.ncr = iwb / 16;
+        pl.g.bquads = (bands + 3) / 4;
+        pl.g.blocks = static_cast<long long>(groups) * pl.g.bquads * n;
+        pl.nk = nk;
+        pl.ok = true;
+    }
+    (*plans)[key] = pl;
+    *out = pl.g;
+    *nk_out = pl.nk;
+    return pl.ok;
+}
+
 }  // namespace
 
 int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, double ys, int extend,
@@ -584,6 +1052,28 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
     a.in_img = img_bytes(w, h, b);
     a.out_img = img_bytes(a.ow, a.oh, b);
     if (a.in_img >= 0x7fffffffLL) return MIPX_EUNSUPPORTED;
+    // enlargements on the matrix cores (k_enlm); MIPX_ENLM=0 keeps the VALU kernels (A/B),
+    // 2 (tests) makes a scale outside k_enlm's tiles an error instead of a fallback
+    const char *em = tune_env("MIPX_ENLM");
+    if (!(em && *em == '0') && a.out_img < 0x7fffffffLL) {
+        EnlmArgs g{};
+        int nk = 0;
+        if (enlm_plan(n, w, h, b, a.ow, a.oh, xs, ys, &g, &nk)) {
+            g.in = in, g.out = out, g.w = w, g.h = h, g.ow = a.ow, g.oh = a.oh, g.extend = a.extend, g.fill = a.fill;
+            g.in_img = a.in_img, g.out_img = a.out_img;
+            if (grid_ok(g.blocks)) {
+                const size_t lds = static_cast<size_t>(kEmNU) * nk * 2 * 1024 + 4 * static_cast<size_t>(16 * g.rs + 16 * kEmOS + 16 * g.br);
+                const dim3 grid(static_cast<unsigned>(g.blocks));
+                if (nk == 1) {
+                    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_enlm<B_, 1>), grid, dim3(256), lds, st, g));
+                } else {
+                    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_enlm<B_, 2>), grid, dim3(256), lds, st, g));
+                }
+                return launch_check("k_enlm");
+            }
+        }
+        if (em && *em == '2') return MIPX_EUNSUPPORTED;  // tests: k_enlm or an error
+    }
     // exactly 2 x 2: the fixed-pattern kernel (MIPX_ENLARGE2=0 / 1 forces it off / on, A/B)
     const char *e2 = tune_env("MIPX_ENLARGE2");
     // (strips of 256 output pixels: a ragged last strip leaves lanes idle; below 90 % strip

@@ -128,7 +128,10 @@ __device__ __forceinline__ void rc_edge_frag(const float *tabf, int taps, int pp
 // each).  Output rows start on a dword (host-checked).
 // WPE: the minimum waves per SIMD the register allocation must allow (1: the compiler's
 // choice; 4 for the one build where that costs only two spilled registers)
-template <int B, int NKS, int KMAX, int WPE>
+// UNAL (r05): input rows off a dword (w B % 4 != 0, e.g. C5's 1333-pixel RGB rows): every
+// 16-byte chunk is loaded from its dword-aligned-down offset with the next dword and
+// realigned (v_alignbyte) when it is written to the ring
+template <int B, int NKS, int KMAX, int WPE, bool UNAL = false>
 __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_rcol(RcArgs a) {
     constexpr int WV = kRcNT / 64, XW = 16 * WV;
     constexpr int UPW = B;  // horizontal units per wave: XW B / 16 / WV
@@ -162,7 +165,9 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     const int ka = a.k0 + seg * a.seg_steps;  // this segment's 16-row groups [ka, ka + steps)
     const int steps = min(a.k0 + a.ksteps, ka + a.seg_steps) - ka;
 
-    const __amdgpu_buffer_rsrc_t src = image_rsrc(a.in + img * a.in_img, a.in_img);
+    int idelta = 0;  // UNAL: byte offset of the image in its dword-aligned-down descriptor
+    const __amdgpu_buffer_rsrc_t src = UNAL ? image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &idelta)
+                                            : image_rsrc(a.in + img * a.in_img, a.in_img);
     const __amdgpu_buffer_rsrc_t prs = image_rsrc(a.plan, static_cast<long long>(a.plan_rows) * kRcolPlanRow);
     rc_cint *srow = (rc_cint *)(a.plan + static_cast<size_t>(a.plan_rows) * kRcolPlanRow);  // [group][first, end]
     const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
@@ -258,20 +263,31 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // (no memory access) and they write nothing, so a narrow strip's lanes do not reach
     // past a step's new rows into ring slots still in use (r03: admits narrow last
     // strips and shrinks to ~2.5)
+    uint32_t re[2][UNAL ? KMAX : 1];  // UNAL: the dword after each chunk
+    auto chunk_off = [&](int r, int j) { return clampi(r + rr[j], 0, a.h - 1) * pitch + cof[j] + idelta; };
+    auto realign = [&](rc_u4 v, uint32_t e, int off) -> rc_u4 {
+        if constexpr (!UNAL) return v;
+        const uint32_t sh = static_cast<uint32_t>(off & 3);
+        return rc_u4{__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh),
+                     __builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(e, v.w, sh)};
+    };
     auto issue_ring = [&](auto pc, int r0) {
         constexpr int P = decltype(pc)::value;
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            rv[P][j] = __builtin_bit_cast(
-                rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
-                           src, rr[j] < a.rcap ? clampi(r0 + rr[j], 0, a.h - 1) * pitch + cof[j] : 0x7ffffff0, 0, 0));
+        for (int j = 0; j < KMAX; ++j) {
+            const int off = rr[j] < a.rcap ? chunk_off(r0, j) : 0x7ffffff0;
+            rv[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
+            if constexpr (UNAL)
+                re[P][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
+        }
     };
     auto write_ring = [&](auto pc, int r0) {
         constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             if (rr[j] < a.rcap)
-                lds_wr128(static_cast<uint32_t>(((r0 + rr[j]) & a.rmask) * a.rs) + lcol[j], rv[P][j] ^ 0x80808080u);
+                lds_wr128(static_cast<uint32_t>(((r0 + rr[j]) & a.rmask) * a.rs) + lcol[j],
+                          realign(rv[P][j], re[P][UNAL ? j : 0], chunk_off(r0, j)) ^ 0x80808080u);
     };
     // wst: the wave's units are consecutive (bytes 16 UPW wave ..), staged through a
     // wave-private LDS tile [16 rows][16 UPW (+ 16 for RGBA: bank spread) bytes] and
@@ -412,14 +428,18 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     const int bka = srow[2 * ka], eka = srow[2 * ka + 1];
     for (int r = bka; r < eka; r += lkf) {
         rc_u4 tv[KMAX];
+        uint32_t te[UNAL ? KMAX : 1];
 #pragma unroll
-        for (int j = 0; j < KMAX; ++j)
-            tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  src, clampi(r + rr[j], 0, a.h - 1) * pitch + cof[j], 0, 0));
+        for (int j = 0; j < KMAX; ++j) {
+            const int off = chunk_off(r, j);
+            tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
+            if constexpr (UNAL) te[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
+        }
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             if (rr[j] < lkf && r + rr[j] < eka)
-                lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j], tv[j] ^ 0x80808080u);
+                lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j],
+                          realign(tv[j], te[UNAL ? j : 0], chunk_off(r, j)) ^ 0x80808080u);
     }
     issue_taps(I0{}, ka);
     store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
@@ -913,7 +933,11 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     const long long in_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
     // out-of-range store offsets are built from 2^29 and 2^31 (k_rcol store)
     if (in_img >= 0x7fffffffLL || out_img >= (1LL << 29)) return MIPX_EUNSUPPORTED;
-    if ((w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0) return MIPX_EUNSUPPORTED;
+    // input rows off a dword: the realigning build (RGB only; MIPX_RCOL_UNAL=0 keeps them
+    // on k_rmf2, A/B)
+    const bool unal = (w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0;
+    const char *eun = tune_env("MIPX_RCOL_UNAL");
+    if (unal && (b != 3 || (eun && *eun == '0') || in_img >= 0x7fffff00LL)) return MIPX_EUNSUPPORTED;
     // output rows off a dword go out as unaligned 16-byte pieces (wst 3); with the 4-byte
     // stores (MIPX_RCOL_WST=0) they stay on k_rmf2
     const bool out_al = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
@@ -1019,7 +1043,9 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     const char *esz = tune_env("MIPX_RCOL_SWZ");
     a.swz = !(esz && *esz == '0');
     const void *fn = nullptr;
-#define MIPX_RC_K(B_, NKS_, KM_) fn = reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, 1>);
+#define MIPX_RC_K(B_, NKS_, KM_)                                                                  \
+    fn = unal ? reinterpret_cast<const void *>(&k_rcol<3, NKS_, KM_, 1, true>)                     \
+              : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, 1>);
 #define MIPX_RC_KM(B_, NKS_) \
     if (kmax == 3) { MIPX_RC_K(B_, NKS_, 3) } else { MIPX_RC_K(B_, NKS_, 6) }
     if (b == 3) {
@@ -1061,7 +1087,7 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // MIPX_RCOL_W4=1 (A/B): the 4-wave build whatever the plan says (RGBA too)
     const char *ew4 = tune_env("MIPX_RCOL_W4");
     const bool force4 = ew4 && *ew4 == '1';
-    if (nks == 1 && kmax == 3 && (b == 3 || force4)) {
+    if (nks == 1 && kmax == 3 && !unal && (b == 3 || force4)) {
         const void *f4 = b == 3 ? reinterpret_cast<const void *>(&k_rcol<3, 1, 3, 4>)
                                 : reinterpret_cast<const void *>(&k_rcol<4, 1, 3, 4>);
         int segs4 = 1;

@@ -60,10 +60,57 @@ E2_CASES = [  # h, w, b, extend: k_enlarge2 (exactly 2 x 2) at every band count 
 @pytest.mark.parametrize("h,w,b,extend", E2_CASES)
 def test_enlarge2_matches_oracle(gpu, oracle, rng, monkeypatch, e2, h, w, b, extend):
     """vips_affine at exactly 2 x 2 on k_enlarge2 (the fixed phase-96 / phase-32 pattern,
-    MIPX_ENLARGE2=1, default) and on k_affine_sep (0): strips and bands that end at the
+    MIPX_ENLARGE2=1) and on k_affine_sep (0), k_enlm off: strips and bands that end at the
     image edges, images narrower than the 6-pixel window, every extend mode, all bands."""
+    monkeypatch.setenv("MIPX_ENLM", "0")
     monkeypatch.setenv("MIPX_ENLARGE2", e2)
     imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
     got = gpu.run_op("affine", imgs, xscale=2.0, yscale=2.0, extend=extend)
     for i in range(2):
         assert_same(got[i], oracle.affine(imgs[i], 2.0, 2.0, extend), f"enlarge2 e2={e2} {h}x{w}x{b} e{extend} img{i}")
+
+
+# k_enlm (both passes on the matrix cores): integer and fractional scales, per-axis mixes,
+# every extend mode, every band count, ragged last column groups and bands, images smaller
+# than a tile, the op-survey shapes
+ENLM_SCALES = [(2.0, 2.0), (3.0, 3.0), (4.0, 4.0), (1.5, 1.5), (2.5, 2.5), (3.0, 2.0), (2.0, 4.0), (1.5, 3.0),
+               (1.4, 1.4), (5.0, 5.0), (8.0, 8.0)]
+ENLM_SHAPES = [(740, 550, 3, 1), (33, 1201, 4, 0), (97, 203, 1, 2), (61, 130, 2, 3), (64, 640, 3, 4),
+               (5, 7, 3, 5), (1, 1, 4, 1), (2, 3, 3, 0), (70, 129, 4, 1), (129, 128, 3, 3), (31, 30, 1, 1),
+               (1151, 1150, 3, 1)]
+
+
+@pytest.mark.parametrize("xs,ys", ENLM_SCALES, ids=[f"{x}x{y}" for x, y in ENLM_SCALES])
+def test_enlm_matches_oracle(gpu, oracle, rng, monkeypatch, xs, ys):
+    monkeypatch.setenv("MIPX_ENLM", "2")  # k_enlm or an error, never a fallback
+    for h, w, b, extend in ENLM_SHAPES:
+        if h * w * xs * ys > 3e6:
+            continue
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("affine", imgs, xscale=xs, yscale=ys, extend=extend)
+        for i in range(2):
+            assert_same(got[i], oracle.affine(imgs[i], xs, ys, extend), f"enlm {h}x{w}x{b} {xs}x{ys} e{extend} img{i}")
+
+
+def test_enlm_extremes(gpu, oracle, monkeypatch):
+    """Saturating content (0 / 255 steps: the bicubic over- and undershoot, H outside
+    0..255 before the vertical pass) at 2 x, 3 x and 1.5 x."""
+    monkeypatch.setenv("MIPX_ENLM", "2")
+    h, w = 90, 130
+    y, x = np.mgrid[0:h, 0:w]
+    for b in (1, 3, 4):
+        chans = [(((x // 3 + y // 3) % 2) * 255), ((x % 2) * 255), ((y % 2) * 255), np.full((h, w), 255)]
+        img = np.stack(chans[:b], -1).astype(np.uint8)
+        for s in (2.0, 3.0, 1.5):
+            got = gpu.run_op("affine", img[None], xscale=s, yscale=s, extend=1)
+            assert_same(got[0], oracle.affine(img, s, s, 1), f"enlm extremes b{b} x{s}")
+
+
+def test_enlm_declines_outside_its_tiles(gpu, rng, monkeypatch):
+    """Scales below 1 or too close to 1 are outside k_enlm's tiles: with MIPX_ENLM=2 an
+    error, by default the other kernels (checked against the oracle elsewhere)."""
+    monkeypatch.setenv("MIPX_ENLM", "2")
+    img = rng.integers(0, 256, (1, 40, 50, 3), dtype=np.uint8)
+    for xs, ys in ((0.8, 2.0), (2.0, 1.0), (1.2, 1.1)):
+        with pytest.raises(Exception):
+            gpu.run_op("affine", img, xscale=xs, yscale=ys, extend=1)

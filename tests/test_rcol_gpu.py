@@ -3,8 +3,8 @@ the i8 matrix cores), against the oracle: strips at both image edges (the COPY e
 folded into the horizontal operands), images narrower than a strip and shorter than
 a step, segment boundaries in tall images, RGB and RGBA, shrink pairs across
 (1, 2.75), windows (reduce -> extract), unaligned output rows (byte stores) and a
-seeded fuzz over shapes.  Unaligned input rows leave k_rcol (MIPX_EUNSUPPORTED) for
-k_rmf2; those cases check that the hand-off stays exact."""
+seeded fuzz over shapes.  RGB input rows off a dword (r05) run k_rcol's realigning
+build (MIPX_RCOL_UNAL=0 leaves them to k_rmf2, as the norcol route does)."""
 import numpy as np
 import pytest
 
@@ -60,9 +60,7 @@ def test_rcol_fuzz(gpu, oracle):
     r = np.random.default_rng(20241220)
     for case in range(60):
         b = int(r.choice([3, 4]))
-        w = int(r.integers(1, 900))
-        if b == 3:
-            w = max(4, w & ~3)  # dword-aligned rows (k_rcol's domain)
+        w = int(r.integers(1, 900))  # RGB rows off a dword: the realigning build
         h = int(r.integers(1, 500))
         hs, vs = float(r.uniform(1.01, 2.74)), float(r.uniform(1.01, 2.74))
         if int(w / hs + 0.5) < 1 or int(h / vs + 0.5) < 1:
@@ -76,8 +74,9 @@ def test_rcol_fuzz(gpu, oracle):
 
 @pytest.mark.parametrize("probe", ["ok", "fail"])
 def test_unaligned_rows_probe_fallback(gpu, oracle, rng, monkeypatch, probe):
-    """Rows whose pitch is not a multiple of 4 bytes leave k_rcol for k_rmf2, whose
-    staging relies on direct-to-LDS loads at unaligned byte offsets.  Each device
+    """Rows whose pitch is not a multiple of 4 bytes: k_rcol's realigning build (rcol
+    routes) or k_rmf2 (norcol), whose staging relies on direct-to-LDS loads at unaligned
+    byte offsets.  Each device
     runs a probe of that behaviour once; MIPX_LDS_PROBE=fail makes the engine act as
     on a device that fails it, so those rows take the aligned-only kernels.  Both
     routes must give the oracle's bytes."""
