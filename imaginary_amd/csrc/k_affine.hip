@@ -544,8 +544,9 @@ __global__ void __launch_bounds__(256) k_enlarge2(Enl2Args a) {
 typedef _Float16 em_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 em_h4 __attribute__((ext_vector_type(4)));
 typedef float em_f4 __attribute__((ext_vector_type(4)));
-constexpr int kEmNU = 4;           // 16-byte output units per wave
-constexpr int kEmOS = 80;          // output tile row stride (bytes)
+// a wave's output columns: NU units of 16 bytes (4 or 8); its output tile's row stride
+// is 16 NU + 16 bytes (16 x odd)
+constexpr int em_os(int nu) { return 16 * nu + 16; }
 constexpr float kEmMagic = 1200.0f;
 constexpr int kEmRec = 8;       // ints per axis record: {pos, tap sum, taps 0 1, taps 2 3 (int16)}, {pos, tap sum, Ch + 64, Cl (u8 x 4)}
 
@@ -576,8 +577,9 @@ __device__ __forceinline__ int em_tap(const int4 &r, int i) {
     return (i >= 0 && i < 4) ? t : 0;
 }
 
-template <int B, int NK>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) k_enlm(EnlmArgs a) {
+template <int B, int NK, int NU>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 4 ? 5 : 4, 8))) k_enlm(EnlmArgs a) {
+    constexpr int kEmNU = NU, kEmOS = em_os(NU);
     extern __shared__ __attribute__((aligned(16))) uint32_t ems[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -594,10 +596,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
     int4 *rrec = reinterpret_cast<int4 *>(otl + 16 * kEmOS);  // [br] the band's row records
     const int n = lane & 15, kg = lane >> 4;
     const int rowb = a.ow * B, pitch = a.w * B;
-    const int x0b = 64 * grp;
+    const int x0b = 16 * NU * grp;
     const int ws = B * (a.cols[2 * (x0b / B)].x - 2);  // input byte of staged column 0
 
-    // ---- horizontal operands: wave w builds unit w's into LDS; K origins and seeds per wave ----
+    // ---- horizontal operands: wave w builds units w, w + 4 into LDS; K origins and seeds per wave ----
     int kb[kEmNU];
     float hseed[kEmNU];
 #pragma unroll
@@ -610,7 +612,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
         const int x = ob / B, c = ob - B * x;
         const int4 cr = a.cols[2 * x];
         hseed[u] = kEmMagic + 1.0f / 8192.0f - 0.25f * static_cast<float>(cr.y);
-        if (u != wave) continue;
+        if ((u & 3) != wave) continue;
         const int first = B * (cr.x - 2) + c - ws;
 #pragma unroll
         for (int ks = 0; ks < NK; ++ks) {
@@ -752,8 +754,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
             // B: the 4 taps moved to the K slots of their H rows: slot j of this tile holds
             // tap j - s, of the previous tile j - s - 16
             const int s = c0.x - 2 - (r0 + 4 * kg);
-            auto place = [](uint64_t v, int sh) -> uint64_t {
-                return sh >= 4 || sh <= -4 ? 0ull : sh >= 0 ? v << (16 * sh) : v >> (-16 * sh);
+            auto place = [](uint64_t v, int sh) -> uint64_t {  // branch-free: both shifts, then the range mask
+                const uint32_t l = static_cast<uint32_t>(min(max(16 * sh, 0), 48)), r = static_cast<uint32_t>(min(max(-16 * sh, 0), 48));
+                const uint64_t keep = (sh > -4 && sh < 4) ? ~0ull : 0ull;
+                return ((v << l) >> r) & keep;
             };
             const uint64_t hc = place(th64, s), lc = place(tl64, s), hp = place(th64, s + 16), lp = place(tl64, s + 16);
             const em_h8 bh = __builtin_bit_cast(em_h8, rc_u4{static_cast<uint32_t>(hp), static_cast<uint32_t>(hp >> 32),
@@ -775,17 +779,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))
                 q = __builtin_amdgcn_cvt_pk_u8_f32(d[3], 3, q);
                 *reinterpret_cast<uint32_t *>(otl + n * kEmOS + 16 * u + 4 * kg) = q;
             }
-            // 16 rows x 64 bytes as 16-byte pieces: lane = (row lane / 4, piece lane % 4)
-            const int rr = lane >> 2, pc2 = lane & 3;
-            const rc_u4 v = *reinterpret_cast<const rc_u4 *>(otl + rr * kEmOS + 16 * pc2);
-            const int yy = oy + rr, bo = x0b + 16 * pc2;
-            if (yy <= yl && bo < rowb) {
-                const int off = yy * rowb + bo;
-                if (bo + 16 <= rowb) {
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, v), dst, off, 0, 0);
-                } else {
-                    for (int e = 0; e < rowb - bo; ++e)
-                        __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(v[e >> 2] >> (8 * (e & 3))), dst, off + e, 0, 0);
+            // 16 rows x 16 NU bytes as 16-byte pieces: lane = (row lane / 4, pieces lane % 4 + 4 i)
+            const int rr = lane >> 2;
+#pragma unroll
+            for (int i = 0; i < NU / 4; ++i) {
+                const int pc2 = (lane & 3) + 4 * i;
+                const rc_u4 v = *reinterpret_cast<const rc_u4 *>(otl + rr * kEmOS + 16 * pc2);
+                const int yy = oy + rr, bo = x0b + 16 * pc2;
+                if (yy <= yl && bo < rowb) {
+                    const int off = yy * rowb + bo;
+                    if (bo + 16 <= rowb) {
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, v), dst, off, 0, 0);
+                    } else {  // the row's ragged end: whole dwords, then bytes
+                        const int nb = rowb - bo;
+#pragma unroll
+                        for (int d = 0; d < 3; ++d)
+                            if (4 * d + 4 <= nb) __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(v[d]), dst, off + 4 * d, 0, 0);
+                        for (int e = nb & ~3; e < nb; ++e)
+                            __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(v[e >> 2] >> (8 * (e & 3))), dst, off + e, 0, 0);
+                    }
                 }
             }
             oy += 16;
@@ -927,40 +939,20 @@ const EmAxis *em_axis_locked(int dev, double s, int n) {
 // (device, n, w, h, b, xs, ys) (the checks walk every column and row).
 struct EmPlan {
     bool ok;
-    int nk;
+    int nk, nu;
     EnlmArgs g;
     unsigned gen;
 };
-bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys, EnlmArgs *out, int *nk_out) {
-    if (!(xs >= 1.0) || !(ys >= 1.0) || n <= 0) return false;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    std::lock_guard<std::mutex> lk(g_em_mu);
-    static auto *plans = new std::map<std::tuple<int, int, int, int, int, double, double>, EmPlan>();
-    const unsigned gen = device_tables_generation();
-    const auto key = std::make_tuple(dev, n, w, h, b, xs, ys);
-    auto pit = plans->find(key);
-    if (pit != plans->end() && pit->second.gen == gen) {
-        *out = pit->second.g;
-        *nk_out = pit->second.nk;
-        return pit->second.ok;
-    }
-    if (plans->size() > 1024) plans->clear();
-    EmPlan pl{false, 0, EnlmArgs{}, gen};
-    const EmAxis *cx = em_axis_locked(dev, xs, ow);
-    const int4 *cols = cx ? cx->dev : nullptr;
-    const std::vector<int> xh = cx ? cx->host : std::vector<int>();
-    const EmAxis *cy = em_axis_locked(dev, ys, oh);
-    if (!cols || !cy) return false;
-    const int *px = xh.data(), *py = cy->host.data();
-    const int rowb = ow * b;
-    const int groups = (rowb + 63) / 64;
-    int nk = 1, kbmax = 0;
-    bool ok = true;
-    for (int gi = 0; gi < groups && ok; ++gi) {
-        const int x0b = 64 * gi;
+// the window of every group of 16 NU output bytes: unit K origins within 32 NK of their
+// taps; false when a unit needs NK > 2 or the window passes 128 bytes
+bool enlm_columns(const int *px, int b, int rowb, int nu, int *nk_out, int *iwb_out) {
+    const int groups = (rowb + 16 * nu - 1) / (16 * nu);
+    int ph = 0, nk = 1, kbmax = 0;
+    (void)ph;
+    for (int gi = 0; gi < groups; ++gi) {
+        const int x0b = 16 * nu * gi;
         const int ws = b * (px[kEmRec * (x0b / b)] - 2);
-        for (int u = 0; u < kEmNU; ++u) {
+        for (int u = 0; u < nu; ++u) {
             const int xf = std::min(x0b + 16 * u, rowb - 1) / b;
             const int kbu = (b * (px[kEmRec * xf] - 2) - ws) & ~7;
             int last = 0;
@@ -970,20 +962,60 @@ bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys,
                 last = std::max(last, b * (px[kEmRec * x] + 1) + (ob - b * x) - ws);
             }
             const int need = (last - kbu) / 32 + 1;
-            if (kbu < 0 || need > 2) {
-                ok = false;
-                break;
-            }
+            if (kbu < 0 || need > 2) return false;
             nk = std::max(nk, need);
             kbmax = std::max(kbmax, kbu);
         }
     }
     const int iwb = (kbmax + 32 * nk + 15) & ~15;
-    ok = ok && iwb <= 128;
+    if (iwb > 128) return false;
+    *nk_out = nk;
+    *iwb_out = iwb;
+    return true;
+}
+bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys, EnlmArgs *out, int *nk_out, int *nu_out) {
+    if (!(xs >= 1.0) || !(ys >= 1.0) || n <= 0) return false;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    std::lock_guard<std::mutex> lk(g_em_mu);
+    static auto *plans = new std::map<std::tuple<int, int, int, int, int, double, double, int>, EmPlan>();
+    const unsigned gen = device_tables_generation();
+    // MIPX_ENLM_NU=4 / 8 forces the group width (A/B); by default 8 for 1-3 bands where its
+    // window fits and the launch still has >= 5 rounds of resident waves at 4 per SIMD
+    // (20480 on 256 CUs; profiles/r05/enlm/nu_ab.jsonl: RGB 1080p x2 / x3 / x4 +9 / +11 / +16 %
+    // with ~24k waves; RGBA and 550x740 RGB x64 (~20k) lost 3-12 %)
+    const char *enu = tune_env("MIPX_ENLM_NU");
+    const int nu_force = enu && *enu ? std::atoi(enu) : 0;
+    const auto key = std::make_tuple(dev, n, w, h, b, xs, ys, nu_force);
+    auto pit = plans->find(key);
+    if (pit != plans->end() && pit->second.gen == gen) {
+        *out = pit->second.g;
+        *nk_out = pit->second.nk;
+        *nu_out = pit->second.nu;
+        return pit->second.ok;
+    }
+    if (plans->size() > 1024) plans->clear();
+    EmPlan pl{false, 0, 4, EnlmArgs{}, gen};
+    const EmAxis *cx = em_axis_locked(dev, xs, ow);
+    const int4 *cols = cx ? cx->dev : nullptr;
+    const std::vector<int> xh = cx ? cx->host : std::vector<int>();
+    const EmAxis *cy = em_axis_locked(dev, ys, oh);
+    if (!cols || !cy) return false;
+    const int *px = xh.data(), *py = cy->host.data();
+    const int rowb = ow * b;
+    int nk = 1, iwb = 0, nu = 8;
+    const long long waves8 = static_cast<long long>((rowb + 127) / 128) * ((oh + 127) / 128) * n;
+    const bool try8 = nu_force == 8 || (nu_force != 4 && b <= 3 && waves8 >= 20480);
+    bool ok = try8 && enlm_columns(px, b, rowb, 8, &nk, &iwb);
+    if (!ok && nu_force != 8) {
+        nu = 4;
+        ok = enlm_columns(px, b, rowb, 4, &nk, &iwb);
+    }
+    const int groups = (rowb + 16 * nu - 1) / (16 * nu);
     int rs = iwb;
     while ((rs / 16) % 2 == 0) rs += 16;
     // LDS per block for a band height (the kernel's layout); 5 blocks per CU need <= 32 KB
-    auto lds_of = [&](int c) { return kEmNU * nk * 2 * 1024 + 4 * (16 * rs + 16 * kEmOS + 16 * c); };
+    auto lds_of = [&](int c) { return nu * nk * 2 * 1024 + 4 * (16 * rs + 16 * em_os(nu) + 16 * c); };
     // band height: the multiple of 16 output rows whose input tiles are best used (input rows
     // needed / staged) times the share of a block's 4 waves that have a band, among those
     // that still give >= 8192 waves
@@ -995,7 +1027,7 @@ bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys,
         const double eff = rows / (16.0 * std::ceil((rows + 4.0) / 16.0)) * nb / (4.0 * ((nb + 3) / 4));
         const long long tasks = static_cast<long long>(groups) * nb * n;
         if (tasks < 8192 && c > 64) break;
-        if (lds_of(c) > 32 * 1024 && c > 64) break;
+        if (lds_of(c) > (nu == 4 ? 32 : 40) * 1024 && c > 64) break;
         if (eff > best + 1e-9) {
             best = eff;
             br = c;
@@ -1023,11 +1055,13 @@ bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys,
         pl.g.bquads = (bands + 3) / 4;
         pl.g.blocks = static_cast<long long>(groups) * pl.g.bquads * n;
         pl.nk = nk;
+        pl.nu = nu;
         pl.ok = true;
     }
     (*plans)[key] = pl;
     *out = pl.g;
     *nk_out = pl.nk;
+    *nu_out = pl.nu;
     return pl.ok;
 }
 
@@ -1057,18 +1091,19 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
     const char *em = tune_env("MIPX_ENLM");
     if (!(em && *em == '0') && a.out_img < 0x7fffffffLL) {
         EnlmArgs g{};
-        int nk = 0;
-        if (enlm_plan(n, w, h, b, a.ow, a.oh, xs, ys, &g, &nk)) {
+        int nk = 0, nu = 0;
+        if (enlm_plan(n, w, h, b, a.ow, a.oh, xs, ys, &g, &nk, &nu)) {
             g.in = in, g.out = out, g.w = w, g.h = h, g.ow = a.ow, g.oh = a.oh, g.extend = a.extend, g.fill = a.fill;
             g.in_img = a.in_img, g.out_img = a.out_img;
             if (grid_ok(g.blocks)) {
-                const size_t lds = static_cast<size_t>(kEmNU) * nk * 2 * 1024 + 4 * static_cast<size_t>(16 * g.rs + 16 * kEmOS + 16 * g.br);
+                const size_t lds = static_cast<size_t>(nu) * nk * 2 * 1024 + 4 * static_cast<size_t>(16 * g.rs + 16 * em_os(nu) + 16 * g.br);
                 const dim3 grid(static_cast<unsigned>(g.blocks));
-                if (nk == 1) {
-                    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_enlm<B_, 1>), grid, dim3(256), lds, st, g));
-                } else {
-                    MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_enlm<B_, 2>), grid, dim3(256), lds, st, g));
-                }
+#define MIPX_EM_K(NK_, NU_) MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_enlm<B_, NK_, NU_>), grid, dim3(256), lds, st, g))
+                if (nk == 1 && nu == 4) { MIPX_EM_K(1, 4); }
+                else if (nk == 1) { MIPX_EM_K(1, 8); }
+                else if (nu == 4) { MIPX_EM_K(2, 4); }
+                else { MIPX_EM_K(2, 8); }
+#undef MIPX_EM_K
                 return launch_check("k_enlm");
             }
         }
