@@ -671,16 +671,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
                 pq[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off & ~3, 0, 0));
                 pe[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
                 psh[j] = static_cast<uint32_t>(off & 3);
-            } else {  // a chunk across an image edge: per byte through the extend mode
+            } else {  // a chunk across an image edge: per byte through the extend mode, four
+                      // byte loads in flight per wait
                 uint32_t d[4] = {0u, 0u, 0u, 0u};
+                const u8 *rowp = a.in + img * a.in_img + static_cast<long long>(sr) * pitch;
+#pragma unroll 4
                 for (int e = 0; e < 16; ++e) {
                     const int ib = b0 + e;
                     const int col = ib >= 0 ? ib / B : -((-ib + B - 1) / B);
                     const int ch = ib - col * B;
                     const int sc = extend_idx(col, a.w, a.extend);
-                    const uint32_t byte = sc < 0 ? static_cast<uint32_t>(a.fill)
-                                                 : static_cast<uint32_t>(a.in[img * a.in_img + static_cast<long long>(sr) * pitch + sc * B + ch]);
-                    d[e >> 2] |= byte << (8 * (e & 3));
+                    const uint32_t byte = static_cast<uint32_t>(rowp[max(sc, 0) * B + ch]);
+                    d[e >> 2] |= (sc < 0 ? static_cast<uint32_t>(a.fill) : byte) << (8 * (e & 3));
                 }
                 pq[j] = rc_u4{d[0], d[1], d[2], d[3]};
             }
@@ -986,7 +988,8 @@ bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys,
     // with ~24k waves; RGBA and 550x740 RGB x64 (~20k) lost 3-12 %)
     const char *enu = tune_env("MIPX_ENLM_NU");
     const int nu_force = enu && *enu ? std::atoi(enu) : 0;
-    const auto key = std::make_tuple(dev, n, w, h, b, xs, ys, nu_force);
+    const char *ebr0 = tune_env("MIPX_ENLM_BR");
+    const auto key = std::make_tuple(dev, n, w, h, b, xs, ys, nu_force * 4096 + (ebr0 && *ebr0 ? std::atoi(ebr0) : 0));
     auto pit = plans->find(key);
     if (pit != plans->end() && pit->second.gen == gen) {
         *out = pit->second.g;
@@ -1033,6 +1036,8 @@ bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys,
             br = c;
         }
     }
+    const char *ebr = tune_env("MIPX_ENLM_BR");  // A/B: force the band height (a multiple of 16)
+    if (ebr && *ebr && std::atoi(ebr) >= 16) br = std::atoi(ebr) & ~15;
     const int bands = (oh + br - 1) / br;
     for (int band = 0; band < bands && ok; ++band) {
         const int ya = band * br, yb = std::min(ya + br, oh);
