@@ -562,6 +562,7 @@ struct EnlmArgs {
     int rs;                 // staged row stride (bytes, 16 x odd: conflict-free operand reads)
     int ncr;                // 16-byte chunks staged per row (<= 8)
     long long blocks;
+    int dbg;                // MIPX_ENLM_DBG (timing probes only, wrong pixels): 1 no staging loads, 2 no stores
 };
 
 // 8 bytes -> 8 f16 of value 1024 + p
@@ -666,6 +667,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
             if (sr < 0) {
                 const uint32_t f = 0x01010101u * static_cast<uint32_t>(a.fill);
                 pq[j] = rc_u4{f, f, f, f};
+            } else if (a.dbg & 1) {
+                // timing probe: no load
             } else if (b0 >= 0 && b0 + 16 <= pitch) {
                 const int off = sr * pitch + b0 + delta;
                 pq[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off & ~3, 0, 0));
@@ -788,7 +791,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
                 const int pc2 = (lane & 3) + 4 * i;
                 const rc_u4 v = *reinterpret_cast<const rc_u4 *>(otl + rr * kEmOS + 16 * pc2);
                 const int yy = oy + rr, bo = x0b + 16 * pc2;
-                if (yy <= yl && bo < rowb) {
+                if (yy <= yl && bo < rowb && !(a.dbg & 2)) {
                     const int off = yy * rowb + bo;
                     if (bo + 16 <= rowb) {
                         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, v), dst, off, 0, 0);
@@ -1100,6 +1103,8 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
         if (enlm_plan(n, w, h, b, a.ow, a.oh, xs, ys, &g, &nk, &nu)) {
             g.in = in, g.out = out, g.w = w, g.h = h, g.ow = a.ow, g.oh = a.oh, g.extend = a.extend, g.fill = a.fill;
             g.in_img = a.in_img, g.out_img = a.out_img;
+            const char *edb = tune_env("MIPX_ENLM_DBG");
+            g.dbg = edb && *edb ? std::atoi(edb) : 0;
             if (grid_ok(g.blocks)) {
                 const size_t lds = static_cast<size_t>(nu) * nk * 2 * 1024 + 4 * static_cast<size_t>(16 * g.rs + 16 * em_os(nu) + 16 * g.br);
                 const dim3 grid(static_cast<unsigned>(g.blocks));
