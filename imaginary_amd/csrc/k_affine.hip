@@ -559,7 +559,6 @@ struct EnlmArgs {
     long long in_img, out_img;
     int groups, bands, br;  // column groups of 64 output bytes; bands of br output rows
     int bquads;             // blocks per column group and image: (bands + 3) / 4
-    int gbase, gstep, gcount;  // this launch's column groups: gbase + gstep i, i < gcount
     int rs;                 // staged row stride (bytes, 16 x odd: conflict-free operand reads)
     int ncr;                // 16-byte chunks staged per row (<= 8)
     long long blocks;
@@ -588,8 +587,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
     // a block = one column group x 4 consecutive bands (wave w: band 4 q + w), so the
     // horizontal operands, which depend on the columns only, are built once per block
     const long long blk = xcd_remap(blockIdx.x, gridDim.x);  // neighbouring groups (shared halo) on one L2
-    const int grp = a.gbase + static_cast<int>(blk % a.gcount) * a.gstep;
-    const long long rest = blk / a.gcount;
+    const int grp = static_cast<int>(blk % a.groups);
+    const long long rest = blk / a.groups;
     const int band = 4 * static_cast<int>(rest % a.bquads) + wave;
     const int img = static_cast<int>(rest / a.bquads);
     u8 *opl = reinterpret_cast<u8 *>(ems);  // [unit][ks][hi, lo][64 lanes] x 16 bytes
@@ -708,6 +707,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
 #pragma unroll
     for (int u = 0; u < kEmNU; ++u) hh[u] = em_h8{0, 0, 0, 0, 0, 0, 0, 0};
     int oy = ya;  // the next 16 output rows
+    // row records of the lane's output row in the next two groups of 16 (clipped to the
+    // band), each loaded two groups before it is used
     // the band's row records into the wave's LDS once: read per 16 output rows from there
     // (a record in registers loaded ahead across the variable-length emission loop would
     // make the compiler wait for every load in flight, the staging ones included)
@@ -806,209 +807,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
             }
             oy += 16;
         }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_enlm_fx<B, NK, NU, E>: k_enlm for the interior column groups (no staged chunk crosses
-// an image edge, no ragged row end; the host launches k_enlm for the first and last
-// groups) with a fixed memory-instruction sequence per input tile: E output-tile slots
-// (a phantom slot stores out of range) and the staging loads of the tile two ahead issued
-// at the tile's end.  The compiler's vmcnt waits then count exactly, so the loads of the
-// next tile stay in flight while this one's are consumed (k_enlm's variable-length
-// emission loop made them wait for everything).  E >= the most 16-row output groups one
-// 16-row input tile can complete (host: 3 for vertical scales <= 2, 5 for <= 4).
-template <int B, int NK, int NU, int E>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 4 ? 5 : 3, 8))) k_enlm_fx(EnlmArgs a) {
-    constexpr int kEmNU = NU, kEmOS = em_os(NU), NCL = NU / 4;
-    extern __shared__ __attribute__((aligned(16))) uint32_t ems[];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int grp = a.gbase + static_cast<int>(blk % a.gcount) * a.gstep;
-    const long long rest = blk / a.gcount;
-    const int band = 4 * static_cast<int>(rest % a.bquads) + wave;
-    const int img = static_cast<int>(rest / a.bquads);
-    u8 *opl = reinterpret_cast<u8 *>(ems);
-    u8 *stg = opl + kEmNU * NK * 2 * 1024 + wave * (16 * a.rs + 16 * kEmOS + 16 * a.br);
-    u8 *otl = stg + 16 * a.rs;
-    int4 *rrec = reinterpret_cast<int4 *>(otl + 16 * kEmOS);
-    const int n = lane & 15, kg = lane >> 4;
-    const int rowb = a.ow * B, pitch = a.w * B;
-    const int x0b = 16 * NU * grp;
-    const int ws = B * (a.cols[2 * (x0b / B)].x - 2);
-
-    int kb[kEmNU];
-    float hseed[kEmNU];
-#pragma unroll
-    for (int u = 0; u < kEmNU; ++u) {
-        const int xf = min(x0b + 16 * u, rowb - 1) / B;
-        kb[u] = __builtin_amdgcn_readfirstlane((B * (a.cols[2 * xf].x - 2) - ws) & ~7);
-        const int ob = min(x0b + 16 * u + n, rowb - 1);
-        const int x = ob / B, c = ob - B * x;
-        const int4 cr = a.cols[2 * x];
-        hseed[u] = kEmMagic + 1.0f / 8192.0f - 0.25f * static_cast<float>(cr.y);
-        if ((u & 3) != wave) continue;
-        const int first = B * (cr.x - 2) + c - ws;
-#pragma unroll
-        for (int ks = 0; ks < NK; ++ks) {
-            em_h8 th, tl;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int e = kb[u] + 32 * ks + 8 * kg + j - first;
-                const int i = e / B;
-                const int T = (e >= 0 && e - B * i == 0) ? em_tap(cr, i) : 0;
-                th[j] = static_cast<_Float16>(static_cast<float>(T >> 6) * (1.0f / 64.0f));
-                tl[j] = static_cast<_Float16>(static_cast<float>(T & 63) * (1.0f / 4096.0f));
-            }
-            *reinterpret_cast<em_h8 *>(opl + ((u * NK + ks) * 2) * 1024 + 16 * lane) = th;
-            *reinterpret_cast<em_h8 *>(opl + ((u * NK + ks) * 2 + 1) * 1024 + 16 * lane) = tl;
-        }
-    }
-    __syncthreads();
-    if (band >= a.bands) return;
-
-    const int ya = band * a.br, yb = min(ya + a.br, a.oh);
-    const int ra = a.rows[2 * ya].x - 2, rb = a.rows[2 * (yb - 1)].x + 1;
-    const int ntile = (rb - ra + 16) >> 4;
-    int delta = 0;
-    const __amdgpu_buffer_rsrc_t src = image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &delta);
-    const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
-    int crow[NCL], ccol[NCL];
-#pragma unroll
-    for (int j = 0; j < NCL; ++j) {
-        const int q = lane + 64 * j;
-        crow[j] = q / a.ncr;
-        ccol[j] = q - crow[j] * a.ncr;
-    }
-    // two tiles of chunks in flight (raw 20 bytes + shift; shift 4 = a fill row)
-    rc_u4 pq[2][NCL];
-    uint32_t pe[2][NCL], psh[2][NCL];
-    auto load = [&](auto pc, int r0) {
-        constexpr int P = decltype(pc)::value;
-        const bool redge = r0 < 0 || r0 + 16 > a.h;
-#pragma unroll
-        for (int j = 0; j < NCL; ++j) {
-            int sr = r0 + crow[j];
-            if (redge) sr = extend_idx(sr, a.h, a.extend);
-            const bool live = crow[j] < 16 && sr >= 0;
-            const int off = live ? sr * pitch + ws + 16 * ccol[j] + delta : 0x7ffffff0;
-            // every tile issues the same two loads per chunk (out of range when idle)
-            pq[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off & ~3, 0, 0));
-            pe[P][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
-            psh[P][j] = sr < 0 ? 4u : static_cast<uint32_t>(off & 3);
-        }
-    };
-    auto put = [&](auto pc) {
-        constexpr int P = decltype(pc)::value;
-#pragma unroll
-        for (int j = 0; j < NCL; ++j)
-            if (crow[j] < 16) {
-                const rc_u4 p = pq[P][j];
-                const uint32_t sh = psh[P][j] & 3u, f = 0x01010101u * static_cast<uint32_t>(a.fill);
-                rc_u4 v = rc_u4{__builtin_amdgcn_alignbyte(p.y, p.x, sh), __builtin_amdgcn_alignbyte(p.z, p.y, sh),
-                                __builtin_amdgcn_alignbyte(p.w, p.z, sh), __builtin_amdgcn_alignbyte(pe[P][j], p.w, sh)};
-                if (psh[P][j] == 4u) v = rc_u4{f, f, f, f};
-                *reinterpret_cast<rc_u4 *>(stg + crow[j] * a.rs + 16 * ccol[j]) = v;
-            }
-    };
-
-    em_h8 hh[kEmNU];
-#pragma unroll
-    for (int u = 0; u < kEmNU; ++u) hh[u] = em_h8{0, 0, 0, 0, 0, 0, 0, 0};
-    int oy = ya;
-    for (int i = lane; i < yb - ya; i += 64) rrec[i] = a.rows[2 * (ya + i) + 1];
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    load(I0{}, ra);
-    load(I1{}, ra + 16);
-    auto tile = [&](auto pc, int t) {
-        const int r0 = ra + 16 * t;
-        put(pc);
-#pragma unroll
-        for (int u = 0; u < kEmNU; ++u) {
-            em_f4 d = em_f4{hseed[u], hseed[u], hseed[u], hseed[u]};
-#pragma unroll
-            for (int ks = 0; ks < NK; ++ks) {
-                const uint2 v = *reinterpret_cast<const uint2 *>(stg + n * a.rs + kb[u] + 32 * ks + 8 * kg);
-                const em_h8 th = *reinterpret_cast<const em_h8 *>(opl + ((u * NK + ks) * 2) * 1024 + 16 * lane);
-                const em_h8 tl = *reinterpret_cast<const em_h8 *>(opl + ((u * NK + ks) * 2 + 1) * 1024 + 16 * lane);
-                const em_h8 av = em_cvt8(v.x, v.y);
-                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, th, d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, tl, d, 0, 0, 0);
-            }
-            hh[u] = em_h8{hh[u][4], hh[u][5], hh[u][6], hh[u][7], static_cast<_Float16>(d[0]), static_cast<_Float16>(d[1]),
-                          static_cast<_Float16>(d[2]), static_cast<_Float16>(d[3])};
-        }
-        // E output slots: the groups of 16 rows whose last H row is in this tile, then
-        // phantoms (no compute, stores out of range)
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const int yl = min(oy + 15, yb - 1);
-            const int4 c0 = rrec[max(min(oy + n, yl) - ya, 0)];
-            const bool live = oy < yb && __builtin_amdgcn_readlane(c0.x, 15) + 1 <= r0 + 15;
-            rc_u4 v[NU / 4];
-#pragma unroll
-            for (int i = 0; i < NU / 4; ++i) v[i] = rc_u4{0u, 0u, 0u, 0u};
-            const int rr = lane >> 2;
-            if (live) {
-                typedef _Float16 em_h2 __attribute__((ext_vector_type(2)));
-                const uint32_t k64 = 0x64646464u;
-                auto cvt2 = [&](uint32_t w, uint32_t sel, float sc, float off) {
-                    const em_h2 x = __builtin_bit_cast(em_h2, __builtin_amdgcn_perm(k64, w, sel));
-                    const em_h2 r = x * em_h2{static_cast<_Float16>(sc), static_cast<_Float16>(sc)} +
-                                    em_h2{static_cast<_Float16>(off), static_cast<_Float16>(off)};
-                    return __builtin_bit_cast(uint32_t, r);
-                };
-                const uint32_t uh = static_cast<uint32_t>(c0.z), ul = static_cast<uint32_t>(c0.w);
-                const uint64_t th64 = (static_cast<uint64_t>(cvt2(uh, 0x04030402u, 1.0f / 64.0f, -17.0f)) << 32) |
-                                      cvt2(uh, 0x04010400u, 1.0f / 64.0f, -17.0f);
-                const uint64_t tl64 = (static_cast<uint64_t>(cvt2(ul, 0x04030402u, 1.0f / 4096.0f, -0.25f)) << 32) |
-                                      cvt2(ul, 0x04010400u, 1.0f / 4096.0f, -0.25f);
-                const int s = c0.x - 2 - (r0 + 4 * kg);
-                auto place = [](uint64_t w, int sh) -> uint64_t {
-                    const uint32_t l = static_cast<uint32_t>(min(max(16 * sh, 0), 48)), r = static_cast<uint32_t>(min(max(-16 * sh, 0), 48));
-                    const uint64_t keep = (sh > -4 && sh < 4) ? ~0ull : 0ull;
-                    return ((w << l) >> r) & keep;
-                };
-                const uint64_t hc = place(th64, s), lc = place(tl64, s), hp = place(th64, s + 16), lp = place(tl64, s + 16);
-                const em_h8 bh = __builtin_bit_cast(em_h8, rc_u4{static_cast<uint32_t>(hp), static_cast<uint32_t>(hp >> 32),
-                                                                 static_cast<uint32_t>(hc), static_cast<uint32_t>(hc >> 32)});
-                const em_h8 bl = __builtin_bit_cast(em_h8, rc_u4{static_cast<uint32_t>(lp), static_cast<uint32_t>(lp >> 32),
-                                                                 static_cast<uint32_t>(lc), static_cast<uint32_t>(lc >> 32)});
-                const float vseed = 1.0f / 8192.0f - kEmMagic / 4096.0f * static_cast<float>(c0.y);
-#pragma unroll
-                for (int u = 0; u < kEmNU; ++u) {
-                    em_f4 d = em_f4{vseed, vseed, vseed, vseed};
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(hh[u], bh, d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(hh[u], bl, d, 0, 0, 0);
-                    uint32_t q = __builtin_amdgcn_cvt_pk_u8_f32(d[0], 0, 0u);
-                    q = __builtin_amdgcn_cvt_pk_u8_f32(d[1], 1, q);
-                    q = __builtin_amdgcn_cvt_pk_u8_f32(d[2], 2, q);
-                    q = __builtin_amdgcn_cvt_pk_u8_f32(d[3], 3, q);
-                    *reinterpret_cast<uint32_t *>(otl + n * kEmOS + 16 * u + 4 * kg) = q;
-                }
-#pragma unroll
-                for (int i = 0; i < NU / 4; ++i) v[i] = *reinterpret_cast<const rc_u4 *>(otl + rr * kEmOS + 16 * ((lane & 3) + 4 * i));
-            }
-            // every slot issues the same stores (interior groups: whole 16-byte pieces)
-#pragma unroll
-            for (int i = 0; i < NU / 4; ++i) {
-                const int yy = oy + rr, bo = x0b + 16 * ((lane & 3) + 4 * i);
-                const int off = live && yy <= yl && !(a.dbg & 2) ? yy * rowb + bo : 0x7ffffff0;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, v[i]), dst, off, 0, 0);
-            }
-            if (live) oy += 16;
-        }
-    };
-    // pairs of tiles with no branch around a memory instruction (an odd last tile is
-    // followed by a phantom one: every output group is emitted by then, so it stores
-    // nothing; loads past the band read rows never consumed)
-    for (int t = 0; t < ntile; t += 2) {
-        tile(I0{}, t);
-        load(I0{}, ra + 16 * (t + 2));
-        tile(I1{}, t + 1);
-        load(I1{}, ra + 16 * (t + 3));
     }
 }
 
@@ -1147,7 +945,6 @@ const EmAxis *em_axis_locked(int dev, double s, int n) {
 struct EmPlan {
     bool ok;
     int nk, nu;
-    int fx_e, glo, ghi;  // k_enlm_fx: E (0: not used) and its interior groups [glo, ghi]
     EnlmArgs g;
     unsigned gen;
 };
@@ -1181,8 +978,7 @@ bool enlm_columns(const int *px, int b, int rowb, int nu, int *nk_out, int *iwb_
     *iwb_out = iwb;
     return true;
 }
-bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys, EnlmArgs *out, int *nk_out, int *nu_out,
-               int *fx_e, int *glo, int *ghi) {
+bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys, EnlmArgs *out, int *nk_out, int *nu_out) {
     if (!(xs >= 1.0) || !(ys >= 1.0) || n <= 0) return false;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
@@ -1196,22 +992,16 @@ bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys,
     const char *enu = tune_env("MIPX_ENLM_NU");
     const int nu_force = enu && *enu ? std::atoi(enu) : 0;
     const char *ebr0 = tune_env("MIPX_ENLM_BR");
-    const char *efx = tune_env("MIPX_ENLM_FX");  // 0: every group on k_enlm (A/B)
-    const bool fx_on = !(efx && *efx == '0');
-    const auto key = std::make_tuple(dev, n, w, h, b, xs, ys,
-                                     (fx_on ? 1 : 0) + 2 * nu_force + 4096 * (ebr0 && *ebr0 ? std::atoi(ebr0) : 0));
+    const auto key = std::make_tuple(dev, n, w, h, b, xs, ys, nu_force * 4096 + (ebr0 && *ebr0 ? std::atoi(ebr0) : 0));
     auto pit = plans->find(key);
     if (pit != plans->end() && pit->second.gen == gen) {
         *out = pit->second.g;
         *nk_out = pit->second.nk;
         *nu_out = pit->second.nu;
-        *fx_e = pit->second.fx_e;
-        *glo = pit->second.glo;
-        *ghi = pit->second.ghi;
         return pit->second.ok;
     }
     if (plans->size() > 1024) plans->clear();
-    EmPlan pl{false, 0, 4, 0, 0, -1, EnlmArgs{}, gen};
+    EmPlan pl{false, 0, 4, EnlmArgs{}, gen};
     const EmAxis *cx = em_axis_locked(dev, xs, ow);
     const int4 *cols = cx ? cx->dev : nullptr;
     const std::vector<int> xh = cx ? cx->host : std::vector<int>();
@@ -1275,37 +1065,11 @@ bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys,
         pl.nk = nk;
         pl.nu = nu;
         pl.ok = true;
-        // k_enlm_fx for the interior groups: every staged chunk inside its row, whole 16-byte
-        // output pieces, a tile's chunks on one register set per lane, vertical scale <= 4;
-        // they must be contiguous (the edge groups, on k_enlm, at the two ends)
-        const int e = ys <= 2.0 ? 3 : ys <= 4.0 ? 5 : 0;
-        if (fx_on && e && 16 * pl.g.ncr <= 64 * (nu / 4)) {
-            int lo = -1, hi = -1;
-            bool contiguous = true;
-            for (int gi = 0; gi < groups; ++gi) {
-                const int x0b = 16 * nu * gi;
-                const int ws = b * (px[kEmRec * (x0b / b)] - 2);
-                const bool in = ws >= 0 && ws + 16 * pl.g.ncr <= w * b && x0b + 16 * nu <= rowb;
-                if (in) {
-                    if (lo < 0) lo = gi;
-                    else if (hi != gi - 1) contiguous = false;
-                    hi = gi;
-                }
-            }
-            if (lo >= 0 && contiguous) {
-                pl.fx_e = e;
-                pl.glo = lo;
-                pl.ghi = hi;
-            }
-        }
     }
     (*plans)[key] = pl;
     *out = pl.g;
     *nk_out = pl.nk;
     *nu_out = pl.nu;
-    *fx_e = pl.fx_e;
-    *glo = pl.glo;
-    *ghi = pl.ghi;
     return pl.ok;
 }
 
@@ -1335,48 +1099,23 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
     const char *em = tune_env("MIPX_ENLM");
     if (!(em && *em == '0') && a.out_img < 0x7fffffffLL) {
         EnlmArgs g{};
-        int nk = 0, nu = 0, fx_e = 0, glo = 0, ghi = -1;
-        if (enlm_plan(n, w, h, b, a.ow, a.oh, xs, ys, &g, &nk, &nu, &fx_e, &glo, &ghi)) {
+        int nk = 0, nu = 0;
+        if (enlm_plan(n, w, h, b, a.ow, a.oh, xs, ys, &g, &nk, &nu)) {
             g.in = in, g.out = out, g.w = w, g.h = h, g.ow = a.ow, g.oh = a.oh, g.extend = a.extend, g.fill = a.fill;
             g.in_img = a.in_img, g.out_img = a.out_img;
             const char *edb = tune_env("MIPX_ENLM_DBG");
             g.dbg = edb && *edb ? std::atoi(edb) : 0;
-            const size_t lds = static_cast<size_t>(nu) * nk * 2 * 1024 + 4 * static_cast<size_t>(16 * g.rs + 16 * em_os(nu) + 16 * g.br);
-            // one launch per contiguous run of groups: [0, glo) and (ghi, groups) on k_enlm,
-            // [glo, ghi] on k_enlm_fx (without it, all on k_enlm)
-            auto launch = [&](int g0, int gn, bool fx) -> int {
-                if (gn <= 0) return MIPX_OK;
-                EnlmArgs q = g;
-                q.gbase = g0, q.gstep = 1, q.gcount = gn;
-                const long long blocks = static_cast<long long>(gn) * q.bquads * n;
-                if (!grid_ok(blocks)) return MIPX_EINVAL;
-                const dim3 grid(static_cast<unsigned>(blocks));
-#define MIPX_EM_K(NK_, NU_) MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_enlm<B_, NK_, NU_>), grid, dim3(256), lds, st, q))
-#define MIPX_EM_F(NK_, NU_, E_) MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_enlm_fx<B_, NK_, NU_, E_>), grid, dim3(256), lds, st, q))
-#define MIPX_EM_FE(NK_, NU_) if (fx_e == 3) { MIPX_EM_F(NK_, NU_, 3); } else { MIPX_EM_F(NK_, NU_, 5); }
-                if (!fx) {
-                    if (nk == 1 && nu == 4) { MIPX_EM_K(1, 4); }
-                    else if (nk == 1) { MIPX_EM_K(1, 8); }
-                    else if (nu == 4) { MIPX_EM_K(2, 4); }
-                    else { MIPX_EM_K(2, 8); }
-                } else {
-                    if (nk == 1 && nu == 4) { MIPX_EM_FE(1, 4) }
-                    else if (nk == 1) { MIPX_EM_FE(1, 8) }
-                    else if (nu == 4) { MIPX_EM_FE(2, 4) }
-                    else { MIPX_EM_FE(2, 8) }
-                }
-#undef MIPX_EM_FE
-#undef MIPX_EM_F
+            if (grid_ok(g.blocks)) {
+                const size_t lds = static_cast<size_t>(nu) * nk * 2 * 1024 + 4 * static_cast<size_t>(16 * g.rs + 16 * em_os(nu) + 16 * g.br);
+                const dim3 grid(static_cast<unsigned>(g.blocks));
+#define MIPX_EM_K(NK_, NU_) MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL((k_enlm<B_, NK_, NU_>), grid, dim3(256), lds, st, g))
+                if (nk == 1 && nu == 4) { MIPX_EM_K(1, 4); }
+                else if (nk == 1) { MIPX_EM_K(1, 8); }
+                else if (nu == 4) { MIPX_EM_K(2, 4); }
+                else { MIPX_EM_K(2, 8); }
 #undef MIPX_EM_K
                 return launch_check("k_enlm");
-            };
-            int rc;
-            if (fx_e) {
-                if ((rc = launch(glo, ghi - glo + 1, true)) != MIPX_OK) return rc;
-                if ((rc = launch(0, glo, false)) != MIPX_OK) return rc;
-                return launch(ghi + 1, g.groups - ghi - 1, false);
             }
-            return launch(0, g.groups, false);
         }
         if (em && *em == '2') return MIPX_EUNSUPPORTED;  // tests: k_enlm or an error
     }

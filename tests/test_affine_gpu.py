@@ -80,13 +80,9 @@ ENLM_SHAPES = [(740, 550, 3, 1), (33, 1201, 4, 0), (97, 203, 1, 2), (61, 130, 2,
                (1151, 1150, 3, 1)]
 
 
-@pytest.mark.parametrize("fx", ["1", "0"])
 @pytest.mark.parametrize("xs,ys", ENLM_SCALES, ids=[f"{x}x{y}" for x, y in ENLM_SCALES])
-def test_enlm_matches_oracle(gpu, oracle, rng, monkeypatch, xs, ys, fx):
-    """fx 1 (default): interior column groups on k_enlm_fx (fixed memory schedule), the
-    edge groups on k_enlm; fx 0: every group on k_enlm."""
+def test_enlm_matches_oracle(gpu, oracle, rng, monkeypatch, xs, ys):
     monkeypatch.setenv("MIPX_ENLM", "2")  # k_enlm or an error, never a fallback
-    monkeypatch.setenv("MIPX_ENLM_FX", fx)
     for h, w, b, extend in ENLM_SHAPES:
         if h * w * xs * ys > 3e6:
             continue
