@@ -42,8 +42,17 @@ def main():
             plans.append(bc.plan_for(opts, w, h, 4))
             w, h = plans[-1].out_w, plans[-1].out_h
         groups = [bc.Group(ia.plan_chain(plans), 512, dev, 3)]
+        runner = lambda: [g.run(sp) for g in groups]
+    elif a.config == "C5":
+        # bench_configs.c5 at one rank: 512 requests in their plan groups, 4 streams
+        shard = bc.workloads.shard_groups(bc.workloads.c5_groups(bc.c5_requests(512)), 1, bc.c5_request_bytes)[0]
+        gl = []
+        for (w, h), opts, cnt in shard:
+            gl.append((bc.Group(bc.plan_for(opts, w, h, 3), cnt, dev, 5 + len(gl)), opts))
+        groups = [g for g, _ in gl]
+        runner, _ = bc.stream_runner(gl, 4, dev, sp, stream)
     else:
-        raise SystemExit("only C3 for now")
+        raise SystemExit("C3 or C5")
     alg = sum(g.in_bytes + g.out_bytes for g in groups)
     knob, vals = a.ab.split("=", 1)
     first = None
@@ -51,7 +60,7 @@ def main():
         for v in vals.split(","):
             os.environ[knob] = v
             lib.mipx_tuning_reload()
-            run_all = lambda: [g.run(sp) for g in groups]
+            run_all = runner
             wall, dev_ms = bc.time_groups(run_all, a.steps, 2, stream)
             same = None
             if rnd == 0:
