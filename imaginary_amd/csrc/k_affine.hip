@@ -562,7 +562,7 @@ struct EnlmArgs {
     int rs;                 // staged row stride (bytes, 16 x odd: conflict-free operand reads)
     int ncr;                // 16-byte chunks staged per row (<= 8)
     long long blocks;
-    int dbg;                // MIPX_ENLM_DBG (timing probes only, wrong pixels): 1 no staging loads, 2 no stores
+    int dbg;                // MIPX_ENLM_DBG (timing probes only, wrong pixels): 1 no staging loads, 2 no stores, 4 no realignment dwords
 };
 
 // 8 bytes -> 8 f16 of value 1024 + p
@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
             } else if (b0 >= 0 && b0 + 16 <= pitch) {
                 const int off = sr * pitch + b0 + delta;
                 pq[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off & ~3, 0, 0));
-                pe[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
+                if (!(a.dbg & 4)) pe[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
                 psh[j] = static_cast<uint32_t>(off & 3);
             } else {  // a chunk across an image edge: per byte through the extend mode, four
                       // byte loads in flight per wait

@@ -88,6 +88,8 @@ struct R2mArgs {
     long long in_img, out_img;
     int seed;               // 128 sum(T) + 2048
     const rc_u4 *ops;       // [64 lanes][bh, bl, wh, wl]: the MFMA tap operands (r2m_operands)
+    int alt;                // odd bands walk up (their edge rows meet the neighbours' in L2)
+    int pp;                 // prime: both row batches in flight together
 };
 
 template <int B>
@@ -114,6 +116,12 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     const int pitch = a.w * B;
     const int ka = a.k_base + band * a.band_steps;
     const int kb = min(ka + a.band_steps, (a.y_end + kMN - 1) / kMN);
+    // a band's first step stages 10 rows its neighbour above also reads; walking odd bands
+    // bottom-up puts both reads of every shared row at about the same time (the bands of a
+    // strip are co-resident on one XCD), so the second comes from L2
+    const bool rev = a.alt && (band & 1);
+    const int kf = rev ? kb - 1 : ka, dk = rev ? -1 : 1, nst = kb - ka;
+    auto new_rows = [&](int k) { return rev ? 32 * k - 37 : 32 * k + 37; };  // first row step k + dk adds
     const __amdgpu_buffer_rsrc_t src = image_rsrc(a.in + img * a.in_img, a.in_img);
     u8 *dst = a.out + img * a.out_img;
 
@@ -153,16 +161,22 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     const bool row_al16 = ((a.ow * B) & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15u) == 0;
 
     // ---- prime: the first step's 42 rows, then the next step's 32 into registers ----
+    rc_u4 pf[KM];
     {
-        const int bk = 32 * ka - 5;
+        const int bk = 32 * kf - 5;
         rc_u4 v[KM];
         load(v, bk, 32);
-        store_ring(v, bk, 32);
-        load(v, bk + 32, 10);
-        store_ring(v, bk + 32, 10);
+        if (a.pp) {  // the 10 rows in the prefetch registers, in flight with the 32
+            load(pf, bk + 32, 10);
+            store_ring(v, bk, 32);
+            store_ring(pf, bk + 32, 10);
+        } else {
+            store_ring(v, bk, 32);
+            load(v, bk + 32, 10);
+            store_ring(v, bk + 32, 10);
+        }
     }
-    rc_u4 pf[KM];
-    load(pf, 32 * ka + 37, 32);  // rows 2 (16 (ka + 1)) + 6 .. : step ka + 1's new rows
+    load(pf, new_rows(kf), 32);  // step kf + dk's new rows
 
     // edge geometry
     const int x_last = min(x0 + kMTW, a.ow) - 1;
@@ -173,7 +187,8 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     const bool edge = nl > 0 || nr > 0;
     const int ib0 = G::OFF + G::ISH;                         // intermediate byte of strip pixel 0
 
-    for (int k = ka; k < kb; ++k) {
+    for (int s = 0; s < nst; ++s) {
+        const int k = kf + dk * s;
         const int bk = 32 * k - 5;
         rc_barrier();  // ring rows of step k staged; the intermediate free
         // ---- vertical: 16-byte column tiles dealt to the waves ----
@@ -220,9 +235,9 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
             }
         }
         rc_barrier();  // the intermediate complete; the ring's rows of step k read
-        if (k + 1 < kb) {
-            store_ring(pf, 32 * k + 37, 32);
-            if (k + 2 < kb) load(pf, 32 * k + 69, 32);
+        if (s + 1 < nst) {
+            store_ring(pf, new_rows(k), 32);
+            if (s + 2 < nst) load(pf, new_rows(k + dk), 32);
         }
         if (edge) {  // EXTEND_COPY: strip pixels outside the image copy the edge pixel
             const int nfill = nl + nr;
@@ -594,6 +609,10 @@ int reduce2m_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
     // MIPX_R2M_BAND overrides (A/B)
     const char *eb = tune_env("MIPX_R2M_BAND");
     a.band_steps = std::max(1, std::min(steps, (eb && *eb) ? std::atoi(eb) : (b == 3 ? 8 : 16)));
+    const char *ea = tune_env("MIPX_R2M_ALT");  // A/B: 0 = every band walks down
+    a.alt = !(ea && *ea == '0');
+    const char *epp = tune_env("MIPX_R2M_PP");  // A/B: 0 = the prime's two row batches one after the other
+    a.pp = !(epp && *epp == '0');
     a.n_bands = (steps + a.band_steps - 1) / a.band_steps;
     const long long blocks = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
