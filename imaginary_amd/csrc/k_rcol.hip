@@ -78,6 +78,7 @@ struct RcArgs {
     int centre;               // centre sampling convention (mipx_set_reduce_sampling)
     int wst;                  // each wave's 16 rows x 16 UPW bytes go out as 16-byte row pieces
     int swz;                  // horizontal reads: odd K blocks read their second 8 bytes first
+    int k4;                   // K origins 4-byte aligned (ds_read2_b32): one K step where 8-byte origins need two
 };
 
 // libvips reduce position (reducev.cpp / reduceh.cpp): X = reduce_x (o * shrink, or
@@ -185,7 +186,8 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         const int u = a.wst ? UPW * wave + i : wave + WV * i;
         int sf, pf;
         rc_pos(a.ox0 + min(x0 + (16 * u) / B, x_last), a.hs, a.hpad, &sf, &pf, a.centre);
-        kb[i] = __builtin_amdgcn_readfirstlane((B * (sf - org) + (16 * u) % B) & ~7);  // K origin (8-byte aligned)
+        // K origin: 8-byte aligned (ds_read_b64), 4-byte with k4
+        kb[i] = __builtin_amdgcn_readfirstlane((B * (sf - org) + (16 * u) % B) & (a.k4 ? ~3 : ~7));
         const int o = 16 * u + n, xl = o / B, c = o - B * xl;
         int sp, pp;
         rc_pos(a.ox0 + min(x0 + xl, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
@@ -376,8 +378,13 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
                 // two ds_read_b64 (2 LDS cycles each) rather than one ds_read2_b64 (16): -0.3 to -2 %
                 // (profiles/r04/small/rcol_rd64_ab.jsonl); lanes of odd K blocks read their
                 // second half first (hsw), so each read's 32-lane half covers all 64 banks
-                q[i][ks].lo = lds_rd64(ir + 64 * ks);
-                q[i][ks].hi = lds_rd64(ir + 64 * ks + hsd);
+                if (a.k4) {
+                    q[i][ks].lo = lds_rd2x32(ir + 64 * ks);
+                    q[i][ks].hi = lds_rd2x32(ir + 64 * ks + hsd);
+                } else {
+                    q[i][ks].lo = lds_rd64(ir + 64 * ks);
+                    q[i][ks].hi = lds_rd64(ir + 64 * ks + hsd);
+                }
             }
         }
 #pragma unroll
@@ -975,8 +982,10 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     }
     if (lmax > 64) return MIPX_EUNSUPPORTED;  // the MFMA K
 
-    // strip geometry: staged chunks per row, K steps of the horizontal units
-    int cpr_min = 1 << 30, cpr_max = 0, nks = 0, kbmax = 0;
+    // strip geometry: staged chunks per row, K steps of the horizontal units (8-byte K
+    // origins, and 4-byte ones: k4 when that saves a K step, e.g. RGB / 1.667, C5's
+    // 1333x1000 -> 800x600; MIPX_RCOL_K4=0 keeps 8, A/B)
+    int cpr_min = 1 << 30, cpr_max = 0, nks = 0, kbmax = 0, nks4 = 0, kbmax4 = 0;
     for (int x0 = 0; x0 < ow; x0 += 64) {
         const int xl = std::min(x0 + 63, ow - 1);
         const int lo = rc_start(ox0 + x0, hs, a.hpad, centre), hi = rc_start(ox0 + xl, hs, a.hpad, centre) + htaps - 1;
@@ -988,11 +997,20 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
             const int o0 = 16 * u, o1 = 16 * u + 15;
             if (x0 + o0 / b > xl) break;
             const int xf = x0 + o0 / b, xe = std::min(x0 + o1 / b, xl);
-            const int kbu = (b * (rc_start(ox0 + xf, hs, a.hpad, centre) - org) + o0 % b) & ~7;
+            const int kb0 = b * (rc_start(ox0 + xf, hs, a.hpad, centre) - org) + o0 % b;
+            const int kbu = kb0 & ~7, kbu4 = kb0 & ~3;
             const int need = b * (rc_start(ox0 + xe, hs, a.hpad, centre) + htaps - 1 - org) + b;
             nks = std::max(nks, (need - kbu + 63) / 64);
             kbmax = std::max(kbmax, kbu);
+            nks4 = std::max(nks4, (need - kbu4 + 63) / 64);
+            kbmax4 = std::max(kbmax4, kbu4);
         }
+    }
+    const char *ek4 = tune_env("MIPX_RCOL_K4");
+    a.k4 = nks4 < nks && !(ek4 && *ek4 == '0');
+    if (a.k4) {
+        nks = nks4;
+        kbmax = kbmax4;
     }
     if (nks > 2) return MIPX_EUNSUPPORTED;
     // chunks per lane: the widest strip's rows of the largest step fit one batch; ring:

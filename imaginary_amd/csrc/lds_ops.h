@@ -57,6 +57,12 @@ __device__ __forceinline__ rc_u2 lds_rd64(uint32_t a) {
     asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
     return v;
 }
+// two dwords from a 4-byte aligned address (ds_read_b64 needs 8)
+__device__ __forceinline__ rc_u2 lds_rd2x32(uint32_t a) {
+    rc_u2 v;
+    asm volatile("ds_read2_b32 %0, %1 offset1:1" : "=v"(v) : "v"(a));
+    return v;
+}
 __device__ __forceinline__ rc_u4 rc_join(const rc_u2x2 &v) { return rc_u4{v.lo.x, v.lo.y, v.hi.x, v.hi.y}; }
 __device__ __forceinline__ rc_u4 lds_rd128(uint32_t a) {
     rc_u4 v;

@@ -1,0 +1,25 @@
+#!/bin/bash
+# k_rcol with 4-byte K origins where that saves a K step (MIPX_RCOL_K4): reduce parity,
+# same-process A/B on the survey reduce shapes and C5
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
+O="$R/gpurun_out/${OUT:-r05k4}"; mkdir -p "$O"
+run() { local lim=$1; shift; timeout -k 10 "$lim" "$@"; local rc=$?; [ $rc -eq 0 ] || { echo "step failed rc=$rc: $*"; exit $rc; }; }
+run 500 python3 -u -m pytest tests/test_rcol_gpu.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/pytest_rcol.log" 2>&1
+tail -2 "$O/pytest_rcol.log"
+run 500 python3 -u -m pytest tests/test_parity_gpu.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread -k "reduce" > "$O/pytest_reduce.log" 2>&1
+tail -2 "$O/pytest_reduce.log"
+: > "$O/k4_ab.jsonl"
+for args in "--w 1333 --h 1000 --b 3 --n 48 --s 1.6666666666666667" "--w 500 --h 375 --b 3 --n 128 --s 1.465" "--w 480 --h 270 --b 3 --n 256 --s 1.6" \
+            "--w 1920 --h 1080 --b 3 --n 64 --s 1.6" "--w 1920 --h 1080 --b 3 --n 64 --s 2.4" "--w 1024 --h 1024 --b 4 --n 512 --s 1.333" \
+            "--w 1000 --h 750 --b 3 --n 64 --s 1.5625" "--w 1920 --h 1080 --b 4 --n 32 --s 1.6"; do
+  run 150 python3 scripts/op_bench.py reduce $args --iters 20 --ab MIPX_RCOL_K4=0,1 >> "$O/k4_ab.jsonl"
+done
+python3 - "$O/k4_ab.jsonl" <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    d = json.loads(l)
+    print(d["w"], d["h"], d["b"], round(d["s"], 3), "k4", d["MIPX_RCOL_K4"], "r", d["round"], d["ms"], round(d["alg_GBps"] / 8000, 3), d["same_as_first"])
+PY
+run 300 python3 scripts/cfg_ab.py --config C5 --ab MIPX_RCOL_K4=0,1 --rounds 2 > "$O/c5_k4_ab.jsonl"
+cut -c1-200 "$O/c5_k4_ab.jsonl"

@@ -4,7 +4,8 @@ folded into the horizontal operands), images narrower than a strip and shorter t
 a step, segment boundaries in tall images, RGB and RGBA, shrink pairs across
 (1, 2.75), windows (reduce -> extract), unaligned output rows (byte stores) and a
 seeded fuzz over shapes.  RGB input rows off a dword (r05) run k_rcol's realigning
-build (MIPX_RCOL_UNAL=0 leaves them to k_rmf2, as the norcol route does)."""
+build (MIPX_RCOL_UNAL=0 leaves them to k_rmf2, as the norcol route does); horizontal K
+origins on 4 bytes where that saves a K step (r05, MIPX_RCOL_K4=0: 8 bytes)."""
 import numpy as np
 import pytest
 
@@ -70,6 +71,19 @@ def test_rcol_fuzz(gpu, oracle):
         got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
         for i in range(n):
             assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"fuzz {case}: {h}x{w}x{b} {hs}x{vs} img{i}")
+
+
+@pytest.mark.parametrize("k4", ["0", "1"])
+def test_rcol_k_origins(gpu, oracle, rng, monkeypatch, k4):
+    """4-byte K origins (ds_read2_b32; the default where they save a K step, e.g. RGB /
+    1.667, C5's 1333x1000 -> 800x600) and the 8-byte ones (MIPX_RCOL_K4=0)."""
+    monkeypatch.setenv("MIPX_RCOL_K4", k4)
+    for h, w, b, hs, vs in ((101, 1333, 3, 1.6666666666666667, 1.6666666666666667), (64, 1332, 3, 1.6666666666666667, 1.6),
+                            (37, 700, 4, 1.7, 1.7), (50, 901, 3, 1.8, 1.25), (20, 96, 3, 1.66, 2.2), (33, 640, 4, 1.9, 1.9)):
+        imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+        got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+        for i in range(2):
+            assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"k4={k4} {h}x{w}x{b} {hs}x{vs} img{i}")
 
 
 @pytest.mark.parametrize("probe", ["ok", "fail"])
