@@ -79,6 +79,7 @@ struct RcArgs {
     int wst;                  // each wave's 16 rows x 16 UPW bytes go out as 16-byte row pieces
     int swz;                  // horizontal reads: odd K blocks read their second 8 bytes first
     int k4;                   // K origins 4-byte aligned (ds_read2_b32): one K step where 8-byte origins need two
+    int allst;                // A/B: every strip issues the edge-piece dword stores (r05 before)
 };
 
 // libvips reduce position (reducev.cpp / reduceh.cpp): X = reduce_x (o * shrink, or
@@ -309,7 +310,10 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
             const int base = o * a.ow * B + B * x0 + we;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, q), dst,
                                                    ok && we + 16 <= vbytes ? base : 0x7ffffff0, 0, 0);
-            if (a.wst == 2) {  // rows whose byte count is not a multiple of 16: the piece at the image edge in dwords
+            if (a.wst == 2 && (vbytes < 16 * UPW * WV || a.allst)) {
+                // rows whose byte count is not a multiple of 16: the piece at the image edge in
+                // dwords, in the last strip only (uniform: r05, the dword stores every other
+                // strip issued with out-of-range offsets were 4 of every 5 store instructions)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     __builtin_amdgcn_raw_buffer_store_b32(
@@ -1008,6 +1012,8 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     }
     const char *ek4 = tune_env("MIPX_RCOL_K4");
     a.k4 = nks4 < nks && !(ek4 && *ek4 == '0');
+    const char *eas = tune_env("MIPX_RCOL_ALLST");
+    a.allst = eas && *eas == '1';
     if (a.k4) {
         nks = nks4;
         kbmax = kbmax4;
