@@ -80,6 +80,7 @@ struct RcArgs {
     int swz;                  // horizontal reads: odd K blocks read their second 8 bytes first
     int k4;                   // K origins 4-byte aligned (ds_read2_b32): one K step where 8-byte origins need two
     int allst;                // A/B: every strip issues the edge-piece dword stores (r05 before)
+    int skipl;                // ring load batches no lane of the wave needs are not issued
 };
 
 // libvips reduce position (reducev.cpp / reduceh.cpp): X = reduce_x (o * shrink, or
@@ -245,6 +246,10 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         lcol[j] = ring_l + static_cast<uint32_t>(16 * col);
     }
     const int lkf = (kRcNT * KMAX) / cpr;  // rows one load batch covers completely
+    // skipl: batch j of this wave loads anything (uniform; the same every step)
+    bool wl[KMAX];
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j) wl[j] = !a.skipl || __builtin_amdgcn_ballot_w64(rr[j] < a.rcap) != 0;
 
     // ---- the step pipeline: register set P = (step - ka) & 1 holds step k + 2's ring
     // chunks and vertical operands from the middle of step k to the top of step k + 2.
@@ -278,6 +283,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
+            if (!wl[j]) continue;
             const int off = rr[j] < a.rcap ? chunk_off(r0, j) : 0x7ffffff0;
             rv[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
             if constexpr (UNAL)
@@ -1014,6 +1020,11 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     a.k4 = nks4 < nks && !(ek4 && *ek4 == '0');
     const char *eas = tune_env("MIPX_RCOL_ALLST");
     a.allst = eas && *eas == '1';
+    // r05: a wave issues no ring load batch whose lanes all idle (MIPX_RCOL_SKIPL=0: every
+    // batch, out-of-range offsets; 500x375 +3 %, 1080p / 1.6 and / 2.4 +2 %,
+    // profiles/r05/small/rcol_skipl_ab.jsonl)
+    const char *esl = tune_env("MIPX_RCOL_SKIPL");
+    a.skipl = !(esl && *esl == '0');
     if (a.k4) {
         nks = nks4;
         kbmax = kbmax4;
