@@ -61,6 +61,7 @@ struct BcArgs {
     uint32_t mag;       // floor(x / scale) == mulhi(x, mag) for the sums here
     int seed;           // 128 scale + (scale + 1) / 2
     int wst2;           // output rows not a multiple of 16 bytes: the edge piece as dwords
+    int skipl;               // load batches no lane of the wave needs are not issued (r05)
     int a16;            // host: horizontal operands 16-byte aligned (k_bcol<.., A16 = true>)
     int sd;             // A16: staged rows start sd bytes into their LDS row (0 / 4 / 8 / 12)
     const signed char *ops;  // device_blur_ops: [NKS][64 lanes][16] horizontal, then [64][16] vertical
@@ -136,10 +137,14 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
         lsl[k] = static_cast<uint32_t>(rr[k] * a.rsd + 16 * col + (A16 ? a.sd : 0));
     }
     rc_u4 rv[2][KMAX];
+    bool wl[KMAX];  // skipl: batch k of this wave loads anything (uniform, the same every step)
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) wl[k] = !a.skipl || __builtin_amdgcn_ballot_w64(rr[k] < kBcRows) != 0;
     auto issue = [&](auto pc, int j) {  // the input rows of step j: 16 j + half + rr
         constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int k = 0; k < KMAX; ++k) {
+            if (!wl[k]) continue;
             const int r = clampi(kBcRows * j + a.half + rr[k], 0, a.h - 1);
             rv[P][k] = __builtin_bit_cast(
                 rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, rr[k] < kBcRows ? r * a.in_pitch + cof[k] : 0x7ffffff0, 0, 0));
@@ -372,6 +377,10 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     a.mag = static_cast<uint32_t>(((1ULL << 32) + scale - 1) / scale);
     a.seed = 128 * scale + (scale + 1) / 2;
     a.wst2 = (ow * b) % 16 != 0;
+    // r05 (as k_rcol): MIPX_BCOL_SKIPL=0 issues every batch, idle lanes out of range; blur
+    // +1-2.3 %, C3 +0.3 %, C5 +0.6 % (profiles/r05/bcol/bsl_ab.jsonl)
+    const char *esl = tune_env("MIPX_BCOL_SKIPL");
+    a.skipl = !(esl && *esl == '0');
     a.ops = device_blur_ops(mask, b, delta, nks);
     if (!a.ops) return MIPX_EDEVICE;
     const size_t lds = static_cast<size_t>(2 * kBcRows) * rsd + static_cast<size_t>(ring) * a.tw +
