@@ -605,10 +605,11 @@ int reduce2m_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
     a.k_base = y0 / kMN;
     a.n_strips = (x1 + kMTW - 1) / kMTW - a.s_base;
     const int steps = (y1 + kMN - 1) / kMN - a.k_base;
-    // 16-row steps per band: 8 (RGB) / 16 (RGBA), measured best (profiles/r04/reduce2m/d_band_sweep.jsonl);
+    // 16-row steps per band: 7 (RGB) / 16 (RGBA), measured best (profiles/r04/reduce2m/d_band_sweep.jsonl;
+    // with the alternating walk RGB 7 beats 8 by 0.7 %, profiles/r05/reduce2m/band_fine_ab.jsonl);
     // MIPX_R2M_BAND overrides (A/B)
     const char *eb = tune_env("MIPX_R2M_BAND");
-    a.band_steps = std::max(1, std::min(steps, (eb && *eb) ? std::atoi(eb) : (b == 3 ? 8 : 16)));
+    a.band_steps = std::max(1, std::min(steps, (eb && *eb) ? std::atoi(eb) : (b == 3 ? 7 : 16)));
     const char *ea = tune_env("MIPX_R2M_ALT");  // A/B: 0 = every band walks down
     a.alt = !(ea && *ea == '0');
     const char *epp = tune_env("MIPX_R2M_PP");  // A/B: 0 = the prime's two row batches one after the other
