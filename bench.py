@@ -83,12 +83,15 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(args, rank_seed=1):
+def cpu_baseline(args, sampling, rank_seed=1):
     """The CPU port timed on the host's cores: oracle/vips_fast.c (the oracle's
     reduce in cache-friendly loop order, -O3 x86-64-v3, tested byte-identical to
     the oracle), OpenMP across images, each image single-threaded as libvips'
-    per-request concurrency 1, over a bounded sample of distinct 4K images."""
+    per-request concurrency 1, over a bounded sample of distinct 4K images.
+    Runs the headline's sampling convention, set explicitly (the oracle switch is
+    process-wide and the verification legs move it)."""
     from oracle import oracle as o
+    o.set_switch("reduce_centre", int(sampling == "centre"))
     threads = args.cpu_threads or host_cores()
     rng = np.random.default_rng(rank_seed)
     distinct = [rng.integers(0, 256, (H_IN, W_IN, BANDS), dtype=np.uint8) for _ in range(args.cpu_distinct)]
@@ -105,7 +108,7 @@ def cpu_baseline(args, rank_seed=1):
             "threads_note": "threads = CPUs allotted to this process (affinity, capped by OMP_NUM_THREADS)"}
 
 
-def c1_cpu_reference(args):
+def c1_cpu_reference(args, sampling):
     """BASELINE.json configs[0] (C1): POST /resize?width=300 on testdata/large.jpg
     through the CPU path, no GPU: host JPEG decode with shrink-on-load (libjpeg DCT
     scaling, 1/4: 480x270), the Lanczos3 reduce of the bimg plan (1.6 x 1.5976,
@@ -115,6 +118,7 @@ def c1_cpu_reference(args):
     import imaginary_amd as ia
     from imaginary_amd import codec
     from oracle import oracle as o
+    o.set_switch("reduce_centre", int(sampling == "centre"))
     path = os.path.join(ROOT, "tests", "golden", "testdata", "large.jpg")
     with open(path, "rb") as f:
         buf = f.read()
@@ -384,8 +388,9 @@ def main():
         if other:
             line["centre"] = other
         if not args.no_cpu and world == 1:  # the CPU figures are N = 1 figures
-            line["cpu_baseline"] = cpu_baseline(args)
-            line["c1_cpu_reference"] = c1_cpu_reference(args)
+            line["cpu_baseline"] = cpu_baseline(args, sampling)
+            line["cpu_baseline"]["sampling"] = sampling
+            line["c1_cpu_reference"] = c1_cpu_reference(args, sampling)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

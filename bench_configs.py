@@ -30,10 +30,15 @@ def _aggregate(texts, nranks):
     """One line per config from the ranks' lines: the whole job's images over the
     slowest rank's step time (the ranks time after a common barrier)."""
     per = {}
+    keys = ("images_per_step", "ms_per_step", "device_ms_per_step", "hbm_frac")
     for r, t in enumerate(texts):
         for ln in t.splitlines():
             if ln.startswith("{"):
                 d = json.loads(ln)
+                if not all(k in d for k in keys):  # E2E / E2EC lines: not step-timed, passed through per rank
+                    d["rank"] = r
+                    print(json.dumps(d), flush=True)
+                    continue
                 per.setdefault(d["config"], []).append(d)
     for name, ds in per.items():
         ms = max(d["ms_per_step"] for d in ds)
@@ -42,8 +47,7 @@ def _aggregate(texts, nranks):
         out.update({"n_gpus": nranks, "images_per_step": imgs, "ms_per_step": ms,
                     "images_per_sec": round(imgs / (ms * 1e-3), 1),
                     "verified_vs_oracle": all(d["verified_vs_oracle"] for d in ds),
-                    "per_rank": [{k: d[k] for k in ("images_per_step", "ms_per_step", "device_ms_per_step",
-                                                    "hbm_frac")} for d in ds]})
+                    "per_rank": [{k: d[k] for k in keys} for d in ds]})
         print(json.dumps(out), flush=True)
 
 

@@ -21,6 +21,7 @@ import ctypes as C
 import dataclasses
 import json
 import math
+import re
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
@@ -83,6 +84,7 @@ class ImageOptions:
     type: str = ""
     aspect_ratio: str = ""
     background: List[int] = field(default_factory=list)
+    color: List[int] = field(default_factory=list)   # text watermark colour (not a pixel-engine op)
     extend: int = 1          # bimg.ExtendCopy default (params.go:342, 356)
     colorspace: int = 0      # bimg.Interpretation (params.go:260, parseColorspace 392)
     quality: int = 0
@@ -113,85 +115,249 @@ class Decoded:
 
 
 # ---- params.go helpers -----------------------------------------------------------
-def parse_int(v: str) -> int:
-    """params.go:376-390: round half up of |float|."""
+# Go's strconv semantics restated exactly (params_test.go's tables pass byte for byte:
+# tests/test_params.py).  The helpers return Go's (value, error) pair: Go returns a
+# value even when it also returns an error, and the tables check both.
+_GO_DEC = re.compile(r"[+-]?(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?\Z")
+_GO_HEX = re.compile(r"[+-]?0[xX](?:[0-9a-fA-F]+\.?[0-9a-fA-F]*|\.[0-9a-fA-F]+)[pP][+-]?[0-9]+\Z")
+_GO_SPECIAL = {"inf": math.inf, "+inf": math.inf, "-inf": -math.inf, "infinity": math.inf,
+               "+infinity": math.inf, "-infinity": -math.inf, "nan": math.nan}
+
+
+class GoParseError(ValueError):
+    """strconv.NumError: ErrSyntax / ErrRange."""
+
+
+def _go_parse_float(v: str):
+    """strconv.ParseFloat(v, 64): no surrounding space, no underscores in decimal
+    literals; inf / infinity / nan in any case; hex floats need a p exponent.  A
+    syntax error gives (0, err); a range error gives (+-Inf, err)."""
+    low = v.lower()
+    if low in _GO_SPECIAL:
+        return _GO_SPECIAL[low], None
+    if _GO_DEC.match(v):
+        f = float(v)
+    elif _GO_HEX.match(v):
+        sign = -1.0 if v[0] == "-" else 1.0
+        try:
+            f = sign * float.fromhex(v.lstrip("+-"))
+        except OverflowError:
+            return sign * math.inf, GoParseError(f'strconv.ParseFloat: parsing "{v}": value out of range')
+    else:
+        return 0.0, GoParseError(f'strconv.ParseFloat: parsing "{v}": invalid syntax')
+    if math.isinf(f):
+        return f, GoParseError(f'strconv.ParseFloat: parsing "{v}": value out of range')
+    return f, None
+
+
+def parse_float(v: str):
+    """params.go:384-390: |strconv.ParseFloat|; "" is (0, nil)."""
     if v == "":
-        return 0
-    return int(math.floor(abs(float(v)) + 0.5))
+        return 0.0, None
+    f, err = _go_parse_float(v)
+    return abs(f), err
 
 
-def parse_float(v: str) -> float:
-    return abs(float(v)) if v != "" else 0.0
-
-
-def parse_bool(v: str) -> bool:
+def parse_int(v: str):
+    """params.go:376-382: int(math.Floor(f + 0.5)) of parse_float; "" is (0, nil)."""
     if v == "":
-        return False
-    s = v.strip().lower()
-    if s in ("1", "t", "true"):
-        return True
-    if s in ("0", "f", "false"):
-        return False
-    raise ValueError(v)
+        return 0, None
+    f, err = parse_float(v)
+    if math.isinf(f) or math.isnan(f):  # Go's int() of +Inf / NaN on amd64: the minimum int64
+        return -(1 << 63), err
+    return int(math.floor(f + 0.5)), err
+
+
+_GO_BOOLS = {"1": True, "t": True, "T": True, "TRUE": True, "true": True, "True": True,
+             "0": False, "f": False, "F": False, "FALSE": False, "false": False, "False": False}
+
+
+def parse_bool(v: str):
+    """params.go:369-374: "" is (false, nil), else strconv.ParseBool's exact set."""
+    if v == "":
+        return False, None
+    if v in _GO_BOOLS:
+        return _GO_BOOLS[v], None
+    return False, GoParseError(f'strconv.ParseBool: parsing "{v}": invalid syntax')
+
+
+def _go_trim_lower(v: str) -> str:
+    return v.lower().strip()   # strings.TrimSpace(strings.ToLower(v))
 
 
 def parse_extend_mode(v: str) -> int:
-    """params.go:421-437 (default mirror)."""
+    """params.go:421-437: bimg.Extend, mirror by default."""
     m = {"white": 4, "black": 0, "copy": 1, "background": 5, "lastpixel": 6}
-    return m.get(v.strip().lower(), 3)
+    return m.get(_go_trim_lower(v), 3)
 
 
 def parse_gravity(v: str) -> int:
-    """params.go:439-453."""
+    """params.go:439-453: bimg.Gravity, centre by default."""
     m = {"south": 3, "north": 1, "east": 2, "west": 4, "smart": 5}
-    return m.get(v.strip().lower(), 0)
+    return m.get(_go_trim_lower(v), 0)
 
 
 def parse_colorspace(v: str) -> int:
-    """params.go:392-397: "bw" -> InterpretationBW, anything else sRGB."""
-    return _abi.INTERPRETATION_BW if v.strip().lower() == "bw" else _abi.INTERPRETATION_SRGB
+    """params.go:392-397: exactly "bw" -> InterpretationBW, anything else sRGB."""
+    return _abi.INTERPRETATION_BW if v == "bw" else _abi.INTERPRETATION_SRGB
+
+
+def _go_parse_uint8(v: str) -> int:
+    """strconv.ParseUint(v, 10, 8) with the error dropped, as params.go:404 does: a
+    syntax error (signs, spaces, letters, "") gives 0, a range error gives 255."""
+    if not v or not all("0" <= c <= "9" for c in v):
+        return 0
+    return min(int(v), 255)
 
 
 def parse_color(v: str) -> List[int]:
-    return [min(int(x.strip() or 0), 255) for x in v.split(",")] if v else []
+    """params.go:399-409: comma-split, TrimSpace, ParseUint(.., 10, 8)."""
+    return [_go_parse_uint8(x.strip()) for x in v.split(",")] if v != "" else []
 
 
-def build_params_from_query(query: Dict[str, Any]) -> ImageOptions:
-    """params.go:354-366 for the pixel-relevant parameters (Extend defaults to copy)."""
-    o = ImageOptions()
-    ints = {"width": "width", "height": "height", "areawidth": "area_width", "areaheight": "area_height",
-            "rotate": "rotate", "top": "top", "left": "left", "factor": "factor", "quality": "quality",
-            "compression": "compression"}
-    for k, v in query.items():
-        v = v if isinstance(v, str) else str(v) if not isinstance(v, (list, dict, bool)) else v
-        if k in ints:
-            setattr(o, ints[k], parse_int(v) if isinstance(v, str) else int(v))
-        elif k in ("sigma", "minampl", "opacity"):
-            setattr(o, {"sigma": "sigma", "minampl": "min_ampl", "opacity": "opacity"}[k],
-                    parse_float(v) if isinstance(v, str) else float(v))
-        elif k in ("flip", "flop", "force", "embed", "nocrop", "norotation"):
-            attr = {"nocrop": "no_crop", "norotation": "no_rotation"}.get(k, k)
-            setattr(o, attr, parse_bool(v) if isinstance(v, str) else bool(v))
-            setattr(o.is_defined, attr, True)
-        elif k == "extend":
+def parse_json_operations(data: str) -> List[Dict[str, Any]]:
+    """params.go:411-419: shorter than 2 bytes is no operations; otherwise a JSON array
+    of {"operation", "ignore_failure", "params"} with unknown fields refused (Go's
+    DisallowUnknownFields; encoding/json matches field names case-insensitively)."""
+    if len(data) < 2:
+        return []
+    ops = json.loads(data)
+    if ops is None:
+        return []
+    if not isinstance(ops, list):
+        raise GoParseError("json: cannot unmarshal into Go value of type main.PipelineOperations")
+    out = []
+    for op in ops:
+        if op is None:
+            op = {}
+        if not isinstance(op, dict):
+            raise GoParseError("json: cannot unmarshal into Go struct field of type main.PipelineOperation")
+        d: Dict[str, Any] = {"operation": "", "ignore_failure": False, "params": None}
+        for k, val in op.items():
+            key = {"operation": "operation", "ignore_failure": "ignore_failure", "params": "params"}.get(k.lower())
+            if key is None:
+                raise GoParseError(f'json: unknown field "{k}"')
+            want = {"operation": str, "ignore_failure": bool, "params": dict}[key]
+            if val is not None and not isinstance(val, want):
+                raise GoParseError(f"json: cannot unmarshal into Go struct field PipelineOperation.{key}")
+            if val is not None:
+                d[key] = val
+        out.append(d)
+    return out
+
+
+# coerceType* (params.go:62-102): a pipeline operation's params are JSON values
+class UnsupportedValue(ValueError):
+    """params.go:14 ErrUnsupportedValue."""
+
+
+def coerce_type_int(p):
+    if isinstance(p, bool):
+        raise UnsupportedValue("unsupported value")
+    if isinstance(p, int):
+        return p
+    if isinstance(p, float):
+        return int(p)              # Go int(float64): truncation toward zero
+    if isinstance(p, str):
+        v, err = parse_int(p)
+        if err:
+            raise err
+        return v
+    raise UnsupportedValue("unsupported value")
+
+
+def coerce_type_float(p):
+    if isinstance(p, bool):
+        raise UnsupportedValue("unsupported value")
+    if isinstance(p, (int, float)):
+        return float(p)            # as given: no abs() for numbers (params.go:75-85)
+    if isinstance(p, str):
+        v, err = parse_float(p)
+        if err:
+            raise err
+        return v
+    raise UnsupportedValue("unsupported value")
+
+
+def coerce_type_bool(p):
+    if isinstance(p, bool):
+        return p
+    if isinstance(p, str):
+        v, err = parse_bool(p)
+        if err:
+            raise err
+        return v
+    raise UnsupportedValue("unsupported value")
+
+
+def coerce_type_string(p):
+    if isinstance(p, str):
+        return p
+    raise UnsupportedValue("unsupported value")
+
+
+_INT_PARAMS = {"width": "width", "height": "height", "areawidth": "area_width", "areaheight": "area_height",
+               "rotate": "rotate", "top": "top", "left": "left", "factor": "factor", "quality": "quality",
+               "compression": "compression"}
+_FLOAT_PARAMS = {"sigma": "sigma", "minampl": "min_ampl", "opacity": "opacity"}
+_BOOL_PARAMS = {"flip": "flip", "flop": "flop", "force": "force", "embed": "embed", "nocrop": "no_crop",
+                "norotation": "no_rotation"}
+_STR_PARAMS = {"type": "type", "aspectratio": "aspect_ratio", "image": "image", "text": "text"}
+
+
+def _coerce(o: ImageOptions, k: str, v) -> None:
+    """paramTypeCoercions (params.go:20-60) for the pixel-relevant keys."""
+    if k in _INT_PARAMS:
+        setattr(o, _INT_PARAMS[k], coerce_type_int(v))
+    elif k in _FLOAT_PARAMS:
+        val = coerce_type_float(v)
+        setattr(o, _FLOAT_PARAMS[k], float(np.float32(val)) if k == "opacity" else val)  # Opacity is float32
+    elif k in _BOOL_PARAMS:
+        setattr(o.is_defined, _BOOL_PARAMS[k], True)
+        setattr(o, _BOOL_PARAMS[k], coerce_type_bool(v))
+    elif k in _STR_PARAMS:
+        setattr(o, _STR_PARAMS[k], coerce_type_string(v))
+    elif k in ("extend", "gravity", "colorspace", "background", "color", "operations"):
+        if not isinstance(v, str):
+            if k == "operations" and isinstance(v, list):   # already decoded (the Python mirror's callers)
+                o.operations = v
+                return
+            raise UnsupportedValue("unsupported value")
+        if k == "extend":
             o.extend = parse_extend_mode(v)
         elif k == "gravity":
             o.gravity = parse_gravity(v)
         elif k == "colorspace":
             o.colorspace = parse_colorspace(v)
         elif k == "background":
-            o.background = parse_color(v) if isinstance(v, str) else list(v)
-        elif k == "type":
-            o.type = v
-        elif k == "aspectratio":
-            o.aspect_ratio = v
-        elif k == "image":
-            o.image = v
-        elif k == "text":
-            o.text = v
-        elif k == "operations":
-            o.operations = v
+            o.background = parse_color(v)
+        elif k == "color":
+            o.color = parse_color(v)
+        else:
+            o.operations = parse_json_operations(v)
+
+
+def _build_params(items) -> ImageOptions:
+    o = ImageOptions()   # Extend defaults to bimg.ExtendCopy (params.go:342, 356)
+    for k, v in items:
+        try:
+            _coerce(o, k, v)
+        except (ValueError, json.JSONDecodeError) as e:
+            raise ImaginaryError(f"error processing parameter {k!r} with value {v!r}: {e}") from e
     return o
+
+
+def build_params_from_query(query: Dict[str, Any]) -> ImageOptions:
+    """params.go:354-366.  A query value is a string (url.Values.Get: the first of a
+    list); a value that is already typed (the Python callers' dicts) coerces as a
+    pipeline param would."""
+    return _build_params((k, (v[0] if v else "") if isinstance(v, list) and k != "operations" else v)
+                         for k, v in query.items())
+
+
+def build_params_from_operation(op: Dict[str, Any]) -> ImageOptions:
+    """params.go:340-352: a pipeline operation's JSON params."""
+    return _build_params((op.get("params") or {}).items())
 
 
 # ---- options.go BimgOptions ----------------------------------------------------------
@@ -611,7 +777,7 @@ def Pipeline(img, o: ImageOptions, **kw):
             if fn is None:
                 raise ImaginaryError(f"Unsupported operation: {name}")
             try:
-                out = fn(out.body, build_params_from_query(op.get("params", {})), **_stage_kw(fn, kw))
+                out = fn(out.body, build_params_from_operation(op), **_stage_kw(fn, kw))
             except ImaginaryError:
                 if not op.get("ignore_failure"):
                     raise
@@ -630,7 +796,7 @@ def Pipeline(img, o: ImageOptions, **kw):
         fn = OperationsMap.get(name)
         if fn is None:
             raise ImaginaryError(f"Unsupported operation: {name}")
-        opts = build_params_from_query(op.get("params", {}))
+        opts = build_params_from_operation(op)
         try:
             out = fn(cur, opts, chain=stages, **_stage_kw(fn, kw))
         except ImaginaryError:

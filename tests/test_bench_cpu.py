@@ -84,3 +84,23 @@ def test_bench_configs_aggregates_rank_lines(capsys):
     d = json.loads(capsys.readouterr().out.strip())
     assert d["n_gpus"] == 2 and d["images_per_step"] == 1024 and d["ms_per_step"] == 5.0
     assert abs(d["images_per_sec"] - 1024 / 5e-3) < 0.1 and len(d["per_rank"]) == 2
+    # E2E / E2EC lines carry no step timing: passed through per rank, not aggregated
+    e2e = json.dumps({"config": "E2E", "requests_per_sec": 100.0, "verified_vs_oracle": True})
+    bench_configs._aggregate([e2e, e2e + "\n" + mk(256, 2.0)], 2)
+    out = [json.loads(ln) for ln in capsys.readouterr().out.strip().splitlines()]
+    assert [(d["config"], d.get("rank")) for d in out] == [("E2E", 0), ("E2E", 1), ("C5", None)]
+    assert out[2]["images_per_step"] == 256 and out[2]["n_gpus"] == 2
+
+
+def test_cpu_baseline_runs_the_headline_convention():
+    """the centre leg's verification left the oracle's process-wide switch at
+    centre, so the corner headline's CPU baseline timed the centre convention. The CPU
+    legs now set the switch to the headline's convention themselves."""
+    import argparse
+    from oracle import oracle as o
+    args = argparse.Namespace(cpu_threads=1, cpu_distinct=1, cpu_images=1)
+    for headline, other in (("corner", 1), ("centre", 0)):
+        o.set_switch("reduce_centre", other)
+        bench.cpu_baseline(args, headline)
+        assert o.get_switch("reduce_centre") == int(headline == "centre")
+    o.set_switch("reduce_centre", 0)
