@@ -280,238 +280,6 @@ __global__ void __launch_bounds__(256) k_affine_sep(AffSepArgs a) {
 }
 
 // ===========================================================================
-// k_enlarge2<B>: vips_affine at exactly 2 x 2 (bimg Enlarge to twice the size, the
-// op-survey's 1080p -> 4K and 550x740 x 2 shapes).  At scale 2 the positions repeat with
-// period 2: output pixel 2k samples input columns k-2 .. k+1 at phase 96 (X = k + 0.75),
-// 2k+1 columns k-1 .. k+2 at phase 32 (X = k + 1.25), and the same for rows.  So every
-// position, tap and window offset is a compile-time pattern:
-//  * a wave owns a strip of 256 output pixels (lane l: pixels 4l .. 4l+3 = input pair
-//    columns k, k+1, window k-2 .. k+3) and walks a band of 32 input rows (64 output rows);
-//    waves are independent (wave-private LDS, no barriers);
-//  * input rows are staged 8 at a time into a 16-row wave-private LDS ring (16-byte
-//    chunks, extend modes applied per byte only in the chunks that cross an image edge,
-//    loaded one batch ahead into registers);
-//  * per input row r, each lane makes H (bicubic.cpp's rounded row sums) for its 4 pixels
-//    x B channels from one 6-pixel window (byte pairs by v_perm, v_dot2 against the
-//    phase-96 / phase-32 taps) into a 4-row register ring;
-//  * rows r-3 .. r then give output rows 2r-2 (phase 96) and 2r-3 (phase 32): the H pairs
-//    (r-3, r-2) and (r-1, r) are packed once and feed both rows' v_dot2.
-// About 7 lane-operations per output byte against ~20 in k_affine_sep.
-// ===========================================================================
-constexpr int kE2RB = 32;  // input rows per wave band
-
-// v_dot2_i32_i16 in its VOP3P form (an accumulator operand, so no v_mov of the seed into the
-// destination, which the compiler's VOP2 v_dot2c form needs): first with an SGPR seed
-__device__ __forceinline__ int e2_dot_s(uint32_t a, uint32_t b, int c) {
-    int d;
-    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
-    return d;
-}
-__device__ __forceinline__ int e2_dot(uint32_t a, uint32_t b, int c) {
-    int d;
-    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
-
-template <int B>
-struct E2 {
-    static constexpr int NCOL = 2 * 64 + 6;                // staged input columns c0 .. c0 + 133
-    static constexpr int SR = (NCOL * B + 4 + 15) & ~15;   // staged row stride (a dword of read slack)
-    static constexpr int NCH = (NCOL * B + 15) / 16;       // 16-byte chunks per staged row
-    static constexpr int KL = (8 * NCH + 63) / 64;         // chunks per lane per 8-row batch
-    static constexpr int NWD = (6 * B + 3) / 4;            // window dwords (6 pixels)
-    static_assert(2 * 63 * B + 4 * (NWD + 1) <= SR, "window read slack");
-};
-
-struct Enl2Args {
-    const u8 *in;
-    u8 *out;
-    int w, h, ow, oh, extend, fill;
-    long long in_img, out_img;
-    int strips, bands;
-    uint32_t e01, e23, o01, o23;  // phase-96 / phase-32 taps as int16 pairs
-    int out_aligned;
-    int seed;                     // 2048: a kernel argument, so the v_dot2 seed is an SGPR
-};
-
-template <int B>
-__global__ void __launch_bounds__(256) k_enlarge2(Enl2Args a) {
-    using G = E2<B>;
-    constexpr int SR = G::SR, NCH = G::NCH, KL = G::KL, NWD = G::NWD;
-    __shared__ __attribute__((aligned(16))) u8 ring_all[4 * 16 * SR];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int task = blockIdx.x * 4 + wave;
-    if (task >= a.strips * a.bands) return;  // whole waves only (gridDim.y = images)
-    const int strip = task % a.strips, band = task / a.strips;
-    const int img = blockIdx.y;
-    u8 *ring = ring_all + wave * 16 * SR;
-    const uint32_t ring_l = rc_lds(ring);
-
-    const int x0 = 256 * strip;          // output pixels x0 .. x0 + 255
-    const int c0 = x0 / 2 - 2;           // first staged input column
-    const int ma = kE2RB * band, mb = min(ma + kE2RB, a.h);
-    const int rfirst = ma - 2, rlast = mb + 1;  // H rows this band needs
-    const int pitch = a.w * B;
-    // over the dword-aligned-down image base, range rounded up to the dword holding the
-    // last byte: the tail dword of a chunk that ends at the image's last byte is then in
-    // range (with image_rsrc it straddled num_records and read 0 when in_img % 4 != 0)
-    int delta = 0;
-    const __amdgpu_buffer_rsrc_t src = image_rsrc_aligned(a.in + img * a.in_img, a.in_img, &delta);
-    u8 *dst = a.out + img * a.out_img;
-
-    // ---- staging: chunk q = lane + 64 j of an 8-row batch = (row t, column chunk cc) ----
-    int ct[KL], cc[KL];
-#pragma unroll
-    for (int j = 0; j < KL; ++j) {
-        const int q = lane + 64 * j;
-        ct[j] = q < 8 * NCH ? q / NCH : 8;  // 8: idle
-        cc[j] = q - (q / NCH) * NCH;
-    }
-    auto load = [&](rc_u4 *v, int r0) {
-#pragma unroll
-        for (int j = 0; j < KL; ++j) {
-            v[j] = rc_u4{0u, 0u, 0u, 0u};
-            const int r = r0 + ct[j];
-            if (ct[j] >= 8 || r > rlast) continue;
-            const int sr = extend_idx(r, a.h, a.extend);
-            const int b0 = c0 * B + 16 * cc[j];  // input byte of the chunk's first staged byte
-            if (sr < 0) {
-                const uint32_t f = 0x01010101u * static_cast<uint32_t>(a.fill);
-                v[j] = rc_u4{f, f, f, f};
-            } else if (b0 >= 0 && b0 + 16 <= pitch) {
-                const int off = sr * pitch + b0 + delta;
-                const rc_u4 p = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off & ~3, 0, 0));
-                const uint32_t e = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
-                const int sh = off & 3;
-                v[j] = rc_u4{__builtin_amdgcn_alignbyte(p.y, p.x, sh), __builtin_amdgcn_alignbyte(p.z, p.y, sh),
-                             __builtin_amdgcn_alignbyte(p.w, p.z, sh), __builtin_amdgcn_alignbyte(e, p.w, sh)};
-            } else {  // a chunk across an image edge: per byte through the extend mode
-                uint32_t d[4] = {0u, 0u, 0u, 0u};
-                for (int e = 0; e < 16; ++e) {
-                    const int col = (b0 + e >= 0 ? (b0 + e) / B : -((-(b0 + e) + B - 1) / B));
-                    const int ch = b0 + e - col * B;
-                    const int sc = extend_idx(col, a.w, a.extend);
-                    const uint32_t byte = sc < 0 ? static_cast<uint32_t>(a.fill)
-                                                 : static_cast<uint32_t>(a.in[img * a.in_img + static_cast<long long>(sr) * pitch + sc * B + ch]);
-                    d[e >> 2] |= byte << (8 * (e & 3));
-                }
-                v[j] = rc_u4{d[0], d[1], d[2], d[3]};
-            }
-        }
-    };
-    auto store = [&](const rc_u4 *v, int r0) {
-#pragma unroll
-        for (int j = 0; j < KL; ++j)
-            if (ct[j] < 8 && r0 + ct[j] <= rlast)
-                lds_wr128(ring_l + static_cast<uint32_t>(((r0 + ct[j] - rfirst) & 15) * SR + 16 * cc[j]), v[j]);
-    };
-
-    // ---- the lane's window: staged bytes 2 l B .. (6 pixels), dword aligned down ----
-    const int wb = 2 * lane * B, wsh = wb & 3;
-    const int sd = a.seed;
-    auto pair = [](const uint32_t *t, int j0, int j1) -> uint32_t {  // bytes j0, j1 as an int16 pair
-        const int d0 = j0 >> 2, d1 = j1 >> 2;
-        const uint32_t sel = static_cast<uint32_t>((j0 & 3) | (0x0c << 8) | (((j1 & 3) + 4) << 16) | (0x0c << 24));
-        return __builtin_amdgcn_perm(t[d1], t[d0], sel);
-    };
-    constexpr int NV = 4 * B;  // H values per lane and row: pixels 0..3 x B channels
-    int hr[4][NV];             // H ring: slot = (row - rfirst) & 3
-    auto hrow = [&](int r, int slot_unused, int *hv) {
-        (void)slot_unused;
-        const uint32_t base = ring_l + static_cast<uint32_t>(((r - rfirst) & 15) * SR + (wb & ~3));
-        uint32_t d[NWD + 1], t[NWD];
-#pragma unroll
-        for (int k = 0; k <= NWD; ++k) d[k] = lds_rd32(base + 4 * k);
-        // the wait as a data dependence of the reads (lds_ops.h lgkm_wait_for)
-#pragma unroll
-        for (int k = 0; k <= NWD; ++k) rc_pin(d[k]);
-        lgkm_wait();
-#pragma unroll
-        for (int k = 0; k <= NWD; ++k) rc_pin(d[k]);
-#pragma unroll
-        for (int k = 0; k < NWD; ++k) t[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], wsh);
-#pragma unroll
-        for (int px = 0; px < 4; ++px) {
-            const int s = px == 0 ? 0 : px == 3 ? 2 : 1;  // window pixel of the first tap
-            const uint32_t c01 = (px & 1) ? a.o01 : a.e01, c23 = (px & 1) ? a.o23 : a.e23;
-#pragma unroll
-            for (int c = 0; c < B; ++c) {
-                const uint32_t p01 = pair(t, s * B + c, (s + 1) * B + c);
-                const uint32_t p23 = pair(t, (s + 2) * B + c, (s + 3) * B + c);
-                hv[px * B + c] = e2_dot(p23, c23, e2_dot_s(p01, c01, sd)) >> 12;
-            }
-        }
-    };
-    const int xl = x0 + 4 * lane;               // the lane's first output pixel
-    const int nb_lane = min(4, a.ow - xl) * B;  // its output bytes in the row (<= 0: none)
-    const bool full = nb_lane == 4 * B && a.out_aligned;
-    auto put = [&](int y, const uint32_t *o) {
-        if (nb_lane <= 0 || y >= a.oh) return;
-        u8 *q = dst + (static_cast<long long>(y) * a.ow + xl) * B;
-        if (full) {  // one 4 B-byte store per lane: a wave writes 256 B contiguous bytes per instruction
-            if (B == 1) *reinterpret_cast<uint32_t *>(q) = o[0];
-            else if (B == 2) *reinterpret_cast<uint2 *>(q) = uint2{o[0], o[B > 1 ? 1 : 0]};
-            else if (B == 3) *reinterpret_cast<uint3 *>(q) = uint3{o[0], o[B > 1 ? 1 : 0], o[B > 2 ? 2 : 0]};
-            else *reinterpret_cast<uint4 *>(q) = uint4{o[0], o[B > 1 ? 1 : 0], o[B > 2 ? 2 : 0], o[B > 3 ? 3 : 0]};
-        } else {
-            for (int e = 0; e < nb_lane; ++e) q[e] = static_cast<u8>(o[e >> 2] >> (8 * (e & 3)));
-        }
-    };
-    // output rows 2r-2 (phase 96) and 2r-3 (phase 32) from H rows r-3 .. r (slots s0 .. s3):
-    // the row pairs (r-3, r-2) and (r-1, r) are packed once for both
-    auto emit2 = [&](int r, int s0, int s1, int s2, int s3) {
-        const bool ev = r - 1 >= ma && r - 1 < mb, od = r - 2 >= ma && r - 2 < mb;
-        if (!ev && !od) return;
-        uint32_t oe[B], oo[B];
-#pragma unroll
-        for (int k = 0; k < B; ++k) {
-            int ve[4], vo[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int i = 4 * k + e;
-                const uint32_t pa = __builtin_amdgcn_perm(static_cast<uint32_t>(hr[s1][i]), static_cast<uint32_t>(hr[s0][i]), 0x05040100u);
-                const uint32_t pb = __builtin_amdgcn_perm(static_cast<uint32_t>(hr[s3][i]), static_cast<uint32_t>(hr[s2][i]), 0x05040100u);
-                ve[e] = e2_dot(pb, a.e23, e2_dot_s(pa, a.e01, sd));
-                vo[e] = e2_dot(pb, a.o23, e2_dot_s(pa, a.o01, sd));
-            }
-            uint32_t lo, hi;
-            asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(ve[0]), "v"(ve[1]));
-            asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(ve[2]), "v"(ve[3]));
-            oe[k] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-            asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(lo) : "v"(vo[0]), "v"(vo[1]));
-            asm("v_ashr_pk_u8_i32 %0, %1, %2, 12" : "=v"(hi) : "v"(vo[2]), "v"(vo[3]));
-            oo[k] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
-        }
-        if (od) put(2 * r - 3, oo);
-        if (ev) put(2 * r - 2, oe);
-    };
-
-    // ---- the band: rows rfirst .. rlast, 8 per staged batch, 4 per unrolled group ----
-    rc_u4 pf[KL];
-    load(pf, rfirst);
-    store(pf, rfirst);
-    load(pf, rfirst + 8);
-    for (int r0 = rfirst; r0 <= rlast; r0 += 8) {
-#pragma unroll
-        for (int g = 0; g < 8; g += 4) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int r = r0 + g + i;  // slot (r - rfirst) & 3 = i (r0 - rfirst is a multiple of 4)
-                if (r > rlast) break;
-                hrow(r, i, hr[i]);
-                // rows r-3 .. r sit in slots i+1, i+2, i+3, i (mod 4)
-                emit2(r, (i + 1) & 3, (i + 2) & 3, (i + 3) & 3, i);
-            }
-        }
-        if (r0 + 8 <= rlast) {
-            store(pf, r0 + 8);
-            if (r0 + 16 <= rlast) load(pf, r0 + 16);
-        }
-    }
-}
-
-// ===========================================================================
 // k_enlm<B, NK>: vips_affine at any enlargement whose windows fit the tiles below
 // (2 x, 3 x, 4 x, 1.5 x, per-axis mixes; the host checks), both passes on the matrix
 // cores in f16 with f32 accumulation — every product and partial sum is an exact f32
@@ -564,6 +332,14 @@ struct EnlmArgs {
     long long blocks;
     int dbg;                // MIPX_ENLM_DBG (timing probes only, wrong pixels): 1 no staging loads, 2 no stores, 4 no realignment dwords
 };
+
+// The timing probes exist only in a -DMIPX_PROBES build (scripts/, `make PROBES=1`): the
+// shipped library compiles them out, so no environment can make Enlarge skip work.
+#ifdef MIPX_PROBES
+__device__ __forceinline__ int em_dbg(const EnlmArgs &a) { return a.dbg; }
+#else
+__device__ __forceinline__ int em_dbg(const EnlmArgs &) { return 0; }
+#endif
 
 // 8 bytes -> 8 f16 of value 1024 + p
 __device__ __forceinline__ em_h8 em_cvt8(uint32_t lo, uint32_t hi) {
@@ -667,12 +443,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
             if (sr < 0) {
                 const uint32_t f = 0x01010101u * static_cast<uint32_t>(a.fill);
                 pq[j] = rc_u4{f, f, f, f};
-            } else if (a.dbg & 1) {
+            } else if (em_dbg(a) & 1) {
                 // timing probe: no load
             } else if (b0 >= 0 && b0 + 16 <= pitch) {
                 const int off = sr * pitch + b0 + delta;
                 pq[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, off & ~3, 0, 0));
-                if (!(a.dbg & 4)) pe[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
+                if (!(em_dbg(a) & 4)) pe[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
                 psh[j] = static_cast<uint32_t>(off & 3);
             } else {  // a chunk across an image edge: per byte through the extend mode, four
                       // byte loads in flight per wait
@@ -791,7 +567,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
                 const int pc2 = (lane & 3) + 4 * i;
                 const rc_u4 v = *reinterpret_cast<const rc_u4 *>(otl + rr * kEmOS + 16 * pc2);
                 const int yy = oy + rr, bo = x0b + 16 * pc2;
-                if (yy <= yl && bo < rowb && !(a.dbg & 2)) {
+                if (yy <= yl && bo < rowb && !(em_dbg(a) & 2)) {
                     const int off = yy * rowb + bo;
                     if (bo + 16 <= rowb) {
                         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, v), dst, off, 0, 0);
@@ -888,8 +664,8 @@ std::map<std::pair<int, double>, EmAxis> &em_axes() {
     static auto *m = new std::map<std::pair<int, double>, EmAxis>();
     return *m;
 }
-std::vector<int4 *> &em_retired() {
-    static auto *v = new std::vector<int4 *>();
+std::vector<std::pair<int, int4 *>> &em_retired() {  // (device, table)
+    static auto *v = new std::vector<std::pair<int, int4 *>>();
     return *v;
 }
 
@@ -931,7 +707,10 @@ const EmAxis *em_axis_locked(int dev, double s, int n) {
         (void)hipFree(d);
         return nullptr;
     }
-    if (it != m.end() && it->second.gen == gen) em_retired().push_back(const_cast<int4 *>(it->second.dev));
+    if (it != m.end()) {
+        if (it->second.gen == gen) em_retired().emplace_back(dev, const_cast<int4 *>(it->second.dev));  // may be in flight
+        else (void)hipFree(const_cast<int4 *>(it->second.dev));  // an older generation's: unused (shutdown drained)
+    }
     ax.dev = d;
     ax.gen = gen;
     m[{dev, s}] = std::move(ax);
@@ -1075,6 +854,25 @@ bool enlm_plan(int n, int w, int h, int b, int ow, int oh, double xs, double ys,
 
 }  // namespace
 
+// Called by free_device_tables (mipx_shutdown, after every queue drained): the axis
+// tables, the retired ones and the cached plans that point at them.
+void free_enlm_tables() {
+    std::lock_guard<std::mutex> lk(g_em_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto &kv : em_axes()) {
+        (void)hipSetDevice(kv.first.first);
+        (void)hipFree(const_cast<int4 *>(kv.second.dev));
+    }
+    em_axes().clear();
+    for (auto &r : em_retired()) {
+        (void)hipSetDevice(r.first);
+        (void)hipFree(r.second);
+    }
+    em_retired().clear();
+    (void)hipSetDevice(cur);
+}
+
 int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, double ys, int extend,
                   hipStream_t st) {
     AffineArgs a{};
@@ -1103,8 +901,10 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
         if (enlm_plan(n, w, h, b, a.ow, a.oh, xs, ys, &g, &nk, &nu)) {
             g.in = in, g.out = out, g.w = w, g.h = h, g.ow = a.ow, g.oh = a.oh, g.extend = a.extend, g.fill = a.fill;
             g.in_img = a.in_img, g.out_img = a.out_img;
+#ifdef MIPX_PROBES
             const char *edb = tune_env("MIPX_ENLM_DBG");
             g.dbg = edb && *edb ? std::atoi(edb) : 0;
+#endif
             if (grid_ok(g.blocks)) {
                 const size_t lds = static_cast<size_t>(nu) * nk * 2 * 1024 + 4 * static_cast<size_t>(16 * g.rs + 16 * em_os(nu) + 16 * g.br);
                 const dim3 grid(static_cast<unsigned>(g.blocks));
@@ -1118,33 +918,6 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
             }
         }
         if (em && *em == '2') return MIPX_EUNSUPPORTED;  // tests: k_enlm or an error
-    }
-    // exactly 2 x 2: the fixed-pattern kernel (MIPX_ENLARGE2=0 / 1 forces it off / on, A/B)
-    const char *e2 = tune_env("MIPX_ENLARGE2");
-    // (strips of 256 output pixels: a ragged last strip leaves lanes idle; below 90 % strip
-    // use k_affine_sep is faster, e.g. 550x740: 1100 = 4.3 strips, profiles/r04/affine/)
-    const bool e2_fits = static_cast<double>(2 * w) / (256.0 * ((2 * w + 255) / 256)) >= 0.9;
-    if (xs == 2.0 && ys == 2.0 && (e2 && *e2 ? *e2 == '1' : e2_fits) && n <= 65535 && a.ow == 2 * w && a.oh == 2 * h) {
-        Enl2Args g{};
-        g.in = in, g.out = out, g.w = w, g.h = h, g.ow = a.ow, g.oh = a.oh, g.extend = a.extend, g.fill = a.fill;
-        g.in_img = a.in_img, g.out_img = a.out_img;
-        g.strips = (a.ow + 255) / 256;
-        g.bands = (h + kE2RB - 1) / kE2RB;
-        int tab[(kTransformScale + 1) * 4];
-        bicubic_table(tab);
-        auto pk = [](int lo, int hi) { return (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16); };
-        g.e01 = pk(tab[96 * 4 + 0], tab[96 * 4 + 1]);
-        g.e23 = pk(tab[96 * 4 + 2], tab[96 * 4 + 3]);
-        g.o01 = pk(tab[32 * 4 + 0], tab[32 * 4 + 1]);
-        g.o23 = pk(tab[32 * 4 + 2], tab[32 * 4 + 3]);
-        g.out_aligned = (a.ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
-        g.seed = kInterpScale >> 1;
-        const long long tasks = static_cast<long long>(g.strips) * g.bands;
-        if ((tasks + 3) / 4 <= 0x7fffffffLL) {
-            const dim3 grid(static_cast<unsigned>((tasks + 3) / 4), n);
-            MIPX_DISPATCH_BANDS(b, hipLaunchKernelGGL(k_enlarge2<B_>, grid, dim3(256), 0, st, g));
-            return launch_check("k_enlarge2");
-        }
     }
     // the staged separable kernel: window spans from the positions, exact per tile size
     const char *es = tune_env("MIPX_AFFINE_SEP");  // 0: the per-pixel gather kernel (A/B)

@@ -423,10 +423,12 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
     const long long blocks = cols * a.segs;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
+#ifdef MIPX_PROBES
     if (tune_env("MIPX_BCOL_DBG"))
         fprintf(stderr, "k_bcol b=%d upw=%d a16=%d nks=%d kmax=%d taps=%d sxb=%d spb=%d e=%d sd=%d kb0=%d rsd=%d tw=%d ring=%d lds=%zu per_cu=%d strips=%d segs=%d seg_steps=%d pre=%d blocks=%lld\n",
                 b, upw, a.a16, nks, kmax, taps, a.sxb, a.spb, e, a.sd, a.kb0, a.rsd, a.tw, ring, lds, per_cu, a.strips, a.segs,
                 a.seg_steps, a.pre, blocks);
+#endif
     hipLaunchKernelGGL(reinterpret_cast<void (*)(BcArgs)>(const_cast<void *>(fn)), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBcNT), lds, st, a);
     return launch_check("k_bcol");

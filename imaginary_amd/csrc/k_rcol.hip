@@ -43,7 +43,6 @@
 
 #include "device_common.h"
 #include "lds_ops.h"
-#include "r2front.h"
 
 namespace mipx {
 namespace {
@@ -284,7 +283,8 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
             if (!wl[j]) continue;
-            const int off = rr[j] < a.rcap ? chunk_off(r0, j) : 0x7ffffff0;
+            // idle lanes: out of range for both loads, and (off & ~3) + 16 stays below 2^31
+            const int off = rr[j] < a.rcap ? chunk_off(r0, j) : 0x7fffffe0;
             rv[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
             if constexpr (UNAL)
                 re[P][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
@@ -497,447 +497,6 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
 
 int rc_start(int o, double s, int pad, bool centre) { return static_cast<int>(reduce_x_host(o, s, centre)) - pad; }
 
-// ===========================================================================
-// k_rchain: vips_reduce 2 x 2 followed by a k_rcol reduce (and its extract window) in
-// one launch — the /pipeline resize -> crop chain of C3 (reference image.go:379-410),
-// without the 2 x 2 output in HBM.
-//
-// The block is k_rcol's (a strip of 64 output pixels, 16-row steps, the same vertical
-// plan, horizontal operands, stores), but its LDS ring of 2 x 2-output rows is filled
-// by a producer ("front") inside the block instead of by loads:
-//   * front vertical, straight from HBM into the matrix cores (no input ring): a lane
-//     (n, kg) loads dword column n of input rows 4 kg .. 4 kg + 3 of a 16-row block,
-//     which is the B operand of v_mfma_i32_16x16x64_i8 with K = (row, byte); the A
-//     operand holds the 2 x 2 taps at M = (output row r < 3, byte c), so D lane (n, kg)
-//     is output row kg's dword n.  One group = 3 output rows (2r + 12 taps <= 16 rows),
-//     one constant A operand for every group; 5 groups = 15 rows per front step;
-//   * front horizontal = k_reduce2m's banded product: GP output pixels from a 64-byte
-//     window of each of the 15 vertical-result rows, written to the ring (- 128 form);
-//   * rows outside the 2 x 2 output (COPY edge) are copies of its first / last row.
-// Per 16-row step: front steps until the ring holds the rows the step reads, then
-// k_rcol's vertical and horizontal products.  The 2 x 2 sums are the ones k_reduce2x2
-// / k_reduce2m compute (taps of the phase the sampling convention gives, same
-// rounding), so the output is bit-identical to the two reduces run one after the other.
-// ===========================================================================
-constexpr int kChRing = 64;   // ring rows (power of two)
-constexpr int kChFR = 15;     // 2 x 2-output rows per front step (5 groups of 3)
-constexpr int kChFRows = 16;  // front intermediate rows allocated (the horizontal product reads 16)
-
-struct RchArgs {
-    const u8 *src;            // the original images (sw x sh x B); the 2 x 2 output is a.w x a.h
-    int sw, sh;
-    long long src_img;
-    const rc_u4 *fops;        // [64 lanes][vh, vl, wh, wl]: the front's MFMA operands (rch_operands)
-    int vseed, hseed;         // front seeds: 128 sum(T) + 2048 - (128 << 12) (results in - 128 form)
-    int fis;                  // front intermediate row stride (bytes)
-    float c0, c1, c3, c5, bias;  // FRONT 1: k_reduce2x2's corner taps / 4096 and its 2^-13 bias
-};
-
-// FRONT 0: the vertical pass straight from HBM into the matrix cores (r05 first build,
-// 15-row steps); FRONT 1: the vertical pass on the VALU as k_reduce2x2 makes it (corner
-// convention: every input row loaded once into a register ring of its odd rows, the next
-// 12-row chunk prefetched while this one is consumed), the horizontal on the matrix cores
-// W3: a build held to 3 waves per SIMD (168 VGPRs, a few spilled) instead of the
-// compiler's 2 (FRONT 1 only; MIPX_CHAIN_W3, A/B)
-template <int B, int NKS, int FRONT, int W3>
-__global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(W3 ? 3 : 1, 8))) k_rchain(RcArgs a, RchArgs c) {
-    using G = RCH<B>;
-    constexpr int FR = FRONT ? 12 : kChFR;  // 2 x 2-output rows per front step
-    constexpr int WV = kRcNT / 64, XW = 16 * WV, GP = G::GP;
-    constexpr int UPW = B;
-    extern __shared__ __attribute__((aligned(16))) uint32_t rcs[];
-    const uint32_t ring_l = rc_lds(rcs);                                         // [64][rs]
-    const uint32_t inter_l = ring_l + static_cast<uint32_t>(kChRing * a.rs);     // [16][iw] + wave tiles
-    constexpr int WSR = 16 * UPW + (UPW == 4 ? 16 : 0);
-    const uint32_t wst_l = inter_l + static_cast<uint32_t>(kRcRows * a.iw);
-    const uint32_t fint_l = wst_l + static_cast<uint32_t>(WV * kRcRows * WSR);   // [FR][fis]
-    u8 *fint = reinterpret_cast<u8 *>(rcs) + (fint_l - ring_l);
-    u8 *ring = reinterpret_cast<u8 *>(rcs);
-
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int strip = static_cast<int>(t % static_cast<uint32_t>(a.strips));
-    const int rest = static_cast<int>(t / static_cast<uint32_t>(a.strips));
-    const int seg = rest % a.segs;
-    const int img = __builtin_amdgcn_readfirstlane(rest / a.segs);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int n = lane & 15, kg = lane >> 4;
-
-    const int x0 = strip * XW, x_last = min(x0 + XW - 1, a.ow - 1);
-    const int vbytes = B * (x_last - x0 + 1);
-    int lo, hi, ph;
-    rc_pos(a.ox0 + x0, a.hs, a.hpad, &lo, &ph, a.centre);
-    rc_pos(a.ox0 + x_last, a.hs, a.hpad, &hi, &ph, a.centre);
-    hi += a.htaps - 1;
-    const int org = lo & (lo < 0 && B == 3 ? ~15 : ~3);
-    const int span = B * (hi - org + 1);
-    const int cpr = (span + 15) >> 4;
-    // front geometry: pixels org .. org + ni - 1 of the 2 x 2 output (covering the ring row)
-    const int ni = (((16 * cpr + B - 1) / B + GP - 1) / GP) * GP;
-    const int vst = 2 * org - 5;                // first front-intermediate pixel (input pixel index)
-    const int vb0 = (B * vst) & ~63;            // 64-byte aligned byte of the first column tile
-    const int ish = B * vst - vb0 + G::LOFF;    // LDS byte of front pixel 0 in a row; == SH (mod 8)
-    const int ntile = (ish - G::LOFF + B * (2 * ni + 10) + 63) >> 6;
-    const int ngr = ni / GP;
-    const int spitch = c.sw * B;
-
-    const int ka = a.k0 + seg * a.seg_steps;
-    const int steps = min(a.k0 + a.ksteps, ka + a.seg_steps) - ka;
-
-    const __amdgpu_buffer_rsrc_t src = image_rsrc(c.src + img * c.src_img, c.src_img);
-    const __amdgpu_buffer_rsrc_t prs = image_rsrc(a.plan, static_cast<long long>(a.plan_rows) * kRcolPlanRow);
-    rc_cint *srow = (rc_cint *)(a.plan + static_cast<size_t>(a.plan_rows) * kRcolPlanRow);
-    const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
-
-    // ---- back-end horizontal operands (k_rcol's, COPY edge folded) ----
-    rc_v4i th[UPW][NKS], tl[UPW][NKS];
-    int kb[UPW];
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) {
-        const int u = UPW * wave + i;
-        int sf, pf;
-        rc_pos(a.ox0 + min(x0 + (16 * u) / B, x_last), a.hs, a.hpad, &sf, &pf, a.centre);
-        kb[i] = __builtin_amdgcn_readfirstlane((B * (sf - org) + (16 * u) % B) & ~7);
-        const int o = 16 * u + n, xl = o / B, cc = o - B * xl;
-        int sp, pp;
-        rc_pos(a.ox0 + min(x0 + xl, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
-        const int lfold = -sp, rfold = sp + a.htaps - 1 - (a.w - 1);
-        const signed char *rh =
-            lfold > 0 ? a.tabhf + ((static_cast<size_t>(lfold - 1) * (kTransformScale + 1) + pp) * 2) * kRsTabW
-            : rfold > 0 ? a.tabhf + ((static_cast<size_t>(a.htaps - 1 + rfold - 1) * (kTransformScale + 1) + pp) * 2) * kRsTabW
-                        : a.tabh + static_cast<size_t>(pp) * 2 * kRsTabW;
-        const bool both = lfold > 0 && rfold > 0;
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            const int j0 = kb[i] + 64 * ks + 16 * kg;
-            if (both) {
-                rc_edge_frag(a.tabf, a.htaps, pp, sp, cc, j0, org, a.w, B, &th[i][ks], &tl[i][ks]);
-            } else {
-                const int off = kRsTabPad + j0 - cc - B * (sp - org);
-                th[i][ks] = rc_frag16(rh, off);
-                tl[i][ks] = rc_frag16(rh + kRsTabW, off);
-            }
-        }
-    }
-    rc_v4i hb[UPW];
-#pragma unroll
-    for (int i = 0; i < UPW; ++i) {
-        const int e = 16 * (UPW * wave + i) + 4 * kg;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int sp, pp;
-            rc_pos(a.ox0 + min(x0 + (e + j) / B, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
-            hb[i][j] = 128 * a.sumh[pp] + 2048;
-        }
-    }
-    // ---- front operands ----
-    const rc_u4 *fo = c.fops + 4 * lane;
-    const rc_v4i fvh = __builtin_bit_cast(rc_v4i, fo[0]), fvl = __builtin_bit_cast(rc_v4i, fo[1]);
-    const rc_v4i fwh = __builtin_bit_cast(rc_v4i, fo[2]), fwl = __builtin_bit_cast(rc_v4i, fo[3]);
-    const int vsd = c.vseed, hsd = c.hseed;
-
-    // COPY edge of the front's input columns: front pixels [0, nl) copy pixel nl, [fr, ...) pixel fr - 1
-    const int nl = vst < 0 ? -vst : 0;
-    const int fr = c.sw - vst;
-    const int fr_end = 2 * ni + 9;
-    const int nr = fr_end >= fr ? fr_end - fr + 1 : 0;
-    const bool fedge = nl > 0 || nr > 0;
-
-    // ---- front step: 2 x 2-output rows P .. P + 14 into the ring ----
-    auto front = [&](int P) {
-        const int hh = a.h;  // rows of the 2 x 2 output
-        if constexpr (FRONT == 0) {
-        if (P < hh) {
-            // vertical: wave-dealt 64-byte column tiles; 5 groups of 3 rows, 20 loads per lane in flight
-            for (int tl_ = wave; tl_ < ntile; tl_ += WV) {
-                const int cb = vb0 + 64 * tl_ + 4 * n;
-                const bool cin = cb >= 0 && cb < spitch;
-                uint32_t v[5][4];
-#pragma unroll
-                for (int g = 0; g < 5; ++g)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int r = 2 * (P + 3 * g) - 5 + 4 * kg + j;
-                        v[g][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(
-                            src, cin ? clampi(r, 0, c.sh - 1) * spitch + cb : 0x7ffffff0, 0, 0));
-                    }
-                const uint32_t fw = fint_l + static_cast<uint32_t>(kg * c.fis + 64 * tl_ + 4 * n + G::LOFF);
-#pragma unroll
-                for (int g = 0; g < 5; ++g) {
-                    const rc_v4i bv = rc_v4i{static_cast<int>(v[g][0] ^ 0x80808080u), static_cast<int>(v[g][1] ^ 0x80808080u),
-                                             static_cast<int>(v[g][2] ^ 0x80808080u), static_cast<int>(v[g][3] ^ 0x80808080u)};
-                    rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{vsd, vsd, vsd, vsd};
-                    dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(fvh, bv, dh, 0, 0, 0);
-                    dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(fvl, bv, dl, 0, 0, 0);
-                    if (kg < 3)
-                        lds_wr32(fw + static_cast<uint32_t>(3 * g * c.fis),
-                                 rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
-                                            (dh[3] << 6) + dl[3]));
-                }
-            }
-            rc_barrier();
-            if (fedge) {  // EXTEND_COPY of the input columns, per byte
-                const int nfill = nl + nr;
-                for (int i = tid; i < FR * nfill * B; i += kRcNT) {
-                    const int u = i / (nfill * B);
-                    const int rem = i - u * nfill * B;
-                    const int f = rem / B, ch = rem - f * B;
-                    const int d = f < nl ? f : fr + (f - nl);
-                    const int sp = f < nl ? nl : fr - 1;
-                    fint[u * c.fis + ish + B * d + ch] = fint[u * c.fis + ish + B * sp + ch];
-                }
-                rc_barrier();
-            }
-            // horizontal: groups of GP pixels, 4 groups' windows under one wait
-            const uint32_t fb = fint_l + static_cast<uint32_t>(n * c.fis + (ish & ~7) + 16 * kg);
-            const bool wrow = n < FR && 4 * kg < B * GP;
-            const uint32_t rrow = ring_l + static_cast<uint32_t>(((P + n) & (kChRing - 1)) * a.rs + 4 * kg);
-            for (int q0 = wave; q0 < ngr; q0 += 4 * WV) {
-                rc_u2x2 bq[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) bq[i] = lds_rd64x2(fb + static_cast<uint32_t>(2 * B * GP * min(q0 + WV * i, ngr - 1)));
-                lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3]);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int q = q0 + WV * i;
-                    const rc_v4i bv = __builtin_bit_cast(rc_v4i, rc_join(bq[i]));
-                    rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{hsd, hsd, hsd, hsd};
-                    dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwh, bv, dh, 0, 0, 0);
-                    dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwl, bv, dl, 0, 0, 0);
-                    if (wrow && q < ngr)
-                        lds_wr32(rrow + static_cast<uint32_t>(B * GP * q),
-                                 rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2],
-                                            (dh[3] << 6) + dl[3]));
-                }
-            }
-        }
-        // rows outside the 2 x 2 output: copies of its first / last row (COPY edge of the
-        // second reduce's vertical pass)
-        if (P < 0 || P + FR > hh) {
-            rc_barrier();
-            const int rb = a.rs;  // bytes per ring row copied (>= 16 cpr)
-            for (int i = tid; i < FR * (rb >> 2); i += kRcNT) {
-                const int u = i / (rb >> 2), d = i - u * (rb >> 2);
-                const int R = P + u;
-                if (R >= 0 && R < hh) continue;
-                const int S = R < 0 ? 0 : hh - 1;
-                reinterpret_cast<uint32_t *>(ring + (R & (kChRing - 1)) * a.rs)[d] =
-                    reinterpret_cast<const uint32_t *>(ring + (S & (kChRing - 1)) * a.rs)[d];
-            }
-        }
-        }
-    };
-
-    // ---- FRONT 1: VALU vertical (k_reduce2x2's register ring), matrix-core horizontal ----
-    typedef float f4v_ __attribute__((ext_vector_type(4)));
-    auto cvt4 = [](uint32_t v) { return f4v_{ubyte_once<0>(v), ubyte_once<1>(v), ubyte_once<2>(v), ubyte_once<3>(v)}; };
-    auto tap7 = [&](float e, float m1, float p1, float m3, float p3, float m5, float p5) {
-        float acc = __builtin_fmaf(c.c0, e, c.bias);
-        acc = __builtin_fmaf(c.c1, m1 + p1, acc);
-        acc = __builtin_fmaf(c.c3, m3 + p3, acc);
-        return __builtin_fmaf(c.c5, m5 + p5, acc);
-    };
-    auto pack4 = [](float x, float y, float z, float w) {
-        uint32_t v = __builtin_amdgcn_cvt_pk_u8_f32(x, 0, 0u);
-        v = __builtin_amdgcn_cvt_pk_u8_f32(y, 1, v);
-        v = __builtin_amdgcn_cvt_pk_u8_f32(z, 2, v);
-        return __builtin_amdgcn_cvt_pk_u8_f32(w, 3, v);
-    };
-    const int ib = vb0 + 4 * tid;  // the lane's input dword (front intermediate dword tid)
-    const int nd = (ish - G::LOFF + B * (2 * ni + 10) + 3) >> 2;
-    const bool vlane = tid < nd;
-    const uint32_t voff = vlane && ib >= 0 && ib + 4 <= spitch ? static_cast<uint32_t>(ib) : 0x80000000u;
-    auto load_row = [&](int r) -> uint32_t {
-        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(
-            src, voff, __builtin_amdgcn_readfirstlane(clampi(r, 0, c.sh - 1) * spitch), 0));
-    };
-    f4v_ vring[6];
-    uint32_t podd[12], pevn[12];
-    auto front2_init = [&](int Q) {  // Q: a multiple of 12
-        if constexpr (FRONT == 1) {
-            vring[3] = cvt4(load_row(2 * (Q - 3) + 1));
-            vring[4] = cvt4(load_row(2 * (Q - 2) + 1));
-            vring[5] = cvt4(load_row(2 * (Q - 1) + 1));
-            vring[0] = cvt4(load_row(2 * Q + 1));
-            vring[1] = cvt4(load_row(2 * (Q + 1) + 1));
-            vring[2] = f4v_{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int u = 0; u < 12; ++u) {
-                podd[u] = load_row(2 * (Q + u + 2) + 1);
-                pevn[u] = load_row(2 * (Q + u));
-            }
-        }
-    };
-    auto front2 = [&](int Q) {
-        const int hh = a.h;
-        if constexpr (FRONT == 1) {
-            const uint32_t fw = fint_l + static_cast<uint32_t>(G::LOFF + 4 * tid);
-#pragma unroll
-            for (int u = 0; u < 12; ++u) {
-                vring[(u + 2) % 6] = cvt4(podd[u]);
-                const f4v_ e = cvt4(pevn[u]);
-                podd[u] = load_row(2 * (Q + 12 + u + 2) + 1);  // the next chunk's rows, in flight from here
-                pevn[u] = load_row(2 * (Q + 12 + u));
-                const f4v_ m5 = vring[(u + 3) % 6], m3 = vring[(u + 4) % 6], m1 = vring[(u + 5) % 6];
-                const f4v_ p1 = vring[u % 6], p3 = vring[(u + 1) % 6], p5 = vring[(u + 2) % 6];
-                const uint32_t d = pack4(tap7(e.x, m1.x, p1.x, m3.x, p3.x, m5.x, p5.x),
-                                         tap7(e.y, m1.y, p1.y, m3.y, p3.y, m5.y, p5.y),
-                                         tap7(e.z, m1.z, p1.z, m3.z, p3.z, m5.z, p5.z),
-                                         tap7(e.w, m1.w, p1.w, m3.w, p3.w, m5.w, p5.w));
-                if (vlane) lds_wr32(fw + static_cast<uint32_t>(u * c.fis), d ^ 0x80808080u);
-            }
-            rc_barrier();
-            if (fedge) {  // EXTEND_COPY of the input columns, per byte
-                const int nfill = nl + nr;
-                for (int i = tid; i < FR * nfill * B; i += kRcNT) {
-                    const int u = i / (nfill * B);
-                    const int rem = i - u * nfill * B;
-                    const int f = rem / B, ch = rem - f * B;
-                    const int d = f < nl ? f : fr + (f - nl);
-                    const int sp = f < nl ? nl : fr - 1;
-                    fint[u * c.fis + ish + B * d + ch] = fint[u * c.fis + ish + B * sp + ch];
-                }
-                rc_barrier();
-            }
-            const uint32_t fb = fint_l + static_cast<uint32_t>(n * c.fis + (ish & ~7) + 16 * kg);
-            const bool wrow = n < FR && 4 * kg < B * GP;
-            const uint32_t rrow = ring_l + static_cast<uint32_t>(((Q + n) & (kChRing - 1)) * a.rs + 4 * kg);
-            for (int q0 = wave; q0 < ngr; q0 += 4 * WV) {
-                rc_u2x2 bq[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) bq[i] = lds_rd64x2(fb + static_cast<uint32_t>(2 * B * GP * min(q0 + WV * i, ngr - 1)));
-                lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3]);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const rc_v4i bv = __builtin_bit_cast(rc_v4i, rc_join(bq[i]));
-                    const rc_v4i dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwh, bv, rc_v4i{0, 0, 0, 0}, 0, 0, 0);
-                    const rc_v4i dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwl, bv, rc_v4i{hsd, hsd, hsd, hsd}, 0, 0, 0);
-                    if (wrow && q0 + WV * i < ngr)
-                        lds_wr32(rrow + static_cast<uint32_t>(B * GP * (q0 + WV * i)),
-                                 rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
-                }
-            }
-            // rows outside the 2 x 2 output: those past its last row in this chunk, and with
-            // the first chunk (chunks start at row 0, never above it) the up to 11 rows above row 0
-            if (Q == 0 || Q + FR > hh) {
-                rc_barrier();
-                const int rb = a.rs, u0 = Q == 0 ? -11 : 0;
-                for (int i = tid; i < (FR - u0) * (rb >> 2); i += kRcNT) {
-                    const int u = u0 + i / (rb >> 2), d = i - (u - u0) * (rb >> 2);
-                    const int R = Q + u;
-                    if (R >= 0 && R < hh) continue;
-                    const int S = R < 0 ? 0 : hh - 1;
-                    reinterpret_cast<uint32_t *>(ring + (R & (kChRing - 1)) * a.rs)[d] =
-                        reinterpret_cast<const uint32_t *>(ring + (S & (kChRing - 1)) * a.rs)[d];
-                }
-            }
-        }
-    };
-
-    // ---- back end: k_rcol's vertical / horizontal / stores ----
-    const int toff = n * kRcolPlanRow + 16 * kg;
-    const int wrow_ = min(lane / UPW, kRcRows - 1), wch = lane - UPW * (lane / UPW);
-    const int we = 16 * (UPW * wave + wch);
-    const uint32_t wst_w = wst_l + static_cast<uint32_t>(wave * kRcRows * WSR);
-    int P = srow[2 * ka];  // next ring row to produce
-    if constexpr (FRONT == 1) {  // chunks on multiples of 12 (the register ring's slot map)
-        P = P >= 0 ? P / 12 * 12 : 0;  // rows above row 0 are copies of it, filled with chunk 0
-        front2_init(P);
-    }
-    for (int k = ka; k < ka + steps; ++k) {
-        const int o = k * (kRcRows * kRcolPlanRow);
-        const rc_v4i bh = __builtin_bit_cast(rc_v4i, __builtin_amdgcn_raw_buffer_load_b128(prs, toff + o, 0, 0));
-        const rc_v4i bl = __builtin_bit_cast(rc_v4i, __builtin_amdgcn_raw_buffer_load_b128(prs, toff + o + 64, 0, 0));
-        const int sd = __builtin_amdgcn_raw_buffer_load_b32(prs, n * kRcolPlanRow + 128 + o, 0, 0);
-        const int bk = srow[2 * k], ek = srow[2 * k + 1];
-        bool first = true;
-        while (P < ek) {
-            if (!first) rc_barrier();  // the front intermediate is free again
-            if (FRONT == 1) front2(P);
-            else front(P);
-            P += FR;
-            first = false;
-        }
-        rc_barrier();  // ring rows of step k complete; the back intermediate free
-        {
-            const int r1 = bk + 8 * kg + (n >> 1);
-            const uint32_t a1 = ring_l + static_cast<uint32_t>((r1 & (kChRing - 1)) * a.rs + 8 * (n & 1));
-            const uint32_t a2 = ring_l + static_cast<uint32_t>(((r1 + 32) & (kChRing - 1)) * a.rs + 8 * (n & 1));
-            const uint32_t iq = inter_l + static_cast<uint32_t>(n * a.iw + 4 * kg);
-            for (int ct = wave; ct < cpr; ct += 2 * WV) {
-                const bool two = ct + WV < cpr;
-                rc_v2i t1a = lds_tr8(a1 + 16 * ct), t2a = lds_tr8(a2 + 16 * ct);
-                rc_v2i t1b = t1a, t2b = t2a;
-                if (two) {
-                    t1b = lds_tr8(a1 + 16 * (ct + WV));
-                    t2b = lds_tr8(a2 + 16 * (ct + WV));
-                }
-                lgkm_wait_for<0>(t1a, t2a, t1b, t2b);
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    if (hh == 1 && !two) break;
-                    const rc_v4i av = hh ? rc_v4i{t1b.x, t1b.y, t2b.x, t2b.y} : rc_v4i{t1a.x, t1a.y, t2a.x, t2a.y};
-                    rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
-                    dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bh, dh, 0, 0, 0);
-                    dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bl, dl, 0, 0, 0);
-                    lds_wr32(iq + 16 * (ct + WV * hh), rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1],
-                                                                  (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
-                }
-            }
-        }
-        rc_barrier();  // the intermediate complete
-        uint32_t res[UPW];
-        {
-            rc_u2x2 q[UPW][NKS];
-#pragma unroll
-            for (int i = 0; i < UPW; ++i) {
-                const uint32_t ir = inter_l + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg);
-#pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) q[i][ks] = lds_rd64x2(ir + 64 * ks);
-            }
-#pragma unroll
-            for (int i = 0; i < UPW; ++i)
-#pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) rc_pin(q[i][ks]);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int i = 0; i < UPW; ++i) {
-                rc_v4i ah = rc_v4i{0, 0, 0, 0}, al = hb[i];
-#pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) {
-                    rc_pin(q[i][ks]);
-                    const rc_v4i bz = __builtin_bit_cast(rc_v4i, rc_join(q[i][ks]));
-                    ah = __builtin_amdgcn_mfma_i32_16x16x64_i8(th[i][ks], bz, ah, 0, 0, 0);
-                    al = __builtin_amdgcn_mfma_i32_16x16x64_i8(tl[i][ks], bz, al, 0, 0, 0);
-                }
-                res[i] = rc_round4((ah[0] << 6) + al[0], (ah[1] << 6) + al[1], (ah[2] << 6) + al[2], (ah[3] << 6) + al[3]);
-            }
-        }
-        // stores: the wave's 16 rows x 16 UPW bytes through its LDS tile, 16-byte row pieces
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) lds_wr32(wst_w + static_cast<uint32_t>(n * WSR + 16 * i + 4 * kg), res[i]);
-        rc_u4 qv;
-        {
-            rc_u2x2 qq = lds_rd64x2(wst_w + static_cast<uint32_t>(wrow_ * WSR + 16 * wch));
-            lgkm_wait_for<0>(qq);
-            qv = rc_join(qq);
-        }
-        const int orow = k * kRcRows + wrow_ - a.oy0;
-        const bool ok = lane < 16 * UPW && orow >= 0 && orow < a.oh;
-        const int base = orow * a.ow * B + B * x0 + we;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, qv), dst, ok && we + 16 <= vbytes ? base : 0x7ffffff0, 0, 0);
-        if (a.wst == 2) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                __builtin_amdgcn_raw_buffer_store_b32(qv[j], dst, ok && we + 16 > vbytes && we + 4 * j < vbytes ? base + 4 * j : 0x7ffffff0, 0, 0);
-        } else if (a.wst == 3 && B * x0 + 16 * UPW * WV >= a.ow * B) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(qv[j >> 2] >> (8 * (j & 3))), dst,
-                                                     ok && we + 16 > vbytes && we + j < vbytes ? base + j : 0x7ffffff0, 0, 0);
-        }
-    }
-}
 
 }  // namespace
 
@@ -1141,175 +700,5 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     return launch_check("k_rcol");
 }
 
-// vips_reduce(2, 2) then vips_reduce(hs, vs) over output window [ox0, ox0 + ow) x [oy0,
-// oy0 + oh) of the second, in one launch (k_rchain); MIPX_EUNSUPPORTED when the pair is
-// outside the fused kernel's envelope (the caller runs the two reduces).  taps12: the 2 x 2
-// reduce's 12 taps from 2x - 5 at the convention's phase (reduce2_front_taps).
-int reduce2_chain_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double hs, double vs, int ox0, int oy0,
-                         int ow, int oh, const int *taps12, hipStream_t st) {
-    if ((b != 3 && b != 4) || !(hs > 1.0) || !(vs > 1.0)) return MIPX_EUNSUPPORTED;
-    // MIPX_CHAIN=1 / 2 (tests: 2 = the chained kernel or an error); unset or 0: the two
-    // reduces.  Off by default: on C3 the chain measures 3.90 ms per step against 2.43 ms
-    // for k_reduce2x2 + k_rcol (profiles/r05/c3_chain_ab.jsonl)
-    const char *ech = tune_env("MIPX_CHAIN");
-    if (!(ech && (*ech == '1' || *ech == '2'))) return MIPX_EUNSUPPORTED;
-    const int w2 = out_size_reduce(w, 2.0), h2 = out_size_reduce(h, 2.0);
-    const long long src_img = img_bytes(w, h, b), out_img = img_bytes(ow, oh, b);
-    if (src_img >= 0x7fffffffLL - 64 || out_img >= (1LL << 29)) return MIPX_EUNSUPPORTED;
-    if ((w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0) return MIPX_EUNSUPPORTED;
-    const bool out_al = (ow * b) % 4 == 0 && reinterpret_cast<uintptr_t>(out) % 4 == 0;
-    const int vtaps = reduce_points(vs), htaps = reduce_points(hs);
-    if (vtaps > 16 || htaps > 16) return MIPX_EUNSUPPORTED;
-    const bool centre = reduce_centre();
-    const int vpad = vtaps / 2 - 1;
-    RcArgs a{};
-    a.in = nullptr;
-    a.out = out;
-    a.w = w2;
-    a.h = h2;
-    a.ox0 = ox0;
-    a.oy0 = oy0;
-    a.ow = ow;
-    a.oh = oh;
-    a.in_img = img_bytes(w2, h2, b);
-    a.out_img = out_img;
-    a.htaps = htaps;
-    a.hpad = htaps / 2 - 1;
-    a.hs = hs;
-    a.centre = centre;
-    a.k0 = oy0 / kRcRows;
-    const int k1 = (oy0 + oh - 1) / kRcRows;
-    a.ksteps = k1 - a.k0 + 1;
-    auto gb = [&](int k) { return rc_start(kRcRows * k, vs, vpad, centre); };
-    auto ge = [&](int k) { return rc_start(kRcRows * k + kRcRows - 1, vs, vpad, centre) + vtaps; };
-    // the front: FRONT 1 (VALU vertical, corner convention only) unless forced
-    // (MIPX_CHAIN_FRONT=0 / 1, A/B); FRONT 0 for the centre convention
-    const char *efr = tune_env("MIPX_CHAIN_FRONT");
-    int front = (efr && *efr) ? (*efr == '1' && !centre ? 1 : 0) : (centre ? 0 : 1);
-    // FRONT 1 holds a strip's input row in one dword per lane: wider strips (shrinks past
-    // ~1.55 on RGBA) take FRONT 0
-    for (int x0 = 0; front && x0 < ow; x0 += 64) {
-        const int xl = std::min(x0 + 63, ow - 1);
-        const int lo = rc_start(ox0 + x0, hs, a.hpad, centre), hi = rc_start(ox0 + xl, hs, a.hpad, centre) + htaps - 1;
-        const int org = lo & (lo < 0 && b == 3 ? ~15 : ~3);
-        const int cpr = (b * (hi - org + 1) + 15) >> 4;
-        const int gpf = b == 3 ? RCH<3>::GP : RCH<4>::GP;
-        const int ni = (((16 * cpr + b - 1) / b + gpf - 1) / gpf) * gpf;
-        const int vst = 2 * org - 5, ish = b * vst - ((b * vst) & ~63);  // (LOFF cancels)
-        if ((ish + b * (2 * ni + 10) + 3) / 4 > kRcNT) front = 0;
-    }
-    const int fr = front ? 12 : kChFR, falign = front ? 11 : 0;
-    for (int k = a.k0; k <= k1; ++k) {
-        if (ge(k) - gb(k) > 64) return MIPX_EUNSUPPORTED;  // the MFMA K
-        // the ring holds the step's rows plus one front step past its end (and, FRONT 1, the
-        // rows a 12-aligned chunk makes above the step's first)
-        if (ge(k) + fr - 1 + falign - gb(k) > kChRing) return MIPX_EUNSUPPORTED;
-    }
-    int cpr_max = 0, nks = 0, kbmax = 0, fbytes_max = 0, ni_max = 0;
-    const int gp = b == 3 ? RCH<3>::GP : RCH<4>::GP;
-    for (int x0 = 0; x0 < ow; x0 += 64) {
-        const int xl = std::min(x0 + 63, ow - 1);
-        const int lo = rc_start(ox0 + x0, hs, a.hpad, centre), hi = rc_start(ox0 + xl, hs, a.hpad, centre) + htaps - 1;
-        const int org = lo & (lo < 0 && b == 3 ? ~15 : ~3);
-        const int cpr = (b * (hi - org + 1) + 15) >> 4;
-        cpr_max = std::max(cpr_max, cpr);
-        const int ni = (((16 * cpr + b - 1) / b + gp - 1) / gp) * gp;
-        ni_max = std::max(ni_max, ni);
-        const int loff = b == 3 ? RCH<3>::LOFF : RCH<4>::LOFF;
-        const int vst = 2 * org - 5, vb0 = (b * vst) & ~63, ish = b * vst - vb0 + loff;
-        if ((ish & 7) != (b == 3 ? RCH<3>::SH : RCH<4>::SH)) return MIPX_EINVAL;  // the operand's window shift
-        const int ntile = (ish - loff + b * (2 * ni + 10) + 63) >> 6;
-        fbytes_max = std::max({fbytes_max, 64 * ntile + loff, (ish & ~7) + 2 * b * gp * (ni / gp - 1) + 64});
-        for (int u = 0; u < 64 * b / 16; ++u) {
-            const int o0 = 16 * u, o1 = 16 * u + 15;
-            if (x0 + o0 / b > xl) break;
-            const int xf = x0 + o0 / b, xe = std::min(x0 + o1 / b, xl);
-            const int kbu = (b * (rc_start(ox0 + xf, hs, a.hpad, centre) - org) + o0 % b) & ~7;
-            const int need = b * (rc_start(ox0 + xe, hs, a.hpad, centre) + htaps - 1 - org) + b;
-            nks = std::max(nks, (need - kbu + 63) / 64);
-            kbmax = std::max(kbmax, kbu);
-        }
-    }
-    if (nks > 2) return MIPX_EUNSUPPORTED;
-    // dwords, a multiple of 4 (the transposed reads need 8-byte rows; the vertical tiles are 16
-    // bytes): the column tiles and every pixel the front writes
-    int rs = 4 * std::max(cpr_max, (b * ni_max + 15) / 16);
-    while (((rs & 63) >> 2) % 2 == 0) rs += 4;
-    a.rs = 4 * rs;
-    int iw = (std::max(16 * cpr_max, kbmax + 64 * nks) + 16 + 15) & ~15;
-    while ((iw / 4) % 8 != 4) iw += 16;
-    a.iw = iw;
-    int fis = (fbytes_max + 15) & ~15;
-    while ((fis / 4) % 32 % 4 != 2) fis += 8;  // 16 rows x 2 dwords of a half-wave's writes on distinct banks (k_reduce2m)
-    RchArgs c{};
-    c.src = in;
-    c.sw = w;
-    c.sh = h;
-    c.src_img = src_img;
-    c.fis = fis;
-    const size_t lds = static_cast<size_t>(kChRing) * a.rs + static_cast<size_t>(kRcRows) * iw +
-                       static_cast<size_t>(4 * kRcRows * (16 * b + (b == 4 ? 16 : 0))) +
-                       static_cast<size_t>(kChFRows) * fis;
-    if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
-
-    int plan_rows = 0;
-    a.plan = device_rcol_vplan(vs, centre, kRcRows * (k1 + 3), &plan_rows);
-    a.plan_rows = plan_rows;
-    int nth = 0, ntf = 0, nfh = 0;
-    const int *sumh = nullptr;
-    if (!a.plan || !device_reduce_i8(hs, &nth, &sumh)) return MIPX_EDEVICE;
-    a.sumh = sumh;
-    a.tabh = device_reduce_i8s(hs, b, &nth);
-    a.tabf = device_reduce_table(hs, &ntf);
-    a.tabhf = device_reduce_i8s_fold(hs, b, &nfh);
-    if (!a.tabh || !a.tabf || !a.tabhf || nth != htaps || ntf != htaps || nfh != htaps) return MIPX_EDEVICE;
-    a.wst = !out_al ? 3 : (ow * b) % 16 == 0 ? 1 : 2;
-    int sum = 0;
-    for (int i = 0; i < 12; ++i) {
-        sum += taps12[i];
-        if (taps12[i] < -128 * 64 || taps12[i] > 127 * 64 + 63) return MIPX_EUNSUPPORTED;
-    }
-    const std::vector<uint32_t> ops = b == 3 ? rch_operands<3>(taps12) : rch_operands<4>(taps12);
-    c.fops = static_cast<const rc_u4 *>(device_blob(ops.data(), ops.size() * sizeof(uint32_t)));
-    if (!c.fops) return MIPX_EDEVICE;
-    c.vseed = c.hseed = 128 * sum + 2048 - (128 << 12);
-
-    if (front) {
-        float cc[4];
-        if (!reduce2_taps(cc)) return MIPX_EUNSUPPORTED;
-        c.c0 = cc[0] / 4096.0f, c.c1 = cc[1] / 4096.0f, c.c3 = cc[2] / 4096.0f, c.c5 = cc[3] / 4096.0f;
-        c.bias = 1.0f / 8192.0f;
-    }
-    const void *fn = nullptr;
-    const char *ew3 = tune_env("MIPX_CHAIN_W3");
-    const bool w3 = !(ew3 && *ew3 == '0');
-#define MIPX_RCH(B_, NKS_)                                                                                     \
-    fn = front ? (w3 ? reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 1, 1>)                              \
-                     : reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 1, 0>))                             \
-               : reinterpret_cast<const void *>(&k_rchain<B_, NKS_, 0, 0>);
-    if (b == 3) {
-        if (nks == 1) { MIPX_RCH(3, 1) } else { MIPX_RCH(3, 2) }
-    } else {
-        if (nks == 1) { MIPX_RCH(4, 1) } else { MIPX_RCH(4, 2) }
-    }
-#undef MIPX_RCH
-    // segments: one per strip unless the grid would not fill the device (a segment's first
-    // front steps re-make the rows above its first step)
-    a.strips = (ow + 63) / 64;
-    const long long cols = static_cast<long long>(a.strips) * n;
-    const long long slots = static_cast<long long>(device_cu_count()) * occupancy_per_cu(fn, kRcNT, lds, 2);
-    const char *esg = tune_env("MIPX_CHAIN_SEGS");
-    int segs = 1;
-    if (esg && *esg) segs = std::max(1, std::atoi(esg));
-    else
-        while (cols * segs < 2 * slots && a.ksteps / (segs + 1) >= 8) ++segs;
-    a.seg_steps = (a.ksteps + segs - 1) / segs;
-    a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
-    const long long blocks = cols * a.segs;
-    if (!grid_ok(blocks)) return MIPX_EINVAL;
-    hipLaunchKernelGGL(reinterpret_cast<void (*)(RcArgs, RchArgs)>(const_cast<void *>(fn)),
-                       dim3(static_cast<unsigned>(blocks)), dim3(kRcNT), lds, st, a, c);
-    return launch_check("k_rchain");
-}
 
 }  // namespace mipx

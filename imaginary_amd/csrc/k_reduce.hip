@@ -88,7 +88,6 @@ struct Reduce2Args {
     float c0, c1, c3, c5, bias;
     int remap;       // XCD-aware tile order (MIPX_R2_REMAP=0 disables, for A/B)
     int band_major;  // tile order inside an XCD range (MIPX_R2_ORDER=1: bands fastest)
-    int walk;        // strips one workgroup walks left to right (MIPX_R2_WALK, A/B; 1 = one tile)
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -373,25 +372,6 @@ __global__ void __launch_bounds__(R2T<(VAR & 128) ? 2 : (VAR & 64) ? 1 : 0>::kTh
     reduce2_tile<B, R, PF, PK, MEM, LAUX, NTS, WIDE, TIGHT>(a, img, strip, band, lds);
 }
 
-// VERDICT r4 item 7, an access-order experiment: a workgroup owns a band and walks `walk`
-// consecutive strips of it left to right, so each of its input rows is read as one
-// sequential run across those strips (the default grid has the strips of a band on
-// neighbouring workgroups instead).  Same tile code, so the output is identical.
-template <int B>
-__global__ void __launch_bounds__(R2T<1>::kThreads) k_reduce2w(Reduce2Args a) {
-    __shared__ uint32_t lds[2 * 12 * R2T<1>::kPitch];
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int groups = (a.n_strips + a.walk - 1) / a.walk;
-    const int grp = t % groups;
-    const int rest = t / groups;
-    const int band = rest % a.n_bands, img = rest / a.n_bands;
-    const int s1 = min(a.n_strips, (grp + 1) * a.walk);
-    for (int strip = grp * a.walk; strip < s1; ++strip) {
-        reduce2_tile<B, 12, true, false, false, 0, false, 1, 0>(a, img, strip, band, lds);
-        __syncthreads();  // the next tile's first vertical pass reuses the LDS image
-    }
-}
-
 
 }  // namespace
 
@@ -528,19 +508,6 @@ bool reduce2c_taps(float t[6]) {
     return true;
 }
 
-// The 2 x 2 reduce's 12 taps from 2x - 5 under the current sampling convention (corner:
-// phase 0, whose taps 11 and 12 are zero; centre: phase 64, whose tap 12 is zero), for
-// the chained kernel (k_rchain); false when tap 12 is not zero.
-bool reduce2_front_taps(int taps[12]) {
-    std::vector<int> tab;
-    reduce_table(2.0, tab);
-    const int n = reduce_points(2.0);
-    if (n != 13) return false;
-    const int *r = tab.data() + (reduce_centre() ? 64 : 0) * n;
-    if (r[12] != 0) return false;
-    for (int i = 0; i < 12; ++i) taps[i] = r[i];
-    return true;
-}
 
 // Fused path applies to shrink exactly 2 x 2 on 3- or 4-band images whose rows
 // are dword aligned: k_reduce2x2 at the corner convention, k_reduce2m at the centre one.
@@ -582,14 +549,6 @@ int reduce2_launch(const u8 *in, u8 *out, int n, int w, int h, int b, hipStream_
 // Every computed pixel is the same sum as in the full launch.
 int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x0, int y0, int x1, int y1,
                           hipStream_t st) {
-    // MIPX_R2D: 1 = k_reduce2d (no input ring) at either convention, 0 = off (A/B; r05)
-    const char *ed = tune_env("MIPX_R2D");
-    if (ed && *ed == '1') {
-        int taps[12];
-        if (!reduce2_front_taps(taps)) return MIPX_EINVAL;
-        const int e = reduce2d_window_launch(in, out, n, w, h, b, x0, y0, x1, y1, taps, st);
-        if (e != MIPX_EUNSUPPORTED) return e;
-    }
     if (reduce_centre()) {  // k_reduce2m: both passes on the matrix cores
         float tf[6];
         if (!reduce2c_taps(tf)) return MIPX_EINVAL;
@@ -636,14 +595,6 @@ int reduce2_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int
     a.band_major = (eo && *eo) ? std::atoi(eo) : 0;
     const long long tiles = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (tiles > 0x7fffffffLL) return MIPX_EINVAL;
-    const char *ew = tune_env("MIPX_R2_WALK");
-    a.walk = (ew && *ew) ? std::max(1, std::atoi(ew)) : 1;
-    if (a.walk > 1 && var == 66) {
-        const long long wg = static_cast<long long>((a.n_strips + a.walk - 1) / a.walk) * a.n_bands * n;
-        if (b == 3) hipLaunchKernelGGL(k_reduce2w<3>, dim3(static_cast<unsigned>(wg)), dim3(R2T<1>::kThreads), 0, st, a);
-        else hipLaunchKernelGGL(k_reduce2w<4>, dim3(static_cast<unsigned>(wg)), dim3(R2T<1>::kThreads), 0, st, a);
-        return launch_check("k_reduce2w");
-    }
     dim3 grid(static_cast<unsigned>(tiles));
 #define MIPX_R2(V)                                                                                      \
     case V: {                                                                                           \

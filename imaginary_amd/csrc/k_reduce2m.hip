@@ -40,7 +40,6 @@
 
 #include "device_common.h"
 #include "lds_ops.h"
-#include "r2front.h"
 
 namespace mipx {
 namespace {
@@ -320,204 +319,6 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     }
 }
 
-// ===========================================================================
-// k_reduce2d: the 2 x 2 reduce with no input ring (r05).  The front of k_rchain
-// (r2front.h): the vertical pass straight from HBM into the matrix cores (dword loads,
-// 5 groups of 3 output rows per 15-row step, all loads of the next step in flight while
-// this step's horizontal pass and stores run), the horizontal pass as k_reduce2m's banded
-// product, the result through an LDS output tile as 16-byte row pieces.  Either sampling
-// convention (the taps of its phase); two barriers per 15-row step and ~17 KB of LDS.
-// ===========================================================================
-template <int B>
-struct R2D {
-    static constexpr int GP = RCH<B>::GP, LOFF = RCH<B>::LOFF;
-    static constexpr int SPX = B == 3 ? 112 : 72;   // output pixels per strip
-    static constexpr int NT = B == 3 ? 12 : 11;     // 64-byte input column tiles per row
-    static constexpr int TPW = (NT + 3) / 4;        // tiles per wave
-    static constexpr int NGR = SPX / GP;            // horizontal groups per strip
-    static constexpr int OB = B * SPX;              // output bytes per strip row
-    static constexpr int FIS = B == 3 ? 776 : 712;  // vertical-result row stride: (FIS / 4) mod 32 = 2 x odd
-    static constexpr int OTS = B == 3 ? 344 : 296;  // output tile row stride: 16 rows on distinct banks
-    static constexpr int FR = 15;                   // output rows per step
-    static_assert(NGR * GP == SPX && OB % 16 == 0, "strip geometry");
-    static_assert(64 * NT + LOFF <= FIS && OB <= OTS, "LDS rows");
-};
-
-struct R2dArgs {
-    const u8 *in;
-    u8 *out;
-    int w, h, ow, oh;
-    int x_end, y_end;       // computed region ends (exclusive); strips / steps start at s_base / f_base
-    int s_base, f_base;
-    int n_strips, n_bands, band_steps;
-    long long in_img, out_img;
-    int seed;               // 128 sum(T) + 2048 - (128 << 12) (results in the - 128 form)
-    const rc_u4 *ops;       // rch_operands: [64 lanes][vh, vl, wh, wl]
-    int soff;               // 1: interior steps put the row offset in the buffer SGPR offset (no per-load VALU)
-};
-
-template <int B>
-__global__ void __launch_bounds__(256) k_reduce2d(R2dArgs a) {
-    using G = R2D<B>;
-    constexpr int FIS = G::FIS, OTS = G::OTS, FR = G::FR, GP = G::GP, TPW = G::TPW, NT = G::NT;
-    __shared__ __attribute__((aligned(16))) u8 smem[16 * FIS + FR * OTS];
-    const uint32_t fint_l = rc_lds(smem), ot_l = fint_l + 16 * FIS;
-    u8 *fint = smem;
-
-    const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
-    const int strip = static_cast<int>(t % static_cast<uint32_t>(a.n_strips)) + a.s_base;
-    const int rest = static_cast<int>(t / static_cast<uint32_t>(a.n_strips));
-    const int band = rest % a.n_bands;
-    const int img = __builtin_amdgcn_readfirstlane(rest / a.n_bands);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int n = lane & 15, kg = lane >> 4;
-
-    const int x0 = strip * G::SPX;
-    const int vst = 2 * x0 - 5;
-    const int vb0 = (B * vst) & ~63;
-    const int ish = B * vst - vb0 + G::LOFF;
-    const int pitch = a.w * B;
-    const int fa = a.f_base + band * a.band_steps;
-    const int fb = min(fa + a.band_steps, (a.y_end + FR - 1) / FR);
-    const __amdgpu_buffer_rsrc_t src = image_rsrc(a.in + img * a.in_img, a.in_img);
-    const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
-
-    const rc_u4 *op = a.ops + 4 * lane;
-    const rc_v4i fvh = __builtin_bit_cast(rc_v4i, op[0]), fvl = __builtin_bit_cast(rc_v4i, op[1]);
-    const rc_v4i fwh = __builtin_bit_cast(rc_v4i, op[2]), fwl = __builtin_bit_cast(rc_v4i, op[3]);
-    const int sd = a.seed;
-
-    // the lane's input dword column per tile (out-of-row columns read 0 and are replaced below)
-    int cofs[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-        const int cb = vb0 + 64 * (wave + 4 * i) + 4 * n;
-        cofs[i] = (wave + 4 * i < NT && cb >= 0 && cb < pitch) ? cb : -1;
-    }
-    uint32_t v[TPW][5][4];
-    // per-lane part of an interior load's offset: rows 4 kg .. of the 16-row block at this
-    // lane's column (out-of-row columns: an offset past the image, read as 0)
-    int vo[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) vo[i] = cofs[i] >= 0 ? 4 * kg * pitch + cofs[i] : 0x7ffffff0;
-    auto load = [&](int f) {
-        const int P = FR * f;
-        const int r0 = 2 * P - 5;  // first input row of the step's blocks
-        if (a.soff && r0 >= 0 && r0 + 2 * (FR - 1) + 12 <= a.h - 1) {
-            // interior: row 6 g + j of the step in the SGPR offset (uniform), 4 kg rows and the
-            // column in the VGPR offset (range-checked; the whole address stays in the image)
-#pragma unroll
-            for (int i = 0; i < TPW; ++i)
-#pragma unroll
-                for (int g = 0; g < 5; ++g)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        v[i][g][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(
-                            src, vo[i], __builtin_amdgcn_readfirstlane((r0 + 6 * g + j) * pitch), 0));
-            return;
-        }
-#pragma unroll
-        for (int i = 0; i < TPW; ++i)
-#pragma unroll
-            for (int g = 0; g < 5; ++g)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int r = clampi(2 * (P + 3 * g) - 5 + 4 * kg + j, 0, a.h - 1);
-                    v[i][g][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(
-                        src, cofs[i] >= 0 ? r * pitch + cofs[i] : 0x7ffffff0, 0, 0));
-                }
-    };
-
-    // COPY edge: vertical-result pixels [0, nl) copy pixel nl, [fr, fr_end] pixel fr - 1
-    const int nl = vst < 0 ? -vst : 0;
-    const int fr = a.w - vst;
-    const int x_last = min(x0 + G::SPX, a.ow) - 1;
-    const int fr_end = min(2 * x_last + 6 - vst, 2 * G::SPX + 9);
-    const int nr = fr_end >= fr ? fr_end - fr + 1 : 0;
-    const bool edge = nl > 0 || nr > 0;
-    const int rowb = a.ow * B;
-    const int xb0 = x0 * B;
-
-    load(fa);
-    for (int f = fa; f < fb; ++f) {
-        // ---- vertical: this wave's tiles, 5 groups of 3 rows each ----
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-            if (wave + 4 * i >= NT) break;
-            const uint32_t fw = fint_l + static_cast<uint32_t>(kg * FIS + 64 * (wave + 4 * i) + 4 * n + G::LOFF);
-#pragma unroll
-            for (int g = 0; g < 5; ++g) {
-                const rc_v4i bv = rc_v4i{static_cast<int>(v[i][g][0] ^ 0x80808080u), static_cast<int>(v[i][g][1] ^ 0x80808080u),
-                                         static_cast<int>(v[i][g][2] ^ 0x80808080u), static_cast<int>(v[i][g][3] ^ 0x80808080u)};
-                rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
-                dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(fvh, bv, dh, 0, 0, 0);
-                dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(fvl, bv, dl, 0, 0, 0);
-                if (kg < 3)
-                    lds_wr32(fw + static_cast<uint32_t>(3 * g * FIS),
-                             rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
-            }
-        }
-        if (f + 1 < fb) load(f + 1);  // the next step's rows, in flight during the rest of this one
-        rc_barrier();
-        if (edge) {
-            const int nfill = nl + nr;
-            for (int i = tid; i < FR * nfill * B; i += 256) {
-                const int u = i / (nfill * B);
-                const int rem = i - u * nfill * B;
-                const int fp = rem / B, ch = rem - fp * B;
-                const int d = fp < nl ? fp : fr + (fp - nl);
-                const int sp = fp < nl ? nl : fr - 1;
-                fint[u * FIS + ish + B * d + ch] = fint[u * FIS + ish + B * sp + ch];
-            }
-            rc_barrier();
-        }
-        // ---- horizontal: groups q = wave + 4 i -> output tile ----
-        {
-            const uint32_t fbase = fint_l + static_cast<uint32_t>(n * FIS + (ish & ~7) + 16 * kg);
-            const uint32_t ow_l = ot_l + static_cast<uint32_t>(n * OTS + 4 * kg);
-            constexpr int QPW = (G::NGR + 3) / 4;
-            rc_u2x2 bq[QPW];
-#pragma unroll
-            for (int i = 0; i < QPW; ++i)
-                bq[i] = lds_rd64x2(fbase + static_cast<uint32_t>(2 * B * GP * min(wave + 4 * i, G::NGR - 1)));
-            if constexpr (QPW == 7) lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3], bq[4], bq[5], bq[6]);
-            else if constexpr (QPW == 6) lgkm_wait_for<0>(bq[0], bq[1], bq[2], bq[3], bq[4], bq[5]);
-            else static_assert(QPW == 6 || QPW == 7, "groups per wave");
-#pragma unroll
-            for (int i = 0; i < QPW; ++i) {
-                const int q = wave + 4 * i;
-                const rc_v4i bv = __builtin_bit_cast(rc_v4i, rc_join(bq[i]));
-                rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
-                dh = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwh, bv, dh, 0, 0, 0);
-                dl = __builtin_amdgcn_mfma_i32_16x16x64_i8(fwl, bv, dl, 0, 0, 0);
-                if (n < FR && 4 * kg < B * GP && q < G::NGR)
-                    lds_wr32(ow_l + static_cast<uint32_t>(B * GP * q),
-                             rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]) ^
-                                 0x80808080u);
-            }
-        }
-        rc_barrier();
-        // ---- stores: 16-byte row pieces of the tile ----
-        constexpr int PPR = G::OB / 16;  // pieces per tile row
-        for (int i = tid; i < FR * PPR; i += 256) {
-            const int u = i / PPR, pc = i - u * PPR;
-            const int y = FR * f + u;
-            const int xb = xb0 + 16 * pc;
-            rc_u2x2 qq = lds_rd64x2(ot_l + static_cast<uint32_t>(u * OTS + 16 * pc));
-            lgkm_wait_for<0>(qq);
-            const rc_u4 q = rc_join(qq);
-            if (y >= a.oh || y >= a.y_end || xb >= rowb) continue;
-            const int o = y * rowb + xb;
-            if (xb + 16 <= rowb) {
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, q), dst, o, 0, 0);
-            } else {
-                for (int e = 0; e < rowb - xb; ++e)
-                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<u8>(q[e >> 2] >> (8 * (e & 3))), dst, o + e, 0, 0);
-            }
-        }
-    }
-}
 
 // The per-lane tap operands, [lane][bh, bl, wh, wl] x 16 bytes.  Lane (n = lane & 15,
 // kg = lane >> 4) holds K = 16 kg + e, e = 0..15 (the same labelling on both operands
@@ -621,52 +422,6 @@ int reduce2m_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
     if (b == 3) hipLaunchKernelGGL(k_reduce2m<3>, grid, blk, 0, st, a);
     else hipLaunchKernelGGL(k_reduce2m<4>, grid, blk, 0, st, a);
     return launch_check("k_reduce2m");
-}
-
-// k_reduce2d over the output region [x0, x1) x [y0, y1) of a 2 x 2 reduce, either
-// convention (taps12: the 12 taps from 2x - 5 of its phase).  Whole strips / steps around
-// the region are computed, never past the output image.
-int reduce2d_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int x0, int y0, int x1, int y1,
-                           const int *taps12, hipStream_t st) {
-    if (b != 3 && b != 4) return MIPX_EUNSUPPORTED;
-    if ((w * b) % 4 != 0 || reinterpret_cast<uintptr_t>(in) % 4 != 0) return MIPX_EUNSUPPORTED;
-    R2dArgs a{};
-    a.in = in;
-    a.out = out;
-    a.w = w;
-    a.h = h;
-    a.ow = out_size_reduce(w, 2.0);
-    a.oh = out_size_reduce(h, 2.0);
-    if (x0 < 0 || y0 < 0 || x1 > a.ow || y1 > a.oh || x0 >= x1 || y0 >= y1) return MIPX_EINVAL;
-    a.in_img = img_bytes(w, h, b);
-    a.out_img = img_bytes(a.ow, a.oh, b);
-    if (a.in_img >= 0x7fffffffLL - 64 || a.out_img >= 0x7fffffffLL - 64) return MIPX_EUNSUPPORTED;
-    int sum = 0;
-    for (int i = 0; i < 12; ++i) {
-        sum += taps12[i];
-        if (taps12[i] < -128 * 64 || taps12[i] > 127 * 64 + 63) return MIPX_EUNSUPPORTED;
-    }
-    const std::vector<uint32_t> ops = b == 3 ? rch_operands<3>(taps12) : rch_operands<4>(taps12);
-    a.ops = static_cast<const rc_u4 *>(device_blob(ops.data(), ops.size() * sizeof(uint32_t)));
-    if (!a.ops) return MIPX_EDEVICE;
-    a.seed = 128 * sum + 2048 - (128 << 12);
-    const char *eso = tune_env("MIPX_R2D_SOFF");
-    a.soff = !(eso && *eso == '0');
-    const int spx = b == 3 ? R2D<3>::SPX : R2D<4>::SPX, fr = R2D<3>::FR;
-    a.x_end = x1;
-    a.y_end = y1;
-    a.s_base = x0 / spx;
-    a.f_base = y0 / fr;
-    a.n_strips = (x1 + spx - 1) / spx - a.s_base;
-    const int steps = (y1 + fr - 1) / fr - a.f_base;
-    const char *eb = tune_env("MIPX_R2D_BAND");  // 15-row steps per band (A/B)
-    a.band_steps = std::max(1, std::min(steps, (eb && *eb) ? std::atoi(eb) : 8));
-    a.n_bands = (steps + a.band_steps - 1) / a.band_steps;
-    const long long blocks = static_cast<long long>(a.n_strips) * a.n_bands * n;
-    if (!grid_ok(blocks)) return MIPX_EINVAL;
-    if (b == 3) hipLaunchKernelGGL(k_reduce2d<3>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_reduce2d<4>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, st, a);
-    return launch_check("k_reduce2d");
 }
 
 }  // namespace mipx

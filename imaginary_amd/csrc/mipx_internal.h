@@ -124,6 +124,8 @@ void free_device_tables();
 // bumped by free_device_tables: a launcher that caches a table pointer outside the maps
 // above keeps the generation it was made in and refetches when it changed
 unsigned device_tables_generation();
+// free_device_tables also frees every table k_enlm keeps per (device, scale) (k_affine.hip)
+void free_enlm_tables();
 
 // ---- generic separable passes (k_sep.hip) -----------------------------------
 enum { kSepReduce = 0, kSepConv = 1 };
@@ -179,16 +181,8 @@ int reduce2_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, 
 // cores; taps12 = matrixi[64][0..11]
 int reduce2m_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int x0, int y0, int x1,
                            int y1, const int *taps12, hipStream_t st);
-// k_reduce2m.hip: the 2 x 2 reduce with no input ring (k_rchain's front), either convention
-int reduce2d_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int x0, int y0, int x1,
-                           int y1, const int *taps12, hipStream_t st);
 // the corner convention's 2 x 2 mask as k_reduce2x2 uses it: c0, c1, c3, c5 (k_reduce.hip)
 bool reduce2_taps(float c[4]);
-// the 2 x 2 reduce's 12 taps from 2x - 5 at the current convention (k_reduce.hip)
-bool reduce2_front_taps(int taps[12]);
-// k_rcol.hip: reduce 2 x 2 then reduce (hs, vs) over the second's output window, one launch
-int reduce2_chain_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, double hs, double vs, int ox0,
-                         int oy0, int ow, int oh, const int *taps12, hipStream_t st);
 // k_shrink.hip
 int shrink_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int hs, int vs, hipStream_t st);
 int shrink_window_launch(const uint8_t *in, uint8_t *out, int n, int w, int h, int b, int hs, int vs, int x0, int y0,

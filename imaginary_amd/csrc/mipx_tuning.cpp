@@ -126,8 +126,10 @@ int occupancy_per_cu(const void *fn, int threads, size_t lds, int fallback) {
 extern "C" int mipx_set_reduce_sampling(int32_t convention) {
     if (convention != MIPX_SAMPLE_CORNER && convention != MIPX_SAMPLE_CENTRE) return MIPX_EINVAL;
     // plans record the convention they were made under (mipx_plan_make), so queued work
-    // would not change; the setter still refuses while requests are queued or running, so
-    // a caller cannot believe its in-flight requests follow the new setting
+    // does not change; the setter still refuses while it sees mipx_submit requests queued
+    // or running, so a caller does not believe its in-flight requests follow the new
+    // setting.  Advisory only (mipx.h): no lock spans the check and the store, and work
+    // outside mipx_submit is not counted; correctness rests on each plan's a[7]
     if (mipx::requests_in_flight() > 0) {
         mipx::set_error("mipx_set_reduce_sampling: %lld requests queued or running",
                         static_cast<long long>(mipx::requests_in_flight()));

@@ -258,8 +258,12 @@ size_t mipx_op_workspace_bytes(int32_t op, int32_t n, int32_t w, int32_t h, int3
  * keeps its convention when the setting changes later; a zeroed a[7] is the corner
  * convention, any value but 0 / 1 is MIPX_EINVAL).  The per-op entry points
  * (mipx_op_reduce, _reducev, _reduceh, _smartcrop_origin) read the setting once per call.
- * The setter returns MIPX_EBUSY while requests submitted through mipx_submit are queued
- * or running, MIPX_EINVAL for any other value. */
+ * The setter returns MIPX_EINVAL for a value other than the two; it also returns
+ * MIPX_EBUSY when it sees mipx_submit requests queued or running.  That refusal is
+ * advisory, not a guarantee: it counts mipx_submit work only (not mipx_execute_dev or the
+ * per-op calls on a caller's stream) and a submit may land just after the check.  Nothing
+ * depends on it: a plan's own a[7] decides its convention.  Set the convention once at
+ * start-up. */
 #define MIPX_SAMPLE_CORNER 0
 #define MIPX_SAMPLE_CENTRE 1
 int mipx_set_reduce_sampling(int32_t convention);

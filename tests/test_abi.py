@@ -155,6 +155,33 @@ def test_code_object_avoids_known_bad_gfx950_fusion(tmp_path):
     assert seen_dot2, "disassembly lacks the reduce passes' dot2 (extraction failed?)"
 
 
+def test_shipped_library_carries_no_unreachable_kernels_or_probes(tmp_path):
+    """kernels no default dispatch reaches (r05's k_rchain,
+    k_reduce2d, k_reduce2w and the k_enlm-shadowed k_enlarge2) are gone from the
+    product library (their A/B records stay under profiles/), and the pixel-corrupting
+    timing probes (MIPX_ENLM_DBG) and the launch-geometry dump (MIPX_BCOL_DBG) exist
+    only in a `make PROBES=1` build (libmipx_probes.so), never in libmipx.so."""
+    import shutil
+    import imaginary_amd as ia
+    syms = subprocess.run(["nm", "-C", ia.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "k_reduce2x2<3, 66>" in syms and "k_enlm<" in syms   # the listing does name kernels
+    for k in ("k_rchain", "k_reduce2d", "k_reduce2w", "k_enlarge2"):
+        assert k not in syms, k
+    with open(ia.LIB_PATH, "rb") as f:
+        blob = f.read()
+    for knob in (b"MIPX_ENLM_DBG", b"MIPX_BCOL_DBG", b"MIPX_CHAIN", b"MIPX_R2D", b"MIPX_R2_WALK", b"MIPX_ENLARGE2"):
+        assert knob not in blob, knob
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if os.path.exists(objdump):  # nor in the device code objects
+        so = tmp_path / "libmipx.so"
+        shutil.copy(ia.LIB_PATH, so)
+        subprocess.run([objdump, "--offloading", str(so)], cwd=tmp_path, check=True, capture_output=True)
+        kern = "".join(subprocess.run(["nm", "-C", str(p)], capture_output=True, text=True).stdout
+                       for p in tmp_path.iterdir() if "gfx950" in p.name)
+        assert "k_enlm" in kern and "k_reduce2m" in kern
+        assert not any(k in kern for k in ("k_rchain", "k_reduce2d", "k_reduce2w", "k_enlarge2"))
+
+
 def test_build_id_is_the_hash_of_these_sources():
     """Build provenance: libmipx.so carries the hash of the sources it was built
     from (imaginary_amd/srchash.py); it must be the hash of this tree's sources."""

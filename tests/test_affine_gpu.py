@@ -47,7 +47,7 @@ def test_enlarge_plans(gpu, oracle, rng):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"enlarge plan {iw}x{ih}x{b} {opts}")
 
 
-E2_CASES = [  # h, w, b, extend: k_enlarge2 (exactly 2 x 2) at every band count and edge
+E2_CASES = [  # h, w, b, extend: exactly 2 x 2 on the VALU kernels at every band count and edge
     (740, 550, 3, 1), (33, 1201, 4, 0), (97, 203, 1, 2), (61, 130, 2, 3), (64, 640, 3, 4),
     (5, 7, 3, 5), (1, 1, 4, 1), (2, 3, 3, 0), (70, 129, 4, 1), (129, 128, 3, 3),
     # a 16-byte chunk ending exactly at the image's last byte with in_img % 4 != 0
@@ -56,18 +56,32 @@ E2_CASES = [  # h, w, b, extend: k_enlarge2 (exactly 2 x 2) at every band count 
 ]
 
 
-@pytest.mark.parametrize("e2", ["1", "0"])
+@pytest.mark.parametrize("sep", ["1", "0"])
 @pytest.mark.parametrize("h,w,b,extend", E2_CASES)
-def test_enlarge2_matches_oracle(gpu, oracle, rng, monkeypatch, e2, h, w, b, extend):
-    """vips_affine at exactly 2 x 2 on k_enlarge2 (the fixed phase-96 / phase-32 pattern,
-    MIPX_ENLARGE2=1) and on k_affine_sep (0), k_enlm off: strips and bands that end at the
-    image edges, images narrower than the 6-pixel window, every extend mode, all bands."""
+def test_enlarge2_matches_oracle(gpu, oracle, rng, monkeypatch, sep, h, w, b, extend):
+    """vips_affine at exactly 2 x 2 with k_enlm off: k_affine_sep (MIPX_AFFINE_SEP=1) and the
+    per-pixel k_affine (0), strips and bands that end at the image edges, images narrower
+    than the 6-pixel window, every extend mode, all bands.  (r04's fixed-pattern
+    k_enlarge2, shadowed by k_enlm since r05, was removed in r06.)"""
     monkeypatch.setenv("MIPX_ENLM", "0")
-    monkeypatch.setenv("MIPX_ENLARGE2", e2)
+    monkeypatch.setenv("MIPX_AFFINE_SEP", sep)
     imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
     got = gpu.run_op("affine", imgs, xscale=2.0, yscale=2.0, extend=extend)
     for i in range(2):
-        assert_same(got[i], oracle.affine(imgs[i], 2.0, 2.0, extend), f"enlarge2 e2={e2} {h}x{w}x{b} e{extend} img{i}")
+        assert_same(got[i], oracle.affine(imgs[i], 2.0, 2.0, extend), f"enlarge sep={sep} {h}x{w}x{b} e{extend} img{i}")
+
+
+@pytest.mark.parametrize("dbg", ["1", "2", "3", "4", "7"])
+def test_enlm_probe_knob_is_compiled_out(gpu, oracle, rng, monkeypatch, dbg):
+    """the timing probes (MIPX_ENLM_DBG: skip the staging loads / the
+    stores, wrong pixels) exist only in a `make PROBES=1` library; the shipped one ignores
+    the variable, so Enlarge stays oracle-exact whatever the environment says."""
+    monkeypatch.setenv("MIPX_ENLM", "2")
+    monkeypatch.setenv("MIPX_ENLM_DBG", dbg)
+    img = np.stack([rand_img(rng, 61, 130, 3), smooth_img(rng, 61, 130, 3)])
+    got = gpu.run_op("affine", img, xscale=2.0, yscale=2.0, extend=1)
+    for i in range(2):
+        assert_same(got[i], oracle.affine(img[i], 2.0, 2.0, 1), f"MIPX_ENLM_DBG={dbg} img{i}")
 
 
 # k_enlm (both passes on the matrix cores): integer and fractional scales, per-axis mixes,

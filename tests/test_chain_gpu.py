@@ -1,10 +1,11 @@
-"""k_rchain: vips_reduce 2 x 2 followed by a second vips_reduce (and its extract window) in
-one launch, the /pipeline resize -> crop chain of C3 (reference image.go:379-410).
+"""vips_reduce 2 x 2 followed by a second vips_reduce (and its extract window): the
+/pipeline resize -> crop chain of C3 (reference image.go:379-410).
 
 The merged plan (mipx_plan_chain) of a 2 x 2 resize stage and a resize / crop stage runs
-through the chained kernel; each case is checked against the oracle run stage by stage
-(o.reduce twice, then the extract) and against the same plan with the chain off
-(MIPX_CHAIN=0: k_reduce2x2 / k_reduce2m then k_rcol), under both sampling conventions.
+k_reduce2x2 / k_reduce2m (only the rows and columns the second reduce reads, plan_demand)
+then k_rcol over the window; each case is checked against the oracle run stage by stage
+(o.reduce twice, then the extract), under both sampling conventions.  (r05's one-launch
+k_rchain, measured slower, was removed in r06: profiles/r05/c3_chain_ab.jsonl.)
 """
 import numpy as np
 import pytest
@@ -54,60 +55,50 @@ def _oracle(oracle, p1, p2, px):
 
 
 @pytest.mark.parametrize("w,h,b,opts2", CASES, ids=[f"{c[0]}x{c[1]}x{c[2]}-{i}" for i, c in enumerate(CASES)])
-def test_chain_matches_oracle(gpu, oracle, convention, monkeypatch, w, h, b, opts2):
+def test_chain_matches_oracle(gpu, oracle, convention, w, h, b, opts2):
     r = np.random.default_rng(w * 7 + h * 3 + b)
     px = r.integers(0, 256, (2, h, w, b), dtype=np.uint8)
     p1, p2, plan = _chain_plan(gpu, w, h, b, opts2)
-    monkeypatch.setenv("MIPX_CHAIN", "2")  # 2: the chained kernel or an error, never the two reduces
     got = gpu.execute(plan, px, junk=0xA5)
     for i in range(2):
         want = _oracle(oracle, p1, p2, px[i])
         assert got[i].shape == want.shape
         d = np.argwhere(got[i] != want)
         assert len(d) == 0, f"{convention} {w}x{h}x{b} {opts2}: {len(d)} bytes differ, first at {d[0]}"
-    monkeypatch.setenv("MIPX_CHAIN", "0")
-    assert np.array_equal(gpu.execute(plan, px), got)
 
 
-def test_chain_smooth_images_and_extremes(gpu, oracle, convention, monkeypatch):
+def test_chain_smooth_images_and_extremes(gpu, oracle, convention):
     """Saturating inputs (0 / 255 blocks, ramps) through both products' rounding and clamping."""
     h, w, b = 300, 420, 4
     y, x = np.mgrid[0:h, 0:w]
     px = np.stack([((x * 255) // (w - 1)).astype(np.uint8), ((y // 7) % 2 * 255).astype(np.uint8),
                    (((x // 5 + y // 5) % 2) * 255).astype(np.uint8), np.full((h, w), 255, np.uint8)], -1)
     p1, p2, plan = _chain_plan(gpu, w, h, b, dict(width=150, height=100, crop=1))
-    monkeypatch.setenv("MIPX_CHAIN", "2")
     got = gpu.execute(plan, px[None])
     assert np.array_equal(got[0], _oracle(oracle, p1, p2, px))
 
 
-# ---------------------------------------------------------------- k_reduce2d (MIPX_R2D=1)
+# ------------------------------------------------- the default 2 x 2 kernels at edge shapes
 R2D_SHAPES = ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1000, 4), (200, 648, 3), (8, 8, 4), (9, 12, 3),
               (25, 164, 3), (131, 1000, 4), (1081, 324, 3), (16, 3840, 3), (47, 226, 4), (2160, 3840, 3))
 
 
-@pytest.mark.parametrize("band", ["1", "8", "40"])
-def test_reduce2d_exact(gpu, oracle, convention, band, monkeypatch):
-    """The ring-less 2 x 2 kernel (k_reduce2d: vertical pass straight from HBM into the
-    matrix cores) at both conventions: strips ending at the image edges, images shorter
-    than a 15-row step, widths past one strip, full 4K."""
-    monkeypatch.setenv("MIPX_R2D", "1")
-    monkeypatch.setenv("MIPX_R2D_BAND", band)
+def test_reduce2x2_edge_shapes_exact(gpu, oracle, convention):
+    """k_reduce2x2 / k_reduce2m (the generic reduce where rows are off a dword) at both
+    conventions: strips ending at the image edges, images shorter than a step, widths
+    past one strip, full 4K (r05's shapes for the removed ring-less k_reduce2d)."""
     r = np.random.default_rng(11)
     for h, w, b in R2D_SHAPES:
-        if (w * b) % 4 or (h == 2160 and band != "8"):
-            continue
         imgs = r.integers(0, 256, (2, h, w, b), dtype=np.uint8)
         got = gpu.run_op("reduce", imgs, hshrink=2.0, vshrink=2.0)
         for i in range(2):
             want = oracle.reduce(imgs[i], 2.0, 2.0)
             d = np.argwhere(got[i] != want)
-            assert len(d) == 0, f"{convention} band={band} {h}x{w}x{b} img{i}: {len(d)} differ, first {d[0]}"
+            assert len(d) == 0, f"{convention} {h}x{w}x{b} img{i}: {len(d)} differ, first {d[0]}"
 
 
-def test_reduce2d_windows(gpu, oracle, convention, monkeypatch):
-    """k_reduce2d computing only a 2 x 2 reduce's demanded region (reduce -> crop plans)."""
-    monkeypatch.setenv("MIPX_R2D", "1")
+def test_reduce2x2_windows(gpu, oracle, convention):
+    """The 2 x 2 kernels computing only a reduce's demanded region (reduce -> crop plans)."""
     r = np.random.default_rng(12)
     for (w, h, b), (left, top, cw, ch) in (((1200, 800, 3), (150, 100, 300, 200)), ((1200, 800, 4), (0, 280, 500, 120)),
                                            ((640, 960, 3), (0, 0, 320, 100)), ((640, 960, 4), (219, 0, 100, 480))):
