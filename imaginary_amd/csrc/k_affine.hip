@@ -313,7 +313,11 @@ typedef _Float16 em_h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 em_h4 __attribute__((ext_vector_type(4)));
 typedef float em_f4 __attribute__((ext_vector_type(4)));
 // a wave's output columns: NU units of 16 bytes (4 or 8); its output tile's row stride
-// is 16 NU + 16 bytes (16 x odd)
+// is 16 NU + 16 bytes (16 x odd: the dword writes are 2-way, free for ds_write_b32).  r06
+// (osw, VERDICT r5 item 4: conflicts 1.23-1.27x the active LDS cycles): the read-back's
+// lanes take rows by tile_rd_lane, so each ds_read_b128 lane group reads rows g, g + 4,
+// g + 8, g + 12 on disjoint banks (lane / 4 put rows 0 and 3, 0 and 6 of one group on
+// the same banks)
 constexpr int em_os(int nu) { return 16 * nu + 16; }
 constexpr float kEmMagic = 1200.0f;
 constexpr int kEmRec = 8;       // ints per axis record: {pos, tap sum, taps 0 1, taps 2 3 (int16)}, {pos, tap sum, Ch + 64, Cl (u8 x 4)}
@@ -331,6 +335,7 @@ struct EnlmArgs {
     int ncr;                // 16-byte chunks staged per row (<= 8)
     long long blocks;
     int dbg;                // MIPX_ENLM_DBG (timing probes only, wrong pixels): 1 no staging loads, 2 no stores, 4 no realignment dwords
+    int osw;                // the output tile's read-back lanes by tile_rd_lane (r06)
 };
 
 // The timing probes exist only in a -DMIPX_PROBES build (scripts/, `make PROBES=1`): the
@@ -368,9 +373,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
     const int band = 4 * static_cast<int>(rest % a.bquads) + wave;
     const int img = static_cast<int>(rest / a.bquads);
     u8 *opl = reinterpret_cast<u8 *>(ems);  // [unit][ks][hi, lo][64 lanes] x 16 bytes
-    u8 *stg = opl + kEmNU * NK * 2 * 1024 + wave * (16 * a.rs + 16 * kEmOS + 16 * a.br);
+    u8 *stg = opl + kEmNU * NK * 2 * 1024 + wave * (16 * a.rs + 16 * em_os(NU) + 16 * a.br);
     u8 *otl = stg + 16 * a.rs;
-    int4 *rrec = reinterpret_cast<int4 *>(otl + 16 * kEmOS);  // [br] the band's row records
+    int4 *rrec = reinterpret_cast<int4 *>(otl + 16 * em_os(NU));  // [br] the band's row records
     const int n = lane & 15, kg = lane >> 4;
     const int rowb = a.ow * B, pitch = a.w * B;
     const int x0b = 16 * NU * grp;
@@ -479,6 +484,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
             }
     };
 
+    int rr = lane >> 2, tpc = lane & 3;  // the output tile read-back: row, first 16-byte piece
+    if (a.osw) tile_rd_lane(lane, &rr, &tpc);
     em_h8 hh[kEmNU];  // H + 1200: the lane's 4 rows of the previous tile, then of this tile
 #pragma unroll
     for (int u = 0; u < kEmNU; ++u) hh[u] = em_h8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -560,11 +567,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NU == 
                 q = __builtin_amdgcn_cvt_pk_u8_f32(d[3], 3, q);
                 *reinterpret_cast<uint32_t *>(otl + n * kEmOS + 16 * u + 4 * kg) = q;
             }
-            // 16 rows x 16 NU bytes as 16-byte pieces: lane = (row lane / 4, pieces lane % 4 + 4 i)
-            const int rr = lane >> 2;
+            // 16 rows x 16 NU bytes as 16-byte pieces: lane = (row rr, pieces pc + 4 i)
 #pragma unroll
             for (int i = 0; i < NU / 4; ++i) {
-                const int pc2 = (lane & 3) + 4 * i;
+                const int pc2 = tpc + 4 * i;
                 const rc_u4 v = *reinterpret_cast<const rc_u4 *>(otl + rr * kEmOS + 16 * pc2);
                 const int yy = oy + rr, bo = x0b + 16 * pc2;
                 if (yy <= yl && bo < rowb && !(em_dbg(a) & 2)) {
@@ -901,6 +907,8 @@ int affine_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double xs, 
         if (enlm_plan(n, w, h, b, a.ow, a.oh, xs, ys, &g, &nk, &nu)) {
             g.in = in, g.out = out, g.w = w, g.h = h, g.ow = a.ow, g.oh = a.oh, g.extend = a.extend, g.fill = a.fill;
             g.in_img = a.in_img, g.out_img = a.out_img;
+            const char *eos = tune_env("MIPX_ENLM_OSW");  // r06: 0 keeps the padded output tile (A/B)
+            g.osw = !(eos && *eos == '0');
 #ifdef MIPX_PROBES
             const char *edb = tune_env("MIPX_ENLM_DBG");
             g.dbg = edb && *edb ? std::atoi(edb) : 0;

@@ -64,6 +64,8 @@ struct BcArgs {
     int skipl;               // load batches no lane of the wave needs are not issued (r05)
     int a16;            // host: horizontal operands 16-byte aligned (k_bcol<.., A16 = true>)
     int sd;             // A16: staged rows start sd bytes into their LDS row (0 / 4 / 8 / 12)
+    int vperm;          // r06: vertical K index 16 kg + e holds ring row 8 kg + e (e < 8) / 32 + 8 kg + e - 8
+    int wsw;            // r06: the store tile's read-back lanes by tile_rd_lane (UPW 4)
     const signed char *ops;  // device_blur_ops: [NKS][64 lanes][16] horizontal, then [64][16] vertical
 };
 
@@ -91,7 +93,12 @@ __device__ __forceinline__ rc_u2 lds_rd2x32(uint32_t a) {
 template <int B, int NKS, int KMAX, bool A16, int UPW>
 __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
     constexpr int SB = kBcSB * UPW;  // strip bytes
-    constexpr int WSR = 16 * UPW + (UPW % 2 == 0 ? 16 : 0);  // dwords = 4 mod 8: the tile writes on distinct banks
+    // store tile row stride: dwords = 4 mod 8 (the tile writes on distinct banks); with UPW 4
+    // (wsw, r06) the read-back's lanes take rows by tile_rd_lane, so each ds_read_b128 lane
+    // group reads 4 rows on disjoint banks (lane / 4 put rows 0 / 3 / 5 / 6 of one group on
+    // shared banks)
+    constexpr int WSR = 16 * UPW + (UPW % 2 == 0 ? 16 : 0);
+    const bool wsw = UPW == 4 && a.wsw;
     constexpr int NPC = (16 * UPW + 63) / 64;                  // 16-byte row pieces per lane
     constexpr int UC = UPW;                                    // units per operand chunk
     extern __shared__ __attribute__((aligned(16))) uint32_t bcs[];
@@ -223,10 +230,13 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
     };
     // vertical pass of step j: ring rows 16 j - half + K, K = 16 kg + (0..7 | 8..15)
     const uint32_t wst_l = wst_l0 + static_cast<uint32_t>(wave * kBcRows * WSR);
+    // (vperm: K 16 kg + e <-> row 8 kg + e / 32 + 8 kg + e - 8, so the 16 rows of one 32-lane
+    // half's transposed read are consecutive ring slots on distinct banks; the identity
+    // layout put rows r and r + 16 of one half on the same banks: 2-way on every read)
     auto vertical_store = [&](int j, bool live) {
-        const int r1 = kBcRows * j - a.half + 16 * kg + (n >> 1);
+        const int r1 = kBcRows * j - a.half + (a.vperm ? 8 : 16) * kg + (n >> 1);
         const uint32_t a1 = ring_l + static_cast<uint32_t>((r1 & a.rmask) * a.tw + 8 * (n & 1));
-        const uint32_t a2 = ring_l + static_cast<uint32_t>(((r1 + 8) & a.rmask) * a.tw + 8 * (n & 1));
+        const uint32_t a2 = ring_l + static_cast<uint32_t>(((r1 + (a.vperm ? 32 : 8)) & a.rmask) * a.tw + 8 * (n & 1));
 #pragma unroll
         for (int c0 = 0; c0 < UPW; c0 += UC) {
             rc_v2i t1[UC], t2[UC];
@@ -252,7 +262,9 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
         rc_u4 qv[NPC];
 #pragma unroll
         for (int r = 0; r < NPC; ++r) {  // piece lane + 64 r = (row, 16-byte chunk)
-            const int pc = min(lane + 64 * r, 16 * UPW - 1), wrow = pc / UPW, wch = pc - UPW * wrow;
+            const int pc = min(lane + 64 * r, 16 * UPW - 1);
+            int wrow = pc / UPW, wch = pc - UPW * wrow;
+            if (wsw) tile_rd_lane(lane, &wrow, &wch);
             qv[r] = lds_rd128(wst_l + static_cast<uint32_t>(wrow * WSR + 16 * wch));
         }
 #pragma unroll
@@ -261,7 +273,9 @@ __global__ void __launch_bounds__(kBcNT) k_bcol(BcArgs a) {
 #pragma unroll
         for (int r = 0; r < NPC; ++r) {
             rc_pin(qv[r]);
-            const int pc = lane + 64 * r, wrow = pc / UPW, wch = pc - UPW * wrow;
+            const int pc = lane + 64 * r;
+            int wrow = pc / UPW, wch = pc - UPW * wrow;
+            if (wsw) tile_rd_lane(lane, &wrow, &wch);  // (UPW 4: one piece per lane, r = 0)
             const int we = 16 * (UPW * wave + wch);  // the piece's first byte in the strip row
             const int y = kBcRows * j + wrow;
             const bool ok = live && pc < 16 * UPW && y < a.h;
@@ -381,7 +395,13 @@ int blur_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, int left,
     // +1-2.3 %, C3 +0.3 %, C5 +0.6 % (profiles/r05/bcol/bsl_ab.jsonl)
     const char *esl = tune_env("MIPX_BCOL_SKIPL");
     a.skipl = !(esl && *esl == '0');
-    a.ops = device_blur_ops(mask, b, delta, nks);
+    // r06: MIPX_BCOL_VPERM=0 / MIPX_BCOL_WSW=0 keep r05's vertical K
+    // layout / padded store tile (A/B)
+    const char *evp = tune_env("MIPX_BCOL_VPERM");
+    a.vperm = !(evp && *evp == '0');
+    const char *ews = tune_env("MIPX_BCOL_WSW");
+    a.wsw = !(ews && *ews == '0');
+    a.ops = device_blur_ops(mask, b, delta, nks, a.vperm);
     if (!a.ops) return MIPX_EDEVICE;
     const size_t lds = static_cast<size_t>(2 * kBcRows) * rsd + static_cast<size_t>(ring) * a.tw +
                        static_cast<size_t>(4 * kBcRows) * (16 * upw + (upw % 2 == 0 ? 16 : 0));

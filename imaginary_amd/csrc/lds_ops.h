@@ -81,6 +81,18 @@ __device__ __forceinline__ void lds_wr4x32(uint32_t a, rc_u4 v) {
     asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(a), "v"(v.x), "v"(v.y) : "memory");
     asm volatile("ds_write2_b32 %0, %1, %2 offset0:2 offset1:3" ::"v"(a), "v"(v.z), "v"(v.w) : "memory");
 }
+// Lane -> (row, 16-byte chunk) for reading back a 16-row x 4-chunk tile with one
+// ds_read_b128 per lane (r06).  The instruction serves 4 lane groups, {0-3, 12-15, 20-27},
+// {4-11, 16-19, 28-31} and the same + 32: in 4-lane units q = (lane >> 2) & 7 those are
+// the q of even / odd popcount, and q >> 1 numbers each set 0..3.  Group g reads rows g,
+// g + 4, g + 8, g + 12, which sit on 4 disjoint 16-bank quarters whenever the row stride
+// is an odd number of 16-byte units (the tiles' padded strides: 80 / 144 bytes); the
+// plain lane -> (lane / 4, lane % 4) order put rows 0, 3, 5, 6 in one group, 2- to 3-way.
+__device__ __forceinline__ void tile_rd_lane(int lane, int *row, int *chunk) {
+    const int q = (lane >> 2) & 7;
+    *row = 2 * (lane >> 5) + (__builtin_popcount(q) & 1) + 4 * (q >> 1);
+    *chunk = lane & 3;
+}
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // The wait must also be a data dependence of the values it waits for: an asm read's
 // result is an ordinary register to the compiler, which could otherwise schedule its

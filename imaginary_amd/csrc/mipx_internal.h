@@ -113,7 +113,7 @@ constexpr int kRcolPlanRow = 144;
 const uint8_t *device_rcol_vplan(double shrink, bool centre, int rows, int *cap_rows);
 // k_bmf's i8 MFMA operands for a blur mask (cached per device): [nks][64][16]
 // horizontal taps at byte stride `bands` shifted by delta, then [64][16] vertical taps
-const signed char *device_blur_ops(const std::vector<int> &mask, int bands, int delta, int nks);
+const signed char *device_blur_ops(const std::vector<int> &mask, int bands, int delta, int nks, int vperm);
 const float *device_colour_tables();  // [256 v2y | kQuantElements cbrt | 257 y2v]
 const int *device_bicubic_table();     // 129 x 4
 // float copy of the integer gaussmat mask; *scale = mask sum
