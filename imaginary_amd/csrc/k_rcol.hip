@@ -81,6 +81,8 @@ struct RcArgs {
     int allst;                // A/B: every strip issues the edge-piece dword stores (r05 before)
     int skipl;                // ring load batches no lane of the wave needs are not issued
     int trl;                  // RGBA store tile read back by tile_rd_lane (r06)
+    int tearly;               // the first two steps' tap fragments loaded before the prime (r06)
+    int ppipe;                // the prime's row batches pipelined (r06)
     int dbg;                  // MIPX_RCOL_DBG (PROBES builds only): 1 = set-up and prime, no steps
 };
 #ifdef MIPX_PROBES
@@ -140,15 +142,7 @@ __device__ __forceinline__ void rc_edge_frag(const float *tabf, int taps, int pp
 // UNAL (r05): input rows off a dword (w B % 4 != 0, e.g. C5's 1333-pixel RGB rows): every
 // 16-byte chunk is loaded from its dword-aligned-down offset with the next dword and
 // realigned (v_alignbyte) when it is written to the ring
-// OB (r06): one barrier per step, the intermediate double-buffered (step k's vertical
-// result in buffer (k - ka) & 1).  OB 1: step k's horizontal pass runs in step k + 1,
-// after that step's barrier and beside its vertical pass: ring write (k + 1) -> barrier
-// -> vertical (k + 1) -> horizontal (k) -> stores (k); the ring must then hold a step's
-// rows and the next step's new rows at once (host-checked).  OB 2: every wave stages the
-// ring columns its own vertical tiles read (a contiguous quarter of the strip's 16-byte
-// columns), so ring writes and vertical reads never cross waves: ring write (k) ->
-// vertical (k) -> loads -> barrier -> horizontal (k) -> stores (k).  OB 0: two barriers
-template <int B, int NKS, int KMAX, int WPE, bool UNAL = false, int OB = 0>
+template <int B, int NKS, int KMAX, int WPE, bool UNAL = false>
 __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_rcol(RcArgs a) {
     constexpr int WV = kRcNT / 64, XW = 16 * WV;
     constexpr int UPW = B;  // horizontal units per wave: XW B / 16 / WV
@@ -248,22 +242,18 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
 
     // ring chunks: chunk c = tid + 256 j of a step's rows is (row rr, column col); the
     // same map every step.  A lane's chunks past the step's rows load rows below it:
-    // harmless (host-checked: their slots hold rows no longer read).  OB 2: chunk
-    // c = lane + 64 j of the wave's own columns [cb, ce) (none for a wave of a strip
-    // narrower than 4 columns: idle)
-    const int cb = OB == 2 ? (wave * cpr) / WV : 0, ce = OB == 2 ? ((wave + 1) * cpr) / WV : cpr;
-    const int ncw = max(ce - cb, 1);
+    // harmless (host-checked: their slots hold rows no longer read).
     int rr[KMAX], cof[KMAX];
     uint32_t lcol[KMAX];
 #pragma unroll
     for (int j = 0; j < KMAX; ++j) {
-        const int c = OB == 2 ? lane + 64 * j : tid + kRcNT * j;
-        rr[j] = ce > cb ? c / ncw : 1 << 20;
-        const int col = cb + c - (c / ncw) * ncw;
+        const int c = tid + kRcNT * j;
+        rr[j] = c / cpr;
+        const int col = c - rr[j] * cpr;
         cof[j] = B * org + 16 * col;
         lcol[j] = ring_l + static_cast<uint32_t>(16 * col);
     }
-    const int lkf = OB == 2 ? (64 * KMAX) / ncw : (kRcNT * KMAX) / cpr;  // rows one load batch covers completely
+    const int lkf = (kRcNT * KMAX) / cpr;  // rows one load batch covers completely
     // skipl: batch j of this wave loads anything (uniform; the same every step)
     bool wl[KMAX];
 #pragma unroll
@@ -297,13 +287,13 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         return rc_u4{__builtin_amdgcn_alignbyte(v.y, v.x, sh), __builtin_amdgcn_alignbyte(v.z, v.y, sh),
                      __builtin_amdgcn_alignbyte(v.w, v.z, sh), __builtin_amdgcn_alignbyte(e, v.w, sh)};
     };
-    auto issue_ring = [&](auto pc, int r0, bool need = true) {
+    auto issue_ring = [&](auto pc, int r0) {
         constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
             if (!wl[j]) continue;
             // idle lanes: out of range for both loads, and (off & ~3) + 16 stays below 2^31
-            const int off = need && rr[j] < a.rcap ? chunk_off(r0, j) : 0x7fffffe0;
+            const int off = rr[j] < a.rcap ? chunk_off(r0, j) : 0x7fffffe0;
             rv[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
             if constexpr (UNAL)
                 re[P][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
@@ -321,8 +311,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // wave-private LDS tile [16 rows][16 UPW (+ 16 for RGBA: bank spread) bytes] and
     // stored as 16-byte pieces: 16 UPW contiguous bytes per row instead of 16
     constexpr int WSR = 16 * UPW + (UPW == 4 ? 16 : 0);
-    const uint32_t wst_l = inter_l + static_cast<uint32_t>((OB ? 2 : 1) * kRcRows * a.iw + wave * kRcRows * WSR);
-    const uint32_t inter2 = inter_l + static_cast<uint32_t>(kRcRows * a.iw);  // OB: the second buffer
+    const uint32_t wst_l = inter_l + static_cast<uint32_t>(kRcRows * a.iw + wave * kRcRows * WSR);
     int wrow = min(lane / UPW, kRcRows - 1), wch = lane - UPW * (lane / UPW);  // read-back: row, 16-byte chunk
     // r06: RGBA (4 chunks a row, rows 80 bytes apart) reads back by tile_rd_lane: each
     // ds_read_b128 lane group on disjoint banks (MIPX_RCOL_TRL=0: lane / 4, A/B)
@@ -366,14 +355,14 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // vertical pass: 16-byte column tiles dealt to the waves, two in flight per wait.  K
     // index 16 kg + e holds relative row 8 kg + e (e < 8) or 32 + 8 kg + e - 8, so the 16
     // rows one 32-lane half reads per transposed load sit in consecutive ring slots
-    auto vertical = [&](auto pc, int bk, uint32_t ib) {
+    auto vertical = [&](auto pc, int bk) {
         constexpr int P = decltype(pc)::value;
         const rc_v4i bh = vh[P], bl = vl[P];
         const int sd = vsd[P];
         const int r1 = bk + 8 * kg + (n >> 1);
         const uint32_t a1 = ring_l + static_cast<uint32_t>((r1 & a.rmask) * a.rs + 8 * (n & 1));
         const uint32_t a2 = ring_l + static_cast<uint32_t>(((r1 + 32) & a.rmask) * a.rs + 8 * (n & 1));
-        const uint32_t iq = ib + static_cast<uint32_t>(n * a.iw + 4 * kg);
+        const uint32_t iq = inter_l + static_cast<uint32_t>(n * a.iw + 4 * kg);
         auto tile = [&](int ct, rc_v2i t1, rc_v2i t2) {
             const rc_v4i av = rc_v4i{t1.x, t1.y, t2.x, t2.y};
             rc_v4i dh = rc_v4i{0, 0, 0, 0}, dl = rc_v4i{sd, sd, sd, sd};
@@ -382,18 +371,17 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
             lds_wr32(iq + 16 * ct,
                      rc_round4s((dh[0] << 6) + dl[0], (dh[1] << 6) + dl[1], (dh[2] << 6) + dl[2], (dh[3] << 6) + dl[3]));
         };
-            constexpr int CS = OB == 2 ? 1 : WV;  // column stride of a wave's tiles
-            for (int ct = OB == 2 ? cb : wave; ct < ce; ct += 2 * CS) {
-                const bool two = ct + CS < ce;  // uniform
+            for (int ct = wave; ct < cpr; ct += 2 * WV) {
+                const bool two = ct + WV < cpr;  // uniform
                 rc_v2i t1a = lds_tr8(a1 + 16 * ct), t2a = lds_tr8(a2 + 16 * ct);
                 rc_v2i t1b = t1a, t2b = t2a;
                 if (two) {
-                    t1b = lds_tr8(a1 + 16 * (ct + CS));
-                    t2b = lds_tr8(a2 + 16 * (ct + CS));
+                    t1b = lds_tr8(a1 + 16 * (ct + WV));
+                    t2b = lds_tr8(a2 + 16 * (ct + WV));
                 }
                 lgkm_wait_for<0>(t1a, t2a, t1b, t2b);
                 tile(ct, t1a, t2a);
-                if (two) tile(ct + CS, t1b, t2b);
+                if (two) tile(ct + WV, t1b, t2b);
             }
     };
     // horizontal pass: units wave + WV i, operands from registers, every unit's LDS
@@ -402,11 +390,11 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // lanes in one 32-lane half on banks 0-1 / 2-3 (mod 4) each read is conflict-free
     // (both halves of one K block at once were 2-way); MIPX_RCOL_SWZ=0 keeps the old order
     const int hsw = a.swz && (kg & 1) ? 8 : 0, hsd = 8 - 2 * hsw;
-    auto horizontal = [&](uint32_t *res, uint32_t ib) {
+    auto horizontal = [&](uint32_t *res) {
         rc_u2x2 q[UPW][NKS];
 #pragma unroll
         for (int i = 0; i < UPW; ++i) {
-            const uint32_t ir = ib + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg + hsw);
+            const uint32_t ir = inter_l + static_cast<uint32_t>(n * a.iw + kb[i] + 16 * kg + hsw);
 #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
                 // two ds_read_b64 (2 LDS cycles each) rather than one ds_read2_b64 (16): -0.3 to -2 %
@@ -449,50 +437,13 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         if (live) {
             if (!first) write_ring(pc, srow[2 * (k - 1) + 1]);
             rc_barrier();
-            vertical(pc, srow[2 * k], inter_l);
+            vertical(pc, srow[2 * k]);
         }
         issue_ring(pc, srow[2 * (k + 1) + 1]);
         issue_taps(pc, k + 2);
         if (live) {
             rc_barrier();
-            horizontal(res, inter_l);
-        }
-        store(k, live, res);
-    };
-    // OB: step k's vertical pass (vlive) into buffer P, then step k - 1's horizontal pass
-    // (hlive) from buffer 1 - P and its stores; the one barrier covers both.  Loads no later
-    // step writes to the ring go out of range (no memory access), as the loop's phantom
-    // steps' do
-    const int kend = ka + steps;
-    auto body1 = [&](auto pc, int k, bool vlive, bool hlive, bool first) {
-        constexpr int P = decltype(pc)::value;
-        uint32_t res[UPW];
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) res[i] = 0u;
-        if (vlive && !first) write_ring(pc, srow[2 * (k - 1) + 1]);
-        if (vlive || hlive) rc_barrier();
-        if (vlive) vertical(pc, srow[2 * k], P ? inter2 : inter_l);
-        issue_ring(pc, srow[2 * (k + 1) + 1], k + 2 < kend);
-        issue_taps(pc, k + 2);
-        if (hlive) horizontal(res, P ? inter_l : inter2);
-        store(k - 1, hlive, res);
-    };
-    // OB 2: the wave's own ring columns -> vertical into buffer P -> loads -> barrier ->
-    // horizontal from buffer P -> stores
-    auto body2 = [&](auto pc, int k, bool live, bool first) {
-        constexpr int P = decltype(pc)::value;
-        uint32_t res[UPW];
-#pragma unroll
-        for (int i = 0; i < UPW; ++i) res[i] = 0u;
-        if (live) {
-            if (!first) write_ring(pc, srow[2 * (k - 1) + 1]);
-            vertical(pc, srow[2 * k], P ? inter2 : inter_l);
-        }
-        issue_ring(pc, srow[2 * (k + 1) + 1], k + 2 < kend);
-        issue_taps(pc, k + 2);
-        if (live) {
-            rc_barrier();
-            horizontal(res, P ? inter2 : inter_l);
+            horizontal(res);
         }
         store(k, live, res);
     };
@@ -503,26 +454,68 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // pipeline's first loads (r05: issuing those before the prime's ring writes measured
     // within +-1 %, and the extra live registers spilled in the 4-wave build,
     // profiles/r05/prime_ab.jsonl) ----
+    // r06: the first two steps' tap fragments go out before the prime (they depend on ka
+    // only), so their round trip overlaps the prime's row loads instead of following them
+    // (the set-up and prime alone were 16-22 % of a small-image launch,
+    // profiles/r06/rcol_setup_probe_ab.jsonl); MIPX_RCOL_TEARLY=0: after the prime (A/B)
+    const bool tearly = KMAX == 3 && a.tearly;  // (KMAX 6: the live registers would cost a wave per SIMD)
+    if (tearly) {
+        issue_taps(I0{}, ka);
+        issue_taps(I1{}, ka + 1);
+    }
     const int bka = srow[2 * ka], eka = srow[2 * ka + 1];
-    for (int r = bka; r < eka; r += lkf) {
-        rc_u4 tv[KMAX];
-        uint32_t te[UNAL ? KMAX : 1];
+    // the prime's row batches through the two (still idle) pipeline register sets, the
+    // next batch's loads in flight while this one is written (r06, MIPX_RCOL_PPIPE=0: one
+    // batch at a time, A/B)
+    auto pload = [&](auto pc, int r) {
+        constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
             const int off = chunk_off(r, j);
-            tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
-            if constexpr (UNAL) te[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
+            rv[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
+            if constexpr (UNAL) re[P][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
         }
+    };
+    auto pwrite = [&](auto pc, int r) {
+        constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             if (rr[j] < lkf && r + rr[j] < eka)
                 lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j],
-                          realign(tv[j], te[UNAL ? j : 0], chunk_off(r, j)) ^ 0x80808080u);
+                          realign(rv[P][j], re[P][UNAL ? j : 0], chunk_off(r, j)) ^ 0x80808080u);
+    };
+    if (KMAX == 3 && a.ppipe) {  // (KMAX 6: the second live set would cost a wave per SIMD)
+        pload(I0{}, bka);
+        for (int r = bka; r < eka; r += 2 * lkf) {
+            const bool two = r + lkf < eka;  // uniform
+            if (two) pload(I1{}, r + lkf);
+            pwrite(I0{}, r);
+            if (two) {
+                if (r + 2 * lkf < eka) pload(I0{}, r + 2 * lkf);
+                pwrite(I1{}, r + lkf);
+            }
+        }
+    } else {
+        for (int r = bka; r < eka; r += lkf) {
+            rc_u4 tv[KMAX];
+            uint32_t te[UNAL ? KMAX : 1];
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                const int off = chunk_off(r, j);
+                tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
+                if constexpr (UNAL) te[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
+            }
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j)
+                if (rr[j] < lkf && r + rr[j] < eka)
+                    lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j],
+                              realign(tv[j], te[UNAL ? j : 0], chunk_off(r, j)) ^ 0x80808080u);
+        }
     }
-    issue_taps(I0{}, ka);
+    if (!tearly) issue_taps(I0{}, ka);
     store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
     issue_ring(I1{}, eka);
-    issue_taps(I1{}, ka + 1);
+    if (!tearly) issue_taps(I1{}, ka + 1);
     store(ka, false, zero);
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
@@ -561,21 +554,9 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         }
         return;
     }
-    if constexpr (OB == 2) {
-        for (int s = 0; s < steps; s += 2) {
-            body2(I0{}, ka + s, true, s == 0);
-            body2(I1{}, ka + s + 1, s + 1 < steps, false);
-        }
-    } else if constexpr (OB == 1) {
-        for (int s = 0; s <= steps; s += 2) {
-            body1(I0{}, ka + s, s < steps, s > 0, s == 0);
-            body1(I1{}, ka + s + 1, s + 1 < steps, s + 1 <= steps, false);
-        }
-    } else {
-        for (int s = 0; s < steps; s += 2) {
-            body(I0{}, ka + s, true, s == 0);
-            body(I1{}, ka + s + 1, s + 1 < steps, false);
-        }
+    for (int s = 0; s < steps; s += 2) {
+        body(I0{}, ka + s, true, s == 0);
+        body(I1{}, ka + s + 1, s + 1 < steps, false);
     }
 }
 
@@ -675,14 +656,22 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     if (nks > 2) return MIPX_EUNSUPPORTED;
     // chunks per lane: the widest strip's rows of the largest step fit one batch; ring:
     // the rows of a step, and a batch's rows (at most the rows one step adds) must only
-    // land on slots of rows above the step's first.  r06, one barrier per step (OB, the
-    // kernel's comment; MIPX_RCOL_1B=0 / 1 / 2, default 2): OB 2 stages each wave's own
-    // columns (64 lanes over a quarter of the columns); OB 1 needs the ring to hold a step's
-    // rows and the next step's new rows at once
+    // land on slots of rows above the step's first
+    int kmax = 0, ring = 0;
     const int rcap = std::max(maxnew, 1);
-    const char *e1b = tune_env("MIPX_RCOL_1B");
-    int ob = (e1b && *e1b) ? std::atoi(e1b) : 2;
-    if (ob < 0 || ob > 2) ob = 2;
+    for (int km : {3, 6}) {
+        if ((kRcNT * km) / cpr_max < rcap) continue;
+        const int reach = std::min((kRcNT * km + cpr_min - 1) / cpr_min, rcap);
+        for (int r : {32, 64}) {
+            bool ok = lmax <= r;
+            for (int k = a.k0 + 1; ok && k <= k1; ++k) ok = ge(k - 1) + reach <= gb(k) + r;
+            if (ok) { ring = r; break; }
+        }
+        if (ring) { kmax = km; break; }
+    }
+    if (!kmax) return MIPX_EUNSUPPORTED;
+    a.rmask = ring - 1;
+    a.rcap = rcap;
     int rs = 4 * cpr_max;  // dwords
     while (((rs & 63) >> 2) % 2 == 0) rs += 4;  // 16 consecutive rows on distinct bank quads
     a.rs = 4 * rs;
@@ -690,39 +679,12 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     while ((iw / 4) % 8 != 4) iw += 16;  // 4 mod 8 dwords: the intermediate writes hit distinct banks
     a.iw = iw;
     // + the wave store tiles (4 x 16 rows x (16 B + 16 for RGBA))
-    auto lds_of = [&](int rg, int o) {
-        return static_cast<size_t>(rg) * a.rs + static_cast<size_t>(o ? 2 : 1) * kRcRows * iw +
-               static_cast<size_t>(4 * kRcRows * (16 * b + (b == 4 ? 16 : 0)));
-    };
-    int kmax = 0, ring = 0;
-    auto choose = [&](int o) {  // kmax and ring for one-barrier mode o, false when none fits
-        kmax = ring = 0;
-        const int lanes = o == 2 ? 64 : kRcNT;
-        const int cmax = o == 2 ? (cpr_max + 3) / 4 : cpr_max, cmin = o == 2 ? std::max(1, cpr_min / 4) : cpr_min;
-        for (int km : {3, 6}) {
-            if ((lanes * km) / cmax < rcap) continue;
-            const int reach = std::min((lanes * km + cmin - 1) / cmin, rcap);
-            for (int r : {32, 64}) {
-                bool ok = lmax <= r;
-                if (o == 1)
-                    for (int k = a.k0; ok && k < k1; ++k) ok = ge(k) + reach <= gb(k) + r;
-                else
-                    for (int k = a.k0 + 1; ok && k <= k1; ++k) ok = ge(k - 1) + reach <= gb(k) + r;
-                if (ok) { ring = r; break; }
-            }
-            if (ring) { kmax = km; break; }
-        }
-        // one-barrier builds keep 3 blocks per CU (the VGPR limit) within the LDS
-        return kmax > 0 && lds_of(ring, o) <= (o ? 48 : 64) * 1024;
-    };
-    if (ob && !choose(ob)) ob = 0;
-    if (!ob && !choose(0)) return MIPX_EUNSUPPORTED;
-    a.rmask = ring - 1;
-    a.rcap = rcap;
-    const size_t lds = lds_of(ring, ob);
+    const size_t lds = static_cast<size_t>(ring) * a.rs + static_cast<size_t>(kRcRows) * iw +
+                       static_cast<size_t>(4 * kRcRows * (16 * b + (b == 4 ? 16 : 0)));
+    if (lds > 64 * 1024) return MIPX_EUNSUPPORTED;
 
     int plan_rows = 0;
-    a.plan = device_rcol_vplan(vs, centre, kRcRows * (k1 + 5), &plan_rows);  // steps past k1: the pipeline's idle tail
+    a.plan = device_rcol_vplan(vs, centre, kRcRows * (k1 + 3), &plan_rows);
     a.plan_rows = plan_rows;
     int nth = 0, ntf = 0, nfh = 0;
     const int *sumh = nullptr;
@@ -741,16 +703,18 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     const char *edb = tune_env("MIPX_RCOL_DBG");
     a.dbg = edb && *edb ? std::atoi(edb) : 0;
 #endif
+    const char *epp = tune_env("MIPX_RCOL_PPIPE");
+    a.ppipe = !(epp && *epp == '0');
+    const char *ete = tune_env("MIPX_RCOL_TEARLY");
+    a.tearly = !(ete && *ete == '0');
     const char *etr = tune_env("MIPX_RCOL_TRL");
     a.trl = !(etr && *etr == '0');
     const char *esz = tune_env("MIPX_RCOL_SWZ");
     a.swz = !(esz && *esz == '0');
     const void *fn = nullptr;
-#define MIPX_RC_O(U_, B_, NKS_, KM_, W_)                                                                     \
-    (ob == 2   ? reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, W_, U_, 2>)                           \
-     : ob == 1 ? reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, W_, U_, 1>)                           \
-               : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, W_, U_, 0>))
-#define MIPX_RC_K(B_, NKS_, KM_) fn = unal ? MIPX_RC_O(true, 3, NKS_, KM_, 1) : MIPX_RC_O(false, B_, NKS_, KM_, 1);
+#define MIPX_RC_K(B_, NKS_, KM_)                                                                  \
+    fn = unal ? reinterpret_cast<const void *>(&k_rcol<3, NKS_, KM_, 1, true>)                     \
+              : reinterpret_cast<const void *>(&k_rcol<B_, NKS_, KM_, 1>);
 #define MIPX_RC_KM(B_, NKS_) \
     if (kmax == 3) { MIPX_RC_K(B_, NKS_, 3) } else { MIPX_RC_K(B_, NKS_, 6) }
     if (b == 3) {
@@ -793,7 +757,8 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     const char *ew4 = tune_env("MIPX_RCOL_W4");
     const bool force4 = ew4 && *ew4 == '1';
     if (nks == 1 && kmax == 3 && !unal && (b == 3 || force4)) {
-        const void *f4 = b == 3 ? MIPX_RC_O(false, 3, 1, 3, 4) : MIPX_RC_O(false, 4, 1, 3, 4);
+        const void *f4 = b == 3 ? reinterpret_cast<const void *>(&k_rcol<3, 1, 3, 4>)
+                                : reinterpret_cast<const void *>(&k_rcol<4, 1, 3, 4>);
         int segs4 = 1;
         const auto p4 = plan(f4, &segs4);
         if (force4 || (p4.second == 1 && p4.first < best - 1e-9)) {
@@ -801,7 +766,6 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
             best_segs = segs4;
         }
     }
-#undef MIPX_RC_O
     a.seg_steps = (a.ksteps + best_segs - 1) / best_segs;
     a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
     const long long blocks = cols * a.segs;

@@ -528,7 +528,10 @@ bool reduce2_eligible(const u8 *in, int w, int h, int b, double hs, double vs) {
 
 // k_reduce2x2 build variant.  Only the shipped one (66) is compiled now; the r01 / r02
 // A/B builds (strip widths, register prefetch, LDS row strides) are recorded under
-// profiles/r01 and profiles/r02 (scripts/ab_reduce.py, in git history, ran them).
+// profiles/r01 and profiles/r02 (scripts/ab_reduce.py, in git history, ran them).  r06's
+// cache-policy A/B compiled 66 | 16 / 32 / 48 (82 / 98 / 114: non-temporal loads / stores /
+// both, the LAUX / NTS parameters of reduce2_tile) as extra cases here: -15 % / +0.2 % /
+// -14 % (profiles/r06/c2_nt_ab.jsonl), so none is kept.
 constexpr int kR2Default = 66;  // wide strips, R = 12 + register prefetch: measured best (profiles/r01/v10_wide_ab.log)
 int reduce2_variant() {
     const char *e = tune_env("MIPX_R2_VARIANT");

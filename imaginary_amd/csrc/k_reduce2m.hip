@@ -91,21 +91,13 @@ struct R2mArgs {
     int pp;                 // prime: both row batches in flight together
 };
 
-// W1 (r06): one barrier per step.  Each wave stages the ring columns its own vertical
-// tiles read (a contiguous quarter of the strip's 16-byte columns), so ring writes and
-// vertical reads never cross waves and need no barrier; the intermediate is
-// double-buffered (step s in buffer s & 1), so the one barrier between the vertical and
-// the horizontal pass also orders the next step's vertical after this step's reads:
-//   vertical (ring -> inter[s & 1]) -> next rows to the ring, next loads -> barrier ->
-//   [COPY fix-up -> barrier] -> horizontal (inter[s & 1] -> output tile -> HBM)
-template <int B, bool W1>
+template <int B>
 __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     using G = R2M<B>;
-    constexpr int RS = G::RS, CPR = G::CPR, RG = kMRing, IS = G::IS;
-    constexpr int NCW = (CPR + 3) / 4;                        // W1: columns per wave (at most)
-    constexpr int KM = W1 ? (32 * NCW + 63) / 64 : G::KM;     // staged chunks per lane per 32 rows
-    __shared__ __attribute__((aligned(16))) u8 smem[RG * RS + (W1 ? 2 : 1) * kMN * IS];
-    const uint32_t ring_l = rc_lds(smem), inter_l0 = ring_l + RG * RS;
+    constexpr int RS = G::RS, CPR = G::CPR, KM = G::KM, RG = kMRing, IS = G::IS;
+    __shared__ __attribute__((aligned(16))) u8 smem[RG * RS + kMN * IS];
+    const uint32_t ring_l = rc_lds(smem), inter_l = ring_l + RG * RS;
+    u8 *inter = smem + RG * RS;
     auto slot = [](int r) { return static_cast<uint32_t>(r + 2 * RG) % static_cast<uint32_t>(RG); };  // r >= -5
 
     const uint32_t t = xcd_remap(blockIdx.x, gridDim.x);
@@ -132,16 +124,14 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     const __amdgpu_buffer_rsrc_t src = image_rsrc(a.in + img * a.in_img, a.in_img);
     u8 *dst = a.out + img * a.out_img;
 
-    // ---- staging: chunk c = tid + 256 j of a 32-row batch is (row rr, 16-byte column col);
-    // W1: chunk c = lane + 64 j of the wave's columns [cb, ce) ----
+    // ---- staging: chunk c = tid + 256 j of a 32-row batch is (row rr, 16-byte column col) ----
     // packed (row rr << 16 | 16 col), one register per chunk
-    const int cb = W1 ? (wave * CPR) / 4 : 0, ce = W1 ? ((wave + 1) * CPR) / 4 : CPR, ncw = ce - cb;
     uint32_t sg[KM];
 #pragma unroll
     for (int j = 0; j < KM; ++j) {
-        const int c = (W1 ? lane + 64 * j : tid + kMNT * j);
-        const int r = c < 32 * ncw ? c / ncw : 64;  // 64: idle
-        sg[j] = static_cast<uint32_t>(r << 16 | 16 * (cb + c - (c / ncw) * ncw));
+        const int c = tid + kMNT * j;
+        const int r = c < 32 * CPR ? c / CPR : 64;  // 64: idle
+        sg[j] = static_cast<uint32_t>(r << 16 | 16 * (c - (c / CPR) * CPR));
     }
     // a chunk left of the image (negative offset) reads zeros whole: the edge fix-up
     // replaces those pixels; rows clamp to the image (COPY edge)
@@ -199,9 +189,7 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     for (int s = 0; s < nst; ++s) {
         const int k = kf + dk * s;
         const int bk = 32 * k - 5;
-        const uint32_t inter_l = inter_l0 + (W1 ? static_cast<uint32_t>((s & 1) * kMN * IS) : 0u);
-        u8 *inter = smem + (inter_l - ring_l);
-        if constexpr (!W1) rc_barrier();  // ring rows of step k staged; the intermediate free
+        rc_barrier();  // ring rows of step k staged; the intermediate free
         // ---- vertical: 16-byte column tiles dealt to the waves ----
         {
             const int r1 = bk + 8 * kg + (n >> 1);
@@ -225,13 +213,12 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
             // waves per SIMD at 80 VGPRs needs VB = HB = 1 for RGB: -1.4 % from the occupancy,
             // +2 % from the serialised reads, profiles/r04/reduce2m/h_otile_occupancy_ab.jsonl)
             constexpr int VB = 4;
-            constexpr int CS = W1 ? 1 : 4;  // column stride of a wave's tiles
-            for (int c0 = W1 ? cb : wave; c0 < ce; c0 += CS * VB) {
+            for (int c0 = wave; c0 < CPR; c0 += 4 * VB) {
                 rc_v2i p[VB][2];
 #pragma unroll
                 for (int i = 0; i < VB; ++i) {
-                    const int ct = c0 + CS * i;
-                    if (ct < ce) {
+                    const int ct = c0 + 4 * i;
+                    if (ct < CPR) {
                         p[i][0] = lds_tr8(a1 + 16 * ct);
                         p[i][1] = lds_tr8(a2 + 16 * ct);
                     } else {
@@ -243,21 +230,13 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                 else lgkm_wait_for<0>(p[0][0], p[0][1]);
 #pragma unroll
                 for (int i = 0; i < VB; ++i)
-                    if (c0 + CS * i < ce) tile(c0 + CS * i, p[i][0], p[i][1]);
+                    if (c0 + 4 * i < CPR) tile(c0 + 4 * i, p[i][0], p[i][1]);
             }
         }
-        if constexpr (W1) {  // the wave's own ring columns are read: stage the next rows first
-            if (s + 1 < nst) {
-                store_ring(pf, new_rows(k), 32);
-                if (s + 2 < nst) load(pf, new_rows(k + dk), 32);
-            }
-        }
-        rc_barrier();  // the intermediate complete; (two barriers) the ring's rows of step k read
-        if constexpr (!W1) {
-            if (s + 1 < nst) {
-                store_ring(pf, new_rows(k), 32);
-                if (s + 2 < nst) load(pf, new_rows(k + dk), 32);
-            }
+        rc_barrier();  // the intermediate complete; the ring's rows of step k read
+        if (s + 1 < nst) {
+            store_ring(pf, new_rows(k), 32);
+            if (s + 2 < nst) load(pf, new_rows(k + dk), 32);
         }
         if (edge) {  // EXTEND_COPY: strip pixels outside the image copy the edge pixel
             const int nfill = nl + nr;
@@ -440,18 +419,8 @@ int reduce2m_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
     const long long blocks = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const dim3 grid(static_cast<unsigned>(blocks)), blk(kMNT);
-    // r06: one barrier per step (wave-owned ring columns, double-buffered intermediate);
-    // MIPX_R2M_1B=0 keeps the two-barrier step (A/B)
-    // (RGB by default: RGBA's doubled intermediate costs a workgroup per CU; 1 forces it)
-    const char *e1 = tune_env("MIPX_R2M_1B");
-    const bool w1 = (e1 && *e1) ? *e1 == '1' : b == 3;
-    if (b == 3) {
-        if (w1) hipLaunchKernelGGL((k_reduce2m<3, true>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_reduce2m<3, false>), grid, blk, 0, st, a);
-    } else {
-        if (w1) hipLaunchKernelGGL((k_reduce2m<4, true>), grid, blk, 0, st, a);
-        else hipLaunchKernelGGL((k_reduce2m<4, false>), grid, blk, 0, st, a);
-    }
+    if (b == 3) hipLaunchKernelGGL(k_reduce2m<3>, grid, blk, 0, st, a);
+    else hipLaunchKernelGGL(k_reduce2m<4>, grid, blk, 0, st, a);
     return launch_check("k_reduce2m");
 }
 

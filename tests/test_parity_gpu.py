@@ -70,19 +70,14 @@ def test_reduce_unaligned_batches(gpu, oracle, rng, h, w, b, hs, vs):
         assert_same(blur[i], oracle.gaussblur(imgs[i], 1.7, 0.2), f"blur {h}x{w}x{b} img{i}")
 
 
-@pytest.mark.parametrize("one_barrier", ["", "0", "1"])
 @pytest.mark.parametrize("band", ["", "1", "16"])
-def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, band, one_barrier, monkeypatch):
+def test_reduce2x2_variants_exact(gpu, oracle, rng, convention, band, monkeypatch):
     """The fused 2x2 kernels (corner: k_reduce2x2 variant 66, the r01/r02 A/B builds are
     recorded under profiles/ and no longer compiled; centre: k_reduce2m, both passes on
-    the matrix cores, at its default band and at 1 / 16 steps per band, with the one-barrier
-    step (r06: wave-owned ring columns; default for RGB, MIPX_R2M_1B=1 for RGBA too) and
-    the two-barrier one (0)) are bit-exact, including strips that end at the image edge,
-    images shorter than a band and the smallest eligible sizes."""
-    if one_barrier and convention != "centre":
-        pytest.skip("k_reduce2m runs at the centre convention only")
+    the matrix cores, at its default band and at 1 / 16 steps per band) are bit-exact,
+    including strips that end at the image edge, images shorter than a band and the
+    smallest eligible sizes."""
     monkeypatch.setenv("MIPX_R2M_BAND", band)
-    monkeypatch.setenv("MIPX_R2M_1B", one_barrier)
     for h, w, b in ((270, 480, 3), (130, 260, 4), (37, 52, 3), (61, 1001 * 4 // 4 - 1, 4), (200, 646, 3),
                     (8, 8, 4), (9, 12, 3), (25, 164, 3), (131, 1000, 4), (1081, 324, 3), (16, 3840, 3)):
         if (w * b) % 4:

@@ -5,9 +5,8 @@ a step, segment boundaries in tall images, RGB and RGBA, shrink pairs across
 (1, 2.75), windows (reduce -> extract), unaligned output rows (byte stores) and a
 seeded fuzz over shapes.  RGB input rows off a dword (r05) run k_rcol's realigning
 build (MIPX_RCOL_UNAL=0 leaves them to k_rmf2, as the norcol route does); horizontal K
-origins on 4 bytes where that saves a K step (r05, MIPX_RCOL_K4=0: 8 bytes).  r06: one
-barrier per step (MIPX_RCOL_1B: 2 wave-owned ring columns, the default; 1 a shared ring
-holding two steps' rows; 0 the two-barrier step)."""
+origins on 4 bytes where that saves a K step (r05, MIPX_RCOL_K4=0: 8 bytes).  RGBA store
+tiles read back by tile_rd_lane (r06, MIPX_RCOL_TRL=0: lane / 4)."""
 import numpy as np
 import pytest
 
@@ -16,15 +15,15 @@ from test_parity_gpu import assert_same, rand_img, smooth_img
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["rcol", "rcol4b", "rcol1b1", "rcol2b", "norcol"])
+@pytest.fixture(autouse=True, params=["rcol", "rcol4b", "rcoltrl0", "norcol"])
 def route(request, monkeypatch):
     """Every case through k_rcol (the default: 16-byte row pieces through a wave
-    tile, one barrier per step with wave-owned ring columns), k_rcol with 4-byte stores
-    (MIPX_RCOL_WST=0), the shared-ring one-barrier step (MIPX_RCOL_1B=1), the two-barrier
-    step (0), and the kernels behind it (MIPX_RCOL=0: k_rmf2 and the strip walker)."""
+    tile), k_rcol with 4-byte stores (MIPX_RCOL_WST=0), with r05's tile read-back order
+    (MIPX_RCOL_TRL=0), and the kernels behind it (MIPX_RCOL=0: k_rmf2 and the strip
+    walker)."""
     monkeypatch.setenv("MIPX_RCOL", "0" if request.param == "norcol" else "")
     monkeypatch.setenv("MIPX_RCOL_WST", "0" if request.param == "rcol4b" else "")
-    monkeypatch.setenv("MIPX_RCOL_1B", {"rcol1b1": "1", "rcol2b": "0"}.get(request.param, ""))
+    monkeypatch.setenv("MIPX_RCOL_TRL", "0" if request.param == "rcoltrl0" else "")
     yield request.param
 
 SHRINKS = [(1.6, 1.6), (1.3333333333333333, 1.3333333333333333), (2.4, 2.4), (1.02, 1.9), (2.7, 1.5),
