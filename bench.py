@@ -159,7 +159,8 @@ def c1_cpu_reference(args, sampling):
 
 # the newest committed PMC traffic record of the C2 kernel (profiles/<round>/traffic_*.json:
 # one record, or {"records": [...]}, each naming its kernel)
-TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", "r05", "traffic_r05.json"),
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", "r06", "traffic_r06.json"),
+                 os.path.join(ROOT, "profiles", "r05", "traffic_r05.json"),
                  os.path.join(ROOT, "profiles", "r04", "traffic_r04.json"),
                  os.path.join(ROOT, "profiles", "r03", "traffic_r03.json"),
                  os.path.join(ROOT, "profiles", "r02", "traffic_r02.json"),

@@ -81,8 +81,6 @@ struct RcArgs {
     int allst;                // A/B: every strip issues the edge-piece dword stores (r05 before)
     int skipl;                // ring load batches no lane of the wave needs are not issued
     int trl;                  // RGBA store tile read back by tile_rd_lane (r06)
-    int tearly;               // the first two steps' tap fragments loaded before the prime (r06)
-    int ppipe;                // the prime's row batches pipelined (r06)
     int dbg;                  // MIPX_RCOL_DBG (PROBES builds only): 1 = set-up and prime, no steps
 };
 #ifdef MIPX_PROBES
@@ -454,68 +452,26 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // pipeline's first loads (r05: issuing those before the prime's ring writes measured
     // within +-1 %, and the extra live registers spilled in the 4-wave build,
     // profiles/r05/prime_ab.jsonl) ----
-    // r06: the first two steps' tap fragments go out before the prime (they depend on ka
-    // only), so their round trip overlaps the prime's row loads instead of following them
-    // (the set-up and prime alone were 16-22 % of a small-image launch,
-    // profiles/r06/rcol_setup_probe_ab.jsonl); MIPX_RCOL_TEARLY=0: after the prime (A/B)
-    const bool tearly = KMAX == 3 && a.tearly;  // (KMAX 6: the live registers would cost a wave per SIMD)
-    if (tearly) {
-        issue_taps(I0{}, ka);
-        issue_taps(I1{}, ka + 1);
-    }
     const int bka = srow[2 * ka], eka = srow[2 * ka + 1];
-    // the prime's row batches through the two (still idle) pipeline register sets, the
-    // next batch's loads in flight while this one is written (r06, MIPX_RCOL_PPIPE=0: one
-    // batch at a time, A/B)
-    auto pload = [&](auto pc, int r) {
-        constexpr int P = decltype(pc)::value;
+    for (int r = bka; r < eka; r += lkf) {
+        rc_u4 tv[KMAX];
+        uint32_t te[UNAL ? KMAX : 1];
 #pragma unroll
         for (int j = 0; j < KMAX; ++j) {
             const int off = chunk_off(r, j);
-            rv[P][j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
-            if constexpr (UNAL) re[P][j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
+            tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
+            if constexpr (UNAL) te[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
         }
-    };
-    auto pwrite = [&](auto pc, int r) {
-        constexpr int P = decltype(pc)::value;
 #pragma unroll
         for (int j = 0; j < KMAX; ++j)
             if (rr[j] < lkf && r + rr[j] < eka)
                 lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j],
-                          realign(rv[P][j], re[P][UNAL ? j : 0], chunk_off(r, j)) ^ 0x80808080u);
-    };
-    if (KMAX == 3 && a.ppipe) {  // (KMAX 6: the second live set would cost a wave per SIMD)
-        pload(I0{}, bka);
-        for (int r = bka; r < eka; r += 2 * lkf) {
-            const bool two = r + lkf < eka;  // uniform
-            if (two) pload(I1{}, r + lkf);
-            pwrite(I0{}, r);
-            if (two) {
-                if (r + 2 * lkf < eka) pload(I0{}, r + 2 * lkf);
-                pwrite(I1{}, r + lkf);
-            }
-        }
-    } else {
-        for (int r = bka; r < eka; r += lkf) {
-            rc_u4 tv[KMAX];
-            uint32_t te[UNAL ? KMAX : 1];
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) {
-                const int off = chunk_off(r, j);
-                tv[j] = __builtin_bit_cast(rc_u4, __builtin_amdgcn_raw_buffer_load_b128(src, UNAL ? off & ~3 : off, 0, 0));
-                if constexpr (UNAL) te[j] = static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(src, (off & ~3) + 16, 0, 0));
-            }
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j)
-                if (rr[j] < lkf && r + rr[j] < eka)
-                    lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j],
-                              realign(tv[j], te[UNAL ? j : 0], chunk_off(r, j)) ^ 0x80808080u);
-        }
+                          realign(tv[j], te[UNAL ? j : 0], chunk_off(r, j)) ^ 0x80808080u);
     }
-    if (!tearly) issue_taps(I0{}, ka);
+    issue_taps(I0{}, ka);
     store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
     issue_ring(I1{}, eka);
-    if (!tearly) issue_taps(I1{}, ka + 1);
+    issue_taps(I1{}, ka + 1);
     store(ka, false, zero);
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
@@ -703,10 +659,6 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     const char *edb = tune_env("MIPX_RCOL_DBG");
     a.dbg = edb && *edb ? std::atoi(edb) : 0;
 #endif
-    const char *epp = tune_env("MIPX_RCOL_PPIPE");
-    a.ppipe = !(epp && *epp == '0');
-    const char *ete = tune_env("MIPX_RCOL_TEARLY");
-    a.tearly = !(ete && *ete == '0');
     const char *etr = tune_env("MIPX_RCOL_TRL");
     a.trl = !(etr && *etr == '0');
     const char *esz = tune_env("MIPX_RCOL_SWZ");
