@@ -81,7 +81,8 @@ struct RcArgs {
     int allst;                // A/B: every strip issues the edge-piece dword stores (r05 before)
     int skipl;                // ring load batches no lane of the wave needs are not issued
     int trl;                  // RGBA store tile read back by tile_rd_lane (r06)
-    int dbg;                  // MIPX_RCOL_DBG (PROBES builds only): 1 = set-up and prime, no steps
+    int dbg;                  // MIPX_RCOL_DBG (PROBES builds only): 1 = set-up and prime, no steps; 2 = a third
+                              // barrier + the horizontal pass twice, 3 = the vertical pass twice, 4 = both
 };
 #ifdef MIPX_PROBES
 __device__ __forceinline__ int rc_dbg(const RcArgs &a) { return a.dbg; }
@@ -436,12 +437,20 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
             if (!first) write_ring(pc, srow[2 * (k - 1) + 1]);
             rc_barrier();
             vertical(pc, srow[2 * k]);
+            if (rc_dbg(a) >= 3) vertical(pc, srow[2 * k]);  // probe: the vertical pass twice (same result)
         }
         issue_ring(pc, srow[2 * (k + 1) + 1]);
         issue_taps(pc, k + 2);
         if (live) {
             rc_barrier();
             horizontal(res);
+            if (rc_dbg(a) == 2 || rc_dbg(a) == 4) {  // probe: a third barrier and the horizontal pass twice (wrong pixels)
+                uint32_t r2[UPW];
+                rc_barrier();
+                horizontal(r2);
+#pragma unroll
+                for (int i = 0; i < UPW; ++i) res[i] += r2[i];
+            }
         }
         store(k, live, res);
     };
