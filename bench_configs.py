@@ -203,6 +203,13 @@ def c3(args, dev, sp, stream):
         assert e == 0
         px = o.execute(rp, px)
     ok = bool(np.array_equal(g.y[0].cpu().numpy().reshape(px.shape), px))
+    if ok and (len(subs) > 1 or g.n > 1):  # the batch's last image too (a later chunk under MIPX_PIPE)
+        gl = subs[-1]
+        px = gl.x[gl.n - 1].cpu().numpy().reshape(2048, 2048, 4)
+        for opts, p in zip(stages, plans):
+            e, rp = o.plan(opts, dict(w=p.in_w, h=p.in_h, bands=p.in_bands, type=3))
+            px = o.execute(rp, px)
+        ok = bool(np.array_equal(gl.y[gl.n - 1].cpu().numpy().reshape(px.shape), px))
     wall, dev_ms = time_groups(run_all, args.steps, args.warmup, stream)
     line("C3", "pipeline resize(w=1024)+crop(768x512)+blur(sigma=5), 2048^2 RGBA", n, wall, dev_ms,
          sum(x.in_bytes + x.out_bytes for x in subs), ok, {"batch": n, "split": k, "fused_plan": g.plan.describe()})
