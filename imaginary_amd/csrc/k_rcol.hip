@@ -82,7 +82,9 @@ struct RcArgs {
     int skipl;                // ring load batches no lane of the wave needs are not issued
     int trl;                  // RGBA store tile read back by tile_rd_lane (r06)
     int dbg;                  // MIPX_RCOL_DBG (PROBES builds only): 1 = set-up and prime, no steps; 2 = a third
-                              // barrier + the horizontal pass twice, 3 = the vertical pass twice, 4 = both
+                              // barrier + the horizontal pass twice, 3 = the vertical pass twice, 4 = both;
+                              // 8 = per-step phase stamps (s_memtime) into stamps
+    unsigned long long *stamps;  // PROBES, dbg 8: [block][2 + 8 seg_steps]
 };
 #ifdef MIPX_PROBES
 __device__ __forceinline__ int rc_dbg(const RcArgs &a) { return a.dbg; }
@@ -181,6 +183,13 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     const __amdgpu_buffer_rsrc_t prs = image_rsrc(a.plan, static_cast<long long>(a.plan_rows) * kRcolPlanRow);
     rc_cint *srow = (rc_cint *)(a.plan + static_cast<size_t>(a.plan_rows) * kRcolPlanRow);  // [group][first, end]
     const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
+    // PROBES, dbg 8: wave 0 lane 0 stamps the block's start / end and each step's phases
+    unsigned long long *stp = nullptr;
+    if (rc_dbg(a) == 8 && tid == 0) stp = a.stamps + static_cast<size_t>(blockIdx.x) * (2 + 8 * a.seg_steps);
+    auto stamp = [&](int slot) {
+        if (rc_dbg(a) == 8 && stp) stp[slot] = __builtin_amdgcn_s_memtime();
+    };
+    stamp(0);
 
     // ---- per-segment set-up: horizontal operands (registers, COPY edge folded) ----
     // every operand load issued before the first is used (one memory round trip)
@@ -431,19 +440,27 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // (live = false, the odd tail of a pair) issues the same loads and stores, all idle.
     auto body = [&](auto pc, int k, bool live, bool first) {
         uint32_t res[UPW];
+        const int sb = 2 + 8 * (k - ka);  // stamp slots of this step (dbg 8)
 #pragma unroll
         for (int i = 0; i < UPW; ++i) res[i] = 0u;
         if (live) {
+            stamp(sb);
             if (!first) write_ring(pc, srow[2 * (k - 1) + 1]);
+            stamp(sb + 1);
             rc_barrier();
+            stamp(sb + 2);
             vertical(pc, srow[2 * k]);
-            if (rc_dbg(a) >= 3) vertical(pc, srow[2 * k]);  // probe: the vertical pass twice (same result)
+            stamp(sb + 3);
+            if (rc_dbg(a) == 3 || rc_dbg(a) == 4) vertical(pc, srow[2 * k]);  // probe: the vertical pass twice (same result)
         }
         issue_ring(pc, srow[2 * (k + 1) + 1]);
         issue_taps(pc, k + 2);
         if (live) {
+            stamp(sb + 4);
             rc_barrier();
+            stamp(sb + 5);
             horizontal(res);
+            stamp(sb + 6);
             if (rc_dbg(a) == 2 || rc_dbg(a) == 4) {  // probe: a third barrier and the horizontal pass twice (wrong pixels)
                 uint32_t r2[UPW];
                 rc_barrier();
@@ -453,6 +470,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
             }
         }
         store(k, live, res);
+        if (live) stamp(sb + 7);
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -523,9 +541,62 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         body(I0{}, ka + s, true, s == 0);
         body(I1{}, ka + s + 1, s + 1 < steps, false);
     }
+    stamp(1);
 }
 
 int rc_start(int o, double s, int pad, bool centre) { return static_cast<int>(reduce_x_host(o, s, centre)) - pad; }
+
+#ifdef MIPX_PROBES
+// dbg 8 (scripts/ only): launch with per-step phase stamps, wait, and print one JSON line per
+// 10th launch to stderr: block durations and start spread (the rounds of resident blocks),
+// and each phase's mean cycles per live step (s_memtime ticks); the third launch only
+int rcol_stamp_launch(const void *fn, RcArgs a, long long blocks, size_t lds, hipStream_t st, int ow, int oh, int n) {
+    static int calls = 0;
+    const size_t per = 2 + 8 * static_cast<size_t>(a.seg_steps), cnt = per * static_cast<size_t>(blocks);
+    unsigned long long *d = nullptr;
+    if (hipMalloc(&d, cnt * 8) != hipSuccess) return MIPX_EDEVICE;
+    (void)hipMemsetAsync(d, 0, cnt * 8, st);
+    a.stamps = d;
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(RcArgs)>(const_cast<void *>(fn)), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kRcNT), lds, st, a);
+    int e = launch_check("k_rcol");
+    std::vector<unsigned long long> h(cnt);
+    if (!e && hipStreamSynchronize(st) == hipSuccess && hipMemcpy(h.data(), d, cnt * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+        ++calls == 3) {
+        unsigned long long t0 = ~0ull, t1 = 0;
+        double dur = 0, ph[7] = {0, 0, 0, 0, 0, 0, 0};
+        long long nst = 0;
+        std::vector<double> starts;
+        for (long long b = 0; b < blocks; ++b) {
+            const unsigned long long *p = h.data() + b * per;
+            if (!p[0] || !p[1]) continue;
+            t0 = std::min(t0, p[0]);
+            t1 = std::max(t1, p[1]);
+            dur += static_cast<double>(p[1] - p[0]);
+            starts.push_back(static_cast<double>(p[0]));
+            for (int s = 0; s < a.seg_steps; ++s) {
+                const unsigned long long *q = p + 2 + 8 * s;
+                if (!q[0] || !q[7]) continue;
+                for (int i = 0; i < 7; ++i) ph[i] += static_cast<double>(q[i + 1] - q[i]);
+                ++nst;
+            }
+        }
+        std::sort(starts.begin(), starts.end());
+        const double nb = static_cast<double>(starts.size());
+        auto pct = [&](double f) { return starts.empty() ? 0.0 : starts[static_cast<size_t>(f * (nb - 1))] - t0; };
+        fprintf(stderr,
+                "{\"rcol_stamps\": 1, \"ow\": %d, \"oh\": %d, \"n\": %d, \"blocks\": %lld, \"seg_steps\": %d, "
+                "\"span\": %llu, \"block_mean\": %.0f, \"start_p25\": %.0f, \"start_p50\": %.0f, \"start_p75\": %.0f, "
+                "\"start_max\": %.0f, \"steps\": %lld, \"ring_write\": %.1f, \"barrier1\": %.1f, \"vertical\": %.1f, "
+                "\"issue\": %.1f, \"barrier2\": %.1f, \"horizontal\": %.1f, \"store\": %.1f}\n",
+                ow, oh, n, blocks, a.seg_steps, t1 - t0, dur / std::max(1.0, nb), pct(0.25), pct(0.5), pct(0.75), pct(1.0), nst,
+                ph[0] / std::max(1LL, nst), ph[1] / std::max(1LL, nst), ph[2] / std::max(1LL, nst), ph[3] / std::max(1LL, nst),
+                ph[4] / std::max(1LL, nst), ph[5] / std::max(1LL, nst), ph[6] / std::max(1LL, nst));
+    }
+    (void)hipFree(d);
+    return e;
+}
+#endif
 
 
 }  // namespace
@@ -731,6 +802,9 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     a.segs = (a.ksteps + a.seg_steps - 1) / a.seg_steps;
     const long long blocks = cols * a.segs;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
+#ifdef MIPX_PROBES
+    if (a.dbg == 8) return rcol_stamp_launch(fn, a, blocks, lds, st, ow, oh, n);
+#endif
     hipLaunchKernelGGL(reinterpret_cast<void (*)(RcArgs)>(const_cast<void *>(fn)), dim3(static_cast<unsigned>(blocks)),
                        dim3(kRcNT), lds, st, a);
     return launch_check("k_rcol");
