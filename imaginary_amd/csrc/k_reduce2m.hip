@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <vector>
@@ -89,7 +90,14 @@ struct R2mArgs {
     const rc_u4 *ops;       // [64 lanes][bh, bl, wh, wl]: the MFMA tap operands (r2m_operands)
     int alt;                // odd bands walk up (their edge rows meet the neighbours' in L2)
     int pp;                 // prime: both row batches in flight together
+    int dbg;                // PROBES builds only: 8 = per-step phase stamps (MIPX_R2M_DBG)
+    unsigned long long *stamps;  // PROBES, dbg 8: [block][2 + 10 band_steps]
 };
+#ifdef MIPX_PROBES
+__device__ __forceinline__ int r2m_dbg(const R2mArgs &a) { return a.dbg; }
+#else
+__device__ __forceinline__ int r2m_dbg(const R2mArgs &) { return 0; }
+#endif
 
 template <int B>
 __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
@@ -123,6 +131,13 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     auto new_rows = [&](int k) { return rev ? 32 * k - 37 : 32 * k + 37; };  // first row step k + dk adds
     const __amdgpu_buffer_rsrc_t src = image_rsrc(a.in + img * a.in_img, a.in_img);
     u8 *dst = a.out + img * a.out_img;
+    // PROBES, dbg 8: wave 0 lane 0 stamps the block's start / end and each step's phases
+    unsigned long long *stp = nullptr;
+    if (r2m_dbg(a) == 8 && tid == 0) stp = a.stamps + static_cast<size_t>(blockIdx.x) * (2 + 10 * a.band_steps);
+    auto stamp = [&](int sl) {
+        if (r2m_dbg(a) == 8 && stp) stp[sl] = __builtin_amdgcn_s_memtime();
+    };
+    stamp(0);
 
     // ---- staging: chunk c = tid + 256 j of a 32-row batch is (row rr, 16-byte column col) ----
     // packed (row rr << 16 | 16 col), one register per chunk
@@ -189,7 +204,10 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
     for (int s = 0; s < nst; ++s) {
         const int k = kf + dk * s;
         const int bk = 32 * k - 5;
+        const int sb = 2 + 10 * s;  // stamp slots (dbg 8)
+        stamp(sb);
         rc_barrier();  // ring rows of step k staged; the intermediate free
+        stamp(sb + 1);
         // ---- vertical: 16-byte column tiles dealt to the waves ----
         {
             const int r1 = bk + 8 * kg + (n >> 1);
@@ -233,11 +251,17 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                     if (c0 + 4 * i < CPR) tile(c0 + 4 * i, p[i][0], p[i][1]);
             }
         }
+        stamp(sb + 2);
         rc_barrier();  // the intermediate complete; the ring's rows of step k read
+        stamp(sb + 3);
         if (s + 1 < nst) {
             store_ring(pf, new_rows(k), 32);
+            stamp(sb + 4);
             if (s + 2 < nst) load(pf, new_rows(k + dk), 32);
+        } else {
+            stamp(sb + 4);
         }
+        stamp(sb + 5);
         if (edge) {  // EXTEND_COPY: strip pixels outside the image copy the edge pixel
             const int nfill = nl + nr;
             for (int i = tid; i < kMN * nfill * B; i += kMNT) {
@@ -250,6 +274,7 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
             }
             rc_barrier();
         }
+        stamp(sb + 6);
         // ---- horizontal on the matrix cores: D[out byte j][row u] = W[j][window byte] x
         // inter[window byte][u]; a group = GP output pixels of all 16 rows ----
         constexpr int GP = G::GP, GPW = G::GPW, HB = 4;
@@ -289,6 +314,7 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
         // windows cover (EXS on), written once the wave has read all its windows (a wave's
         // LDS operations complete in order); the next step's vertical pass overwrites them
         // only after its barrier
+        stamp(sb + 7);
         const uint32_t otile_w = inter_l + static_cast<uint32_t>(G::EXS + G::EXW * wave);
 #pragma unroll
         for (int g = 0; g < GPW; ++g)
@@ -316,7 +342,9 @@ __global__ void __launch_bounds__(kMNT) k_reduce2m(R2mArgs a) {
                 }
             }
         }
+        stamp(sb + 8);
     }
+    stamp(1);
 }
 
 
@@ -419,8 +447,51 @@ int reduce2m_window_launch(const u8 *in, u8 *out, int n, int w, int h, int b, in
     const long long blocks = static_cast<long long>(a.n_strips) * a.n_bands * n;
     if (!grid_ok(blocks)) return MIPX_EINVAL;
     const dim3 grid(static_cast<unsigned>(blocks)), blk(kMNT);
+#ifdef MIPX_PROBES
+    const char *edb = tune_env("MIPX_R2M_DBG");
+    a.dbg = edb && *edb ? std::atoi(edb) : 0;
+    static int calls = 0;
+    std::vector<unsigned long long> hs;
+    const size_t per = 2 + 10 * static_cast<size_t>(a.band_steps), cnt = per * static_cast<size_t>(blocks);
+    if (a.dbg == 8) {
+        if (hipMalloc(&a.stamps, cnt * 8) != hipSuccess) return MIPX_EDEVICE;
+        (void)hipMemsetAsync(a.stamps, 0, cnt * 8, st);
+    }
+#endif
     if (b == 3) hipLaunchKernelGGL(k_reduce2m<3>, grid, blk, 0, st, a);
     else hipLaunchKernelGGL(k_reduce2m<4>, grid, blk, 0, st, a);
+#ifdef MIPX_PROBES
+    if (a.dbg == 8) {  // one JSON line on the third launch: each phase's mean cycles per step
+        int e = launch_check("k_reduce2m");
+        hs.resize(cnt);
+        if (!e && hipStreamSynchronize(st) == hipSuccess &&
+            hipMemcpy(hs.data(), a.stamps, cnt * 8, hipMemcpyDeviceToHost) == hipSuccess && ++calls == 3) {
+            double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dur = 0;
+            long long nst = 0, nb = 0;
+            for (long long q = 0; q < blocks; ++q) {
+                const unsigned long long *p = hs.data() + q * per;
+                if (!p[0] || !p[1]) continue;
+                dur += static_cast<double>(p[1] - p[0]);
+                ++nb;
+                for (int s2 = 0; s2 < a.band_steps; ++s2) {
+                    const unsigned long long *r = p + 2 + 10 * s2;
+                    if (!r[0] || !r[8]) continue;
+                    for (int i = 0; i < 8; ++i) ph[i] += static_cast<double>(r[i + 1] - r[i]);
+                    ++nst;
+                }
+            }
+            const double d = static_cast<double>(std::max(1LL, nst));
+            fprintf(stderr,
+                    "{\"r2m_stamps\": 1, \"w\": %d, \"h\": %d, \"b\": %d, \"n\": %d, \"blocks\": %lld, \"band_steps\": %d, "
+                    "\"block_mean\": %.0f, \"steps\": %lld, \"barrier1\": %.1f, \"vertical\": %.1f, \"barrier2\": %.1f, "
+                    "\"ring_store\": %.1f, \"loads\": %.1f, \"edge\": %.1f, \"horizontal\": %.1f, \"store\": %.1f}\n",
+                    w, h, b, n, blocks, a.band_steps, dur / std::max(1.0, static_cast<double>(nb)), nst, ph[0] / d,
+                    ph[1] / d, ph[2] / d, ph[3] / d, ph[4] / d, ph[5] / d, ph[6] / d, ph[7] / d);
+        }
+        (void)hipFree(a.stamps);
+        return e;
+    }
+#endif
     return launch_check("k_reduce2m");
 }
 
