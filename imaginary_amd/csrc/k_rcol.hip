@@ -143,8 +143,14 @@ __device__ __forceinline__ void rc_edge_frag(const float *tabf, int taps, int pp
 // UNAL (r05): input rows off a dword (w B % 4 != 0, e.g. C5's 1333-pixel RGB rows): every
 // 16-byte chunk is loaded from its dword-aligned-down offset with the next dword and
 // realigned (v_alignbyte) when it is written to the ring
-template <int B, int NKS, int KMAX, int WPE, bool UNAL = false>
+// WSTC / K4C (r06): the store mode and the K-origin width fixed at compile time (0 / -1: read
+// from the arguments), so the step carries only the one store path and operand read it runs
+template <int B, int NKS, int KMAX, int WPE, bool UNAL = false, int WSTC = 0, int K4C = -1>
 __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE, 8))) k_rcol(RcArgs a) {
+    const int wst = WSTC ? WSTC : a.wst, k4 = K4C >= 0 ? K4C : a.k4;
+    // the specialised builds run only with the default A/B switches (the launcher checks)
+    constexpr bool SPEC = WSTC != 0;
+    const bool skipl = SPEC || a.skipl, trl = SPEC || a.trl, swz = SPEC || a.swz, allst = !SPEC && a.allst;
     constexpr int WV = kRcNT / 64, XW = 16 * WV;
     constexpr int UPW = B;  // horizontal units per wave: XW B / 16 / WV
     extern __shared__ __attribute__((aligned(16))) uint32_t rcs[];
@@ -201,11 +207,11 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     int kb[UPW];
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
-        const int u = a.wst ? UPW * wave + i : wave + WV * i;
+        const int u = wst ? UPW * wave + i : wave + WV * i;
         int sf, pf;
         rc_pos(a.ox0 + min(x0 + (16 * u) / B, x_last), a.hs, a.hpad, &sf, &pf, a.centre);
         // K origin: 8-byte aligned (ds_read_b64), 4-byte with k4
-        kb[i] = __builtin_amdgcn_readfirstlane((B * (sf - org) + (16 * u) % B) & (a.k4 ? ~3 : ~7));
+        kb[i] = __builtin_amdgcn_readfirstlane((B * (sf - org) + (16 * u) % B) & (k4 ? ~3 : ~7));
         const int o = 16 * u + n, xl = o / B, c = o - B * xl;
         int sp, pp;
         rc_pos(a.ox0 + min(x0 + xl, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
@@ -238,7 +244,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     uint32_t sto[UPW];
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
-        const int e = 16 * (a.wst ? UPW * wave + i : wave + WV * i) + 4 * kg;
+        const int e = 16 * (wst ? UPW * wave + i : wave + WV * i) + 4 * kg;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             int sp, pp;
@@ -265,7 +271,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // skipl: batch j of this wave loads anything (uniform; the same every step)
     bool wl[KMAX];
 #pragma unroll
-    for (int j = 0; j < KMAX; ++j) wl[j] = !a.skipl || __builtin_amdgcn_ballot_w64(rr[j] < a.rcap) != 0;
+    for (int j = 0; j < KMAX; ++j) wl[j] = !skipl || __builtin_amdgcn_ballot_w64(rr[j] < a.rcap) != 0;
 
     // ---- the step pipeline: register set P = (step - ka) & 1 holds step k + 2's ring
     // chunks and vertical operands from the middle of step k to the top of step k + 2.
@@ -323,10 +329,10 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     int wrow = min(lane / UPW, kRcRows - 1), wch = lane - UPW * (lane / UPW);  // read-back: row, 16-byte chunk
     // r06: RGBA (4 chunks a row, rows 80 bytes apart) reads back by tile_rd_lane: each
     // ds_read_b128 lane group on disjoint banks (MIPX_RCOL_TRL=0: lane / 4, A/B)
-    if (UPW == 4 && a.trl) tile_rd_lane(lane, &wrow, &wch);
+    if (UPW == 4 && trl) tile_rd_lane(lane, &wrow, &wch);
     const int we = 16 * (UPW * wave + wch);                          // its first byte in the strip row
     auto store = [&](int k, bool live, const uint32_t *res) {
-        if (a.wst) {
+        if (wst) {
 #pragma unroll
             for (int i = 0; i < UPW; ++i) lds_wr32(wst_l + static_cast<uint32_t>(n * WSR + 16 * i + 4 * kg), res[i]);
             rc_u4 q = lds_rd128(wst_l + static_cast<uint32_t>(wrow * WSR + 16 * wch));
@@ -336,7 +342,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
             const int base = o * a.ow * B + B * x0 + we;
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rc_v4i, q), dst,
                                                    ok && we + 16 <= vbytes ? base : 0x7ffffff0, 0, 0);
-            if (a.wst == 2 && (vbytes < 16 * UPW * WV || a.allst)) {
+            if (wst == 2 && (vbytes < 16 * UPW * WV || allst)) {
                 // rows whose byte count is not a multiple of 16: the piece at the image edge in
                 // dwords, in the last strip only (uniform: r05, the dword stores every other
                 // strip issued with out-of-range offsets were 4 of every 5 store instructions)
@@ -344,7 +350,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
                 for (int j = 0; j < 4; ++j)
                     __builtin_amdgcn_raw_buffer_store_b32(
                         q[j], dst, ok && we + 16 > vbytes && we + 4 * j < vbytes ? base + 4 * j : 0x7ffffff0, 0, 0);
-            } else if (a.wst == 3 && B * x0 + 16 * UPW * WV >= a.ow * B) {
+            } else if (wst == 3 && B * x0 + 16 * UPW * WV >= a.ow * B) {
                 // rows not on a dword (the b128 pieces above went out unaligned): the last strip's
                 // edge piece byte by byte
 #pragma unroll
@@ -397,7 +403,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // 16 first (hsw = 8) and the operands' halves are swapped to match: with kg = 0 / 1
     // lanes in one 32-lane half on banks 0-1 / 2-3 (mod 4) each read is conflict-free
     // (both halves of one K block at once were 2-way); MIPX_RCOL_SWZ=0 keeps the old order
-    const int hsw = a.swz && (kg & 1) ? 8 : 0, hsd = 8 - 2 * hsw;
+    const int hsw = swz && (kg & 1) ? 8 : 0, hsd = 8 - 2 * hsw;
     auto horizontal = [&](uint32_t *res) {
         rc_u2x2 q[UPW][NKS];
 #pragma unroll
@@ -408,7 +414,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
                 // two ds_read_b64 (2 LDS cycles each) rather than one ds_read2_b64 (16): -0.3 to -2 %
                 // (profiles/r04/small/rcol_rd64_ab.jsonl); lanes of odd K blocks read their
                 // second half first (hsw), so each read's 32-lane half covers all 64 banks
-                if (a.k4) {
+                if (k4) {
                     q[i][ks].lo = lds_rd2x32(ir + 64 * ks);
                     q[i][ks].hi = lds_rd2x32(ir + 64 * ks + hsd);
                 } else {
@@ -756,6 +762,27 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     }
 #undef MIPX_RC_KM
 #undef MIPX_RC_K
+    // r06: the 3-chunk, one-K-step builds with the store mode and K-origin width compiled in
+    // (profiles/r06/rcol_spec_ab.jsonl: 480x270 +4.7 %, 500x375 +3.3 %, 1024^2 RGBA / 1.333
+    // +1.1 %, 1080p RGB / 1.6 +0.8 %, the rest +-0.1 %; RGBA with 4-byte K origins -1.4 %, so
+    // that one, and RGBA rows off a dword, keep the argument-driven build); MIPX_RCOL_SPEC=0: those builds everywhere (A/B)
+    const char *esp = tune_env("MIPX_RCOL_SPEC");
+    const bool spec = !(esp && *esp == '0') && nks == 1 && kmax == 3 && a.wst >= 1 && a.wst <= 3 &&
+                      !(b == 4 && (a.k4 || a.wst == 3)) && a.skipl && a.trl && a.swz && !a.allst;
+    if (spec) {
+#define MIPX_RC_S(B_, U_, W_, K_) fn = reinterpret_cast<const void *>(&k_rcol<B_, 1, 3, 1, U_, W_, K_>);
+#define MIPX_RC_SK(B_, U_, W_) \
+    if (a.k4) { MIPX_RC_S(B_, U_, W_, 1) } else { MIPX_RC_S(B_, U_, W_, 0) }
+#define MIPX_RC_SW(B_, U_) \
+    if (a.wst == 1) { MIPX_RC_SK(B_, U_, 1) } else if (a.wst == 2) { MIPX_RC_SK(B_, U_, 2) } else { MIPX_RC_SK(B_, U_, 3) }
+        if (unal) { MIPX_RC_SW(3, true) }
+        else if (b == 3) { MIPX_RC_SW(3, false) }
+        else if (a.wst == 1) { MIPX_RC_S(4, false, 1, 0) }
+        else { MIPX_RC_S(4, false, 2, 0) }
+#undef MIPX_RC_SW
+#undef MIPX_RC_SK
+#undef MIPX_RC_S
+    }
 
     // segments: a block's set-up (operand loads, the first group's rows) costs about two
     // steps; pick the split that minimises (rounds of resident blocks) x (steps + 2)
@@ -791,6 +818,15 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     if (nks == 1 && kmax == 3 && !unal && (b == 3 || force4)) {
         const void *f4 = b == 3 ? reinterpret_cast<const void *>(&k_rcol<3, 1, 3, 4>)
                                 : reinterpret_cast<const void *>(&k_rcol<4, 1, 3, 4>);
+        // r06: the specialised RGB build at 4 waves (5-6 spilled) where the specialised 3-wave
+        // one was chosen: 364x273 x 128 -> 256^2 +10 % against the generic 4-wave build
+        // (profiles/r06/rcol_sw4_ab.jsonl; forced on every shape it is 11-20 % slower)
+        if (b == 3 && spec) {
+#define MIPX_RC_S4(W_) f4 = a.k4 ? reinterpret_cast<const void *>(&k_rcol<3, 1, 3, 4, false, W_, 1>) \
+                                 : reinterpret_cast<const void *>(&k_rcol<3, 1, 3, 4, false, W_, 0>);
+            if (a.wst == 1) { MIPX_RC_S4(1) } else if (a.wst == 2) { MIPX_RC_S4(2) } else { MIPX_RC_S4(3) }
+#undef MIPX_RC_S4
+        }
         int segs4 = 1;
         const auto p4 = plan(f4, &segs4);
         if (force4 || (p4.second == 1 && p4.first < best - 1e-9)) {
