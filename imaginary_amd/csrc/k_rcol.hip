@@ -84,7 +84,9 @@ struct RcArgs {
     int dbg;                  // MIPX_RCOL_DBG (PROBES builds only): 1 = set-up and prime, no steps; 2 = a third
                               // barrier + the horizontal pass twice, 3 = the vertical pass twice, 4 = both;
                               // 8 = per-step phase stamps (s_memtime) into stamps
-    unsigned long long *stamps;  // PROBES, dbg 8: [block][2 + 8 seg_steps]
+    unsigned long long *stamps;  // PROBES, dbg 8: [block][8 + 8 seg_steps]
+    const u8 *hops;           // r06, specialised builds: device_rcol_hops records [strip][unit][lane]
+    const int *hkb;           // and the K origins [strip][unit]
 };
 #ifdef MIPX_PROBES
 __device__ __forceinline__ int rc_dbg(const RcArgs &a) { return a.dbg; }
@@ -191,7 +193,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     const __amdgpu_buffer_rsrc_t dst = image_rsrc(a.out + img * a.out_img, a.out_img);
     // PROBES, dbg 8: wave 0 lane 0 stamps the block's start / end and each step's phases
     unsigned long long *stp = nullptr;
-    if (rc_dbg(a) == 8 && tid == 0) stp = a.stamps + static_cast<size_t>(blockIdx.x) * (2 + 8 * a.seg_steps);
+    if (rc_dbg(a) == 8 && tid == 0) stp = a.stamps + static_cast<size_t>(blockIdx.x) * (8 + 8 * a.seg_steps);
     auto stamp = [&](int slot) {
         if (rc_dbg(a) == 8 && stp) stp[slot] = __builtin_amdgcn_s_memtime();
     };
@@ -205,8 +207,25 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     int qsh[UPW][NKS];
     bool both[UPW];
     int kb[UPW];
+    rc_v4i hb[UPW];
+    // r06: the specialised builds load the host-built operands and seeds (device_rcol_hops):
+    // three 16-byte loads per unit instead of the positions, table rows and edge folds
+    constexpr bool HOPS = SPEC && NKS == 1;
+    if constexpr (HOPS) {
+        typedef const __attribute__((address_space(4))) int rc_ckb;
 #pragma unroll
-    for (int i = 0; i < UPW; ++i) {
+        for (int i = 0; i < UPW; ++i) {
+            const int u = UPW * wave + i;
+            const u8 *rec = a.hops + (static_cast<size_t>(strip * 4 * UPW + u) * 64 + lane) * kRcolHopRec;
+            th[i][0] = *reinterpret_cast<const rc_v4i *>(rec);
+            tl[i][0] = *reinterpret_cast<const rc_v4i *>(rec + 16);
+            hb[i] = *reinterpret_cast<const rc_v4i *>(rec + 32);
+            kb[i] = ((rc_ckb *)a.hkb)[strip * 4 * UPW + u];
+            both[i] = true;  // (operands final: no realignment below)
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < UPW && !HOPS; ++i) {
         const int u = wst ? UPW * wave + i : wave + WV * i;
         int sf, pf;
         rc_pos(a.ox0 + min(x0 + (16 * u) / B, x_last), a.hs, a.hpad, &sf, &pf, a.centre);
@@ -238,22 +257,25 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
             }
         }
     }
+    stamp(2);
     // per output byte seeds of the horizontal pass (lane: bytes 16 u + 4 kg + j of row n)
     // and store offsets (past the strip's last byte: beyond any image, so dropped)
-    rc_v4i hb[UPW];
     uint32_t sto[UPW];
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
         const int e = 16 * (wst ? UPW * wave + i : wave + WV * i) + 4 * kg;
+        if constexpr (!HOPS) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            int sp, pp;
-            rc_pos(a.ox0 + min(x0 + (e + j) / B, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
-            hb[i][j] = 128 * a.sumh[pp] + 2048;
+            for (int j = 0; j < 4; ++j) {
+                int sp, pp;
+                rc_pos(a.ox0 + min(x0 + (e + j) / B, x_last), a.hs, a.hpad, &sp, &pp, a.centre);
+                hb[i][j] = 128 * a.sumh[pp] + 2048;
+            }
         }
         sto[i] = e < vbytes ? static_cast<uint32_t>(B * x0 + e) : 0x20000000u;
     }
 
+    stamp(3);
     // ring chunks: chunk c = tid + 256 j of a step's rows is (row rr, column col); the
     // same map every step.  A lane's chunks past the step's rows load rows below it:
     // harmless (host-checked: their slots hold rows no longer read).
@@ -446,7 +468,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // (live = false, the odd tail of a pair) issues the same loads and stores, all idle.
     auto body = [&](auto pc, int k, bool live, bool first) {
         uint32_t res[UPW];
-        const int sb = 2 + 8 * (k - ka);  // stamp slots of this step (dbg 8)
+        const int sb = 8 + 8 * (k - ka);  // stamp slots of this step (dbg 8)
 #pragma unroll
         for (int i = 0; i < UPW; ++i) res[i] = 0u;
         if (live) {
@@ -485,6 +507,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     // pipeline's first loads (r05: issuing those before the prime's ring writes measured
     // within +-1 %, and the extra live registers spilled in the 4-wave build,
     // profiles/r05/prime_ab.jsonl) ----
+    stamp(4);
     const int bka = srow[2 * ka], eka = srow[2 * ka + 1];
     for (int r = bka; r < eka; r += lkf) {
         rc_u4 tv[KMAX];
@@ -501,11 +524,13 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
                 lds_wr128(static_cast<uint32_t>(((r + rr[j]) & a.rmask) * a.rs) + lcol[j],
                           realign(tv[j], te[UNAL ? j : 0], chunk_off(r, j)) ^ 0x80808080u);
     }
+    stamp(5);
     issue_taps(I0{}, ka);
     store(ka, false, zero);  // idle: keeps the load / store sequence the loop's
     issue_ring(I1{}, eka);
     issue_taps(I1{}, ka + 1);
     store(ka, false, zero);
+    stamp(6);
 #pragma unroll
     for (int i = 0; i < UPW; ++i) {
         if (both[i]) continue;
@@ -523,7 +548,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
                                static_cast<int>(__builtin_amdgcn_alignbyte(el[i][ks], e.w, sh))};
         }
     }
-    if (hsw) {  // the K halves of odd blocks, in the order their data is read
+    if (hsw && !HOPS) {  // the K halves of odd blocks, in the order their data is read (the host did it for HOPS)
 #pragma unroll
         for (int i = 0; i < UPW; ++i)
 #pragma unroll
@@ -543,6 +568,7 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
         }
         return;
     }
+    stamp(7);
     for (int s = 0; s < steps; s += 2) {
         body(I0{}, ka + s, true, s == 0);
         body(I1{}, ka + s + 1, s + 1 < steps, false);
@@ -558,7 +584,7 @@ int rc_start(int o, double s, int pad, bool centre) { return static_cast<int>(re
 // and each phase's mean cycles per live step (s_memtime ticks); the third launch only
 int rcol_stamp_launch(const void *fn, RcArgs a, long long blocks, size_t lds, hipStream_t st, int ow, int oh, int n) {
     static int calls = 0;
-    const size_t per = 2 + 8 * static_cast<size_t>(a.seg_steps), cnt = per * static_cast<size_t>(blocks);
+    const size_t per = 8 + 8 * static_cast<size_t>(a.seg_steps), cnt = per * static_cast<size_t>(blocks);
     unsigned long long *d = nullptr;
     if (hipMalloc(&d, cnt * 8) != hipSuccess) return MIPX_EDEVICE;
     (void)hipMemsetAsync(d, 0, cnt * 8, st);
@@ -570,7 +596,7 @@ int rcol_stamp_launch(const void *fn, RcArgs a, long long blocks, size_t lds, hi
     if (!e && hipStreamSynchronize(st) == hipSuccess && hipMemcpy(h.data(), d, cnt * 8, hipMemcpyDeviceToHost) == hipSuccess &&
         ++calls == 3) {
         unsigned long long t0 = ~0ull, t1 = 0;
-        double dur = 0, ph[7] = {0, 0, 0, 0, 0, 0, 0};
+        double dur = 0, ph[7] = {0, 0, 0, 0, 0, 0, 0}, su[6] = {0, 0, 0, 0, 0, 0};
         long long nst = 0;
         std::vector<double> starts;
         for (long long b = 0; b < blocks; ++b) {
@@ -579,9 +605,11 @@ int rcol_stamp_launch(const void *fn, RcArgs a, long long blocks, size_t lds, hi
             t0 = std::min(t0, p[0]);
             t1 = std::max(t1, p[1]);
             dur += static_cast<double>(p[1] - p[0]);
+            const int sl[7] = {0, 2, 3, 4, 5, 6, 7};  // set-up phase boundaries
+            for (int i = 0; i < 6; ++i) su[i] += static_cast<double>(p[sl[i + 1]] - p[sl[i]]);
             starts.push_back(static_cast<double>(p[0]));
             for (int s = 0; s < a.seg_steps; ++s) {
-                const unsigned long long *q = p + 2 + 8 * s;
+                const unsigned long long *q = p + 8 + 8 * s;
                 if (!q[0] || !q[7]) continue;
                 for (int i = 0; i < 7; ++i) ph[i] += static_cast<double>(q[i + 1] - q[i]);
                 ++nst;
@@ -594,10 +622,14 @@ int rcol_stamp_launch(const void *fn, RcArgs a, long long blocks, size_t lds, hi
                 "{\"rcol_stamps\": 1, \"ow\": %d, \"oh\": %d, \"n\": %d, \"blocks\": %lld, \"seg_steps\": %d, "
                 "\"span\": %llu, \"block_mean\": %.0f, \"start_p25\": %.0f, \"start_p50\": %.0f, \"start_p75\": %.0f, "
                 "\"start_max\": %.0f, \"steps\": %lld, \"ring_write\": %.1f, \"barrier1\": %.1f, \"vertical\": %.1f, "
-                "\"issue\": %.1f, \"barrier2\": %.1f, \"horizontal\": %.1f, \"store\": %.1f}\n",
+                "\"issue\": %.1f, \"barrier2\": %.1f, \"horizontal\": %.1f, \"store\": %.1f, \"setup_operands\": %.0f, "
+                "\"setup_seeds\": %.0f, \"setup_chunks\": %.0f, \"setup_prime\": %.0f, \"setup_issue\": %.0f, "
+                "\"setup_realign\": %.0f}\n",
                 ow, oh, n, blocks, a.seg_steps, t1 - t0, dur / std::max(1.0, nb), pct(0.25), pct(0.5), pct(0.75), pct(1.0), nst,
                 ph[0] / std::max(1LL, nst), ph[1] / std::max(1LL, nst), ph[2] / std::max(1LL, nst), ph[3] / std::max(1LL, nst),
-                ph[4] / std::max(1LL, nst), ph[5] / std::max(1LL, nst), ph[6] / std::max(1LL, nst));
+                ph[4] / std::max(1LL, nst), ph[5] / std::max(1LL, nst), ph[6] / std::max(1LL, nst), su[0] / std::max(1.0, nb),
+                su[1] / std::max(1.0, nb), su[2] / std::max(1.0, nb), su[3] / std::max(1.0, nb), su[4] / std::max(1.0, nb),
+                su[5] / std::max(1.0, nb));
     }
     (void)hipFree(d);
     return e;
@@ -770,6 +802,11 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     const bool spec = !(esp && *esp == '0') && nks == 1 && kmax == 3 && a.wst >= 1 && a.wst <= 3 &&
                       !(b == 4 && (a.k4 || a.wst == 3)) && a.skipl && a.trl && a.swz && !a.allst;
     if (spec) {
+        int hstrips = 0;
+        const u8 *hops = device_rcol_hops(hs, b, centre, ox0, ow, w, a.k4, &hstrips);
+        if (!hops) return MIPX_EDEVICE;
+        a.hops = hops;
+        a.hkb = reinterpret_cast<const int *>(hops + static_cast<size_t>(hstrips) * 4 * b * 64 * kRcolHopRec);
 #define MIPX_RC_S(B_, U_, W_, K_) fn = reinterpret_cast<const void *>(&k_rcol<B_, 1, 3, 1, U_, W_, K_>);
 #define MIPX_RC_SK(B_, U_, W_) \
     if (a.k4) { MIPX_RC_S(B_, U_, W_, 1) } else { MIPX_RC_S(B_, U_, W_, 0) }
