@@ -15,6 +15,6 @@ for l in sys.stdin:
     d = json.loads(l)
     ph = ['ring_write','barrier1','vertical','issue','barrier2','horizontal','store']
     tot = sum(d[p] for p in ph)
-    print(d['ow'], d['oh'], d['n'], 'blocks', d['blocks'], 'span', d['span'], 'block', round(d['block_mean']), 'starts', d['start_p50'], d['start_max'],
+    print(d['ow'], d['oh'], d['n'], 'blocks', d['blocks'], 'block', round(d['block_mean']), 'setup', {k[6:]: round(v) for k, v in d.items() if k.startswith('setup_')},
           'step', round(tot), ' '.join(f'{p}={d[p]:.0f}({d[p]/tot:.0%})' for p in ph))
 "
