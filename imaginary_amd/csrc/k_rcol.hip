@@ -799,12 +799,12 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // +1.1 %, 1080p RGB / 1.6 +0.8 %, the rest +-0.1 %; RGBA with 4-byte K origins -1.4 %, so
     // that one, and RGBA rows off a dword, keep the argument-driven build); MIPX_RCOL_SPEC=0: those builds everywhere (A/B)
     const char *esp = tune_env("MIPX_RCOL_SPEC");
-    const bool spec = !(esp && *esp == '0') && nks == 1 && kmax == 3 && a.wst >= 1 && a.wst <= 3 &&
-                      !(b == 4 && (a.k4 || a.wst == 3)) && a.skipl && a.trl && a.swz && !a.allst;
+    bool spec = !(esp && *esp == '0') && nks == 1 && kmax == 3 && a.wst >= 1 && a.wst <= 3 &&
+                !(b == 4 && (a.k4 || a.wst == 3)) && a.skipl && a.trl && a.swz && !a.allst;
+    int hstrips = 0;
+    const u8 *hops = spec ? device_rcol_hops(hs, b, centre, ox0, ow, w, a.k4, &hstrips) : nullptr;
+    spec = spec && hops;  // past the table cap: the builds that compute their operands
     if (spec) {
-        int hstrips = 0;
-        const u8 *hops = device_rcol_hops(hs, b, centre, ox0, ow, w, a.k4, &hstrips);
-        if (!hops) return MIPX_EDEVICE;
         a.hops = hops;
         a.hkb = reinterpret_cast<const int *>(hops + static_cast<size_t>(hstrips) * 4 * b * 64 * kRcolHopRec);
 #define MIPX_RC_S(B_, U_, W_, K_) fn = reinterpret_cast<const void *>(&k_rcol<B_, 1, 3, 1, U_, W_, K_>);
