@@ -210,16 +210,19 @@ __global__ void __launch_bounds__(kRcNT) __attribute__((amdgpu_waves_per_eu(WPE,
     rc_v4i hb[UPW];
     // r06: the specialised builds load the host-built operands and seeds (device_rcol_hops):
     // three 16-byte loads per unit instead of the positions, table rows and edge folds
-    constexpr bool HOPS = SPEC && NKS == 1;
+    constexpr bool HOPS = SPEC;
     if constexpr (HOPS) {
         typedef const __attribute__((address_space(4))) int rc_ckb;
 #pragma unroll
         for (int i = 0; i < UPW; ++i) {
             const int u = UPW * wave + i;
-            const u8 *rec = a.hops + (static_cast<size_t>(strip * 4 * UPW + u) * 64 + lane) * kRcolHopRec;
-            th[i][0] = *reinterpret_cast<const rc_v4i *>(rec);
-            tl[i][0] = *reinterpret_cast<const rc_v4i *>(rec + 16);
-            hb[i] = *reinterpret_cast<const rc_v4i *>(rec + 32);
+            const u8 *rec = a.hops + (static_cast<size_t>(strip * 4 * UPW + u) * 64 + lane) * kRcolHopRec(NKS);
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                th[i][ks] = *reinterpret_cast<const rc_v4i *>(rec + 32 * ks);
+                tl[i][ks] = *reinterpret_cast<const rc_v4i *>(rec + 32 * ks + 16);
+            }
+            hb[i] = *reinterpret_cast<const rc_v4i *>(rec + 32 * NKS);
             kb[i] = ((rc_ckb *)a.hkb)[strip * 4 * UPW + u];
             both[i] = true;  // (operands final: no realignment below)
         }
@@ -799,24 +802,36 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // +1.1 %, 1080p RGB / 1.6 +0.8 %, the rest +-0.1 %; RGBA with 4-byte K origins -1.4 %, so
     // that one, and RGBA rows off a dword, keep the argument-driven build); MIPX_RCOL_SPEC=0: those builds everywhere (A/B)
     const char *esp = tune_env("MIPX_RCOL_SPEC");
-    bool spec = !(esp && *esp == '0') && nks == 1 && kmax == 3 && a.wst >= 1 && a.wst <= 3 &&
+    // (and, with the host-built operands, RGB with two K steps: 1080p RGB / 2.4)
+    const bool spec2 = nks == 2 && b == 3 && !unal;
+    bool spec = !(esp && *esp == '0') && ((nks == 1 && kmax == 3) || spec2) && a.wst >= 1 && a.wst <= 3 &&
                 !(b == 4 && (a.k4 || a.wst == 3)) && a.skipl && a.trl && a.swz && !a.allst;
     int hstrips = 0;
-    const u8 *hops = spec ? device_rcol_hops(hs, b, centre, ox0, ow, w, a.k4, &hstrips) : nullptr;
+    const u8 *hops = spec ? device_rcol_hops(hs, b, centre, ox0, ow, w, a.k4, nks, &hstrips) : nullptr;
     spec = spec && hops;  // past the table cap: the builds that compute their operands
     if (spec) {
         a.hops = hops;
-        a.hkb = reinterpret_cast<const int *>(hops + static_cast<size_t>(hstrips) * 4 * b * 64 * kRcolHopRec);
+        a.hkb = reinterpret_cast<const int *>(hops + static_cast<size_t>(hstrips) * 4 * b * 64 * kRcolHopRec(nks));
 #define MIPX_RC_S(B_, U_, W_, K_) fn = reinterpret_cast<const void *>(&k_rcol<B_, 1, 3, 1, U_, W_, K_>);
+#define MIPX_RC_S2(W_, K_)                                                                 \
+    fn = kmax == 3 ? reinterpret_cast<const void *>(&k_rcol<3, 2, 3, 1, false, W_, K_>) \
+                   : reinterpret_cast<const void *>(&k_rcol<3, 2, 6, 1, false, W_, K_>);
 #define MIPX_RC_SK(B_, U_, W_) \
     if (a.k4) { MIPX_RC_S(B_, U_, W_, 1) } else { MIPX_RC_S(B_, U_, W_, 0) }
+#define MIPX_RC_SK2(W_) \
+    if (a.k4) { MIPX_RC_S2(W_, 1) } else { MIPX_RC_S2(W_, 0) }
 #define MIPX_RC_SW(B_, U_) \
     if (a.wst == 1) { MIPX_RC_SK(B_, U_, 1) } else if (a.wst == 2) { MIPX_RC_SK(B_, U_, 2) } else { MIPX_RC_SK(B_, U_, 3) }
-        if (unal) { MIPX_RC_SW(3, true) }
+        if (spec2) {
+            if (a.wst == 1) { MIPX_RC_SK2(1) } else if (a.wst == 2) { MIPX_RC_SK2(2) } else { MIPX_RC_SK2(3) }
+        }
+        else if (unal) { MIPX_RC_SW(3, true) }
         else if (b == 3) { MIPX_RC_SW(3, false) }
         else if (a.wst == 1) { MIPX_RC_S(4, false, 1, 0) }
         else { MIPX_RC_S(4, false, 2, 0) }
 #undef MIPX_RC_SW
+#undef MIPX_RC_SK2
+#undef MIPX_RC_S2
 #undef MIPX_RC_SK
 #undef MIPX_RC_S
     }

@@ -112,12 +112,12 @@ const signed char *device_reduce_i8s_fold(double shrink, int bands, int *n_taps)
 constexpr int kRcolPlanRow = 144;
 const uint8_t *device_rcol_vplan(double shrink, bool centre, int rows, int *cap_rows);
 // k_rcol's horizontal operands of one window geometry, built on the host (r06): per 64-pixel
-// strip, per 16-byte output unit u < 4 bands, per lane: the hi / lo tap fragments (COPY edge
-// folded, odd K blocks' halves swapped) and the four per-byte seeds, 48 bytes; then per
-// (strip, unit) the K origin (int).  The specialised k_rcol builds load these instead of
-// computing the positions in the block's set-up.
-constexpr int kRcolHopRec = 48;
-const uint8_t *device_rcol_hops(double hs, int bands, bool centre, int ox0, int ow, int w, int k4, int *strips);
+// strip, per 16-byte output unit u < 4 bands, per lane: per K step the hi / lo tap fragments
+// (COPY edge folded, odd K blocks' halves swapped), then the four per-byte seeds,
+// kRcolHopRec(nks) bytes; then per (strip, unit) the K origin (int).  The specialised k_rcol
+// builds load these instead of computing the positions in the block's set-up.
+constexpr int kRcolHopRec(int nks) { return 32 * nks + 16; }
+const uint8_t *device_rcol_hops(double hs, int bands, bool centre, int ox0, int ow, int w, int k4, int nks, int *strips);
 // k_bmf's i8 MFMA operands for a blur mask (cached per device): [nks][64][16]
 // horizontal taps at byte stride `bands` shifted by delta, then [64][16] vertical taps
 const signed char *device_blur_ops(const std::vector<int> &mask, int bands, int delta, int nks, int vperm);
