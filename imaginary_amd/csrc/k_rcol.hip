@@ -802,8 +802,9 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     // +1.1 %, 1080p RGB / 1.6 +0.8 %, the rest +-0.1 %; RGBA with 4-byte K origins -1.4 %, so
     // that one, and RGBA rows off a dword, keep the argument-driven build); MIPX_RCOL_SPEC=0: those builds everywhere (A/B)
     const char *esp = tune_env("MIPX_RCOL_SPEC");
-    // (and, with the host-built operands, RGB with two K steps: 1080p RGB / 2.4)
-    const bool spec2 = nks == 2 && b == 3 && !unal;
+    // (and, with the host-built operands, two K steps: 1080p RGB / 2.4 +13 %, 4K / 2.4 +12 %,
+    // profiles/r06/rcol_hops2_ab; RGB rows off a dword and RGBA with 8-byte K origins only)
+    const bool spec2 = nks == 2 && (b == 3 ? !unal || !a.k4 : !a.k4 && a.wst != 3);
     bool spec = !(esp && *esp == '0') && ((nks == 1 && kmax == 3) || spec2) && a.wst >= 1 && a.wst <= 3 &&
                 !(b == 4 && (a.k4 || a.wst == 3)) && a.skipl && a.trl && a.swz && !a.allst;
     int hstrips = 0;
@@ -822,7 +823,19 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     if (a.k4) { MIPX_RC_S2(W_, 1) } else { MIPX_RC_S2(W_, 0) }
 #define MIPX_RC_SW(B_, U_) \
     if (a.wst == 1) { MIPX_RC_SK(B_, U_, 1) } else if (a.wst == 2) { MIPX_RC_SK(B_, U_, 2) } else { MIPX_RC_SK(B_, U_, 3) }
-        if (spec2) {
+        if (spec2 && unal) {
+#define MIPX_RC_SU2(W_)                                                                   \
+    fn = kmax == 3 ? reinterpret_cast<const void *>(&k_rcol<3, 2, 3, 1, true, W_, 0>) \
+                   : reinterpret_cast<const void *>(&k_rcol<3, 2, 6, 1, true, W_, 0>);
+            if (a.wst == 1) { MIPX_RC_SU2(1) } else if (a.wst == 2) { MIPX_RC_SU2(2) } else { MIPX_RC_SU2(3) }
+#undef MIPX_RC_SU2
+        } else if (spec2 && b == 4) {
+#define MIPX_RC_SA2(W_)                                                                    \
+    fn = kmax == 3 ? reinterpret_cast<const void *>(&k_rcol<4, 2, 3, 1, false, W_, 0>) \
+                   : reinterpret_cast<const void *>(&k_rcol<4, 2, 6, 1, false, W_, 0>);
+            if (a.wst == 1) { MIPX_RC_SA2(1) } else { MIPX_RC_SA2(2) }
+#undef MIPX_RC_SA2
+        } else if (spec2) {
             if (a.wst == 1) { MIPX_RC_SK2(1) } else if (a.wst == 2) { MIPX_RC_SK2(2) } else { MIPX_RC_SK2(3) }
         }
         else if (unal) { MIPX_RC_SW(3, true) }

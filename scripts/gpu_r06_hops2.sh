@@ -10,9 +10,17 @@ run 600 python3 -u -m pytest tests/test_rcol_gpu.py tests/test_chain_gpu.py test
   -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1
 tail -1 "$O/pytest.log"
 ab() { run 150 python3 scripts/op_bench.py "$@" --iters 20 >> "$O/ab.jsonl" 2>> "$O/ab.err"; }
-for a in "--w 1920 --h 1080 --b 3 --n 64 --s 2.4" "--w 1920 --h 1080 --b 3 --n 64 --s 2.0" "--w 1920 --h 1080 --b 3 --n 64 --s 2.2" \
+# SHAPES=2: the RGBA and RGB-rows-off-a-dword builds (second pass)
+if [ "${SHAPES:-1}" = 2 ]; then
+  set -- "--w 1024 --h 1024 --b 4 --n 128 --s 2.4" "--w 1024 --h 1024 --b 4 --n 128 --s 2.2" "--w 800 --h 600 --b 4 --n 128 --s 2.25" \
+    "--w 1333 --h 1000 --b 3 --n 48 --s 2.4" "--w 1366 --h 768 --b 3 --n 64 --s 2.2" "--w 999 --h 750 --b 3 --n 128 --s 2.25" \
+    "--w 1920 --h 1080 --b 3 --n 64 --s 2.4"
+else
+  set -- "--w 1920 --h 1080 --b 3 --n 64 --s 2.4" "--w 1920 --h 1080 --b 3 --n 64 --s 2.0" "--w 1920 --h 1080 --b 3 --n 64 --s 2.2" \
     "--w 3840 --h 2160 --b 3 --n 16 --s 2.4" "--w 1000 --h 750 --b 3 --n 128 --s 2.25" "--w 640 --h 480 --b 3 --n 256 --s 2.5" \
-    "--w 480 --h 270 --b 3 --n 256 --s 1.6 --s2 1.5976331360946747" "--w 1333 --h 1000 --b 3 --n 48 --s 1.6666666666666667"; do
+    "--w 480 --h 270 --b 3 --n 256 --s 1.6 --s2 1.5976331360946747" "--w 1333 --h 1000 --b 3 --n 48 --s 1.6666666666666667"
+fi
+for a in "$@"; do
   ab reduce $a --ab MIPX_RCOL_SPEC=0,1
 done
 python3 - "$O" <<'PY'
