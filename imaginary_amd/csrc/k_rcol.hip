@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -642,6 +643,26 @@ int rcol_stamp_launch(const void *fn, RcArgs a, long long blocks, size_t lds, hi
 
 }  // namespace
 
+// The specialised k_rcol build of one geometry (r06): store mode wst (1..3; RGBA 1..2) and
+// K-origin width k4 as template arguments, for every K-step count and chunk count
+template <int B, int NKS, int KM, bool U>
+const void *rc_spec_wk(int wst, int k4) {
+    auto pk = [&](auto wc) -> const void * {
+        constexpr int W = decltype(wc)::value;
+        return k4 ? reinterpret_cast<const void *>(&k_rcol<B, NKS, KM, 1, U, W, 1>)
+                  : reinterpret_cast<const void *>(&k_rcol<B, NKS, KM, 1, U, W, 0>);
+    };
+    if (wst == 1) return pk(std::integral_constant<int, 1>{});
+    if (wst == 2) return pk(std::integral_constant<int, 2>{});
+    if constexpr (B == 3) return pk(std::integral_constant<int, 3>{});
+    return nullptr;
+}
+template <int B, bool U>
+const void *rc_spec_pick(int nks, int kmax, int wst, int k4) {
+    if (nks == 1) return kmax == 3 ? rc_spec_wk<B, 1, 3, U>(wst, k4) : rc_spec_wk<B, 1, 6, U>(wst, k4);
+    return kmax == 3 ? rc_spec_wk<B, 2, 3, U>(wst, k4) : rc_spec_wk<B, 2, 6, U>(wst, k4);
+}
+
 // The column walker for both shrinks in (1, ~2.5] (<= 16 taps) on 3- / 4-band images
 // whose input rows start on a dword; MIPX_EUNSUPPORTED otherwise (the caller runs
 // another kernel).  Output window [ox0, ox0 + ow) x [oy0, oy0 + oh).
@@ -797,56 +818,23 @@ int reduce_col_launch(const u8 *in, u8 *out, int n, int w, int h, int b, double 
     }
 #undef MIPX_RC_KM
 #undef MIPX_RC_K
-    // r06: the 3-chunk, one-K-step builds with the store mode and K-origin width compiled in
-    // (profiles/r06/rcol_spec_ab.jsonl: 480x270 +4.7 %, 500x375 +3.3 %, 1024^2 RGBA / 1.333
-    // +1.1 %, 1080p RGB / 1.6 +0.8 %, the rest +-0.1 %; RGBA with 4-byte K origins -1.4 %, so
-    // that one, and RGBA rows off a dword, keep the argument-driven build); MIPX_RCOL_SPEC=0: those builds everywhere (A/B)
+    // r06: builds with the store mode and K-origin width compiled in, loading the host-built
+    // operands (device_rcol_hops) instead of computing them in the set-up
+    // (profiles/r06/rcol_spec_ab.jsonl, rcol_hops_ab: 480x270 +12 %, 500x375 +8 %;
+    // rcol_hops2_ab / rcol_hops2b_ab, two K steps: 1080p RGB / 2.4 +13 %, 4K / 2.4 +12 %,
+    // 1333x1000 RGB / 2.4 +15 %, RGBA 1024^2 / 2.2 +11 %; rcol_spec3_ab: the rest);
+    // MIPX_RCOL_SPEC=0: the argument-driven builds everywhere (A/B)
     const char *esp = tune_env("MIPX_RCOL_SPEC");
-    // (and, with the host-built operands, two K steps: 1080p RGB / 2.4 +13 %, 4K / 2.4 +12 %,
-    // profiles/r06/rcol_hops2_ab; RGB rows off a dword and RGBA with 8-byte K origins only)
-    const bool spec2 = nks == 2 && (b == 3 ? !unal || !a.k4 : !a.k4 && a.wst != 3);
-    bool spec = !(esp && *esp == '0') && ((nks == 1 && kmax == 3) || spec2) && a.wst >= 1 && a.wst <= 3 &&
-                !(b == 4 && (a.k4 || a.wst == 3)) && a.skipl && a.trl && a.swz && !a.allst;
+    bool spec = !(esp && *esp == '0') && a.wst >= 1 && a.wst <= (b == 3 ? 3 : 2) && a.skipl && a.trl && a.swz &&
+                !a.allst;
     int hstrips = 0;
     const u8 *hops = spec ? device_rcol_hops(hs, b, centre, ox0, ow, w, a.k4, nks, &hstrips) : nullptr;
     spec = spec && hops;  // past the table cap: the builds that compute their operands
     if (spec) {
         a.hops = hops;
         a.hkb = reinterpret_cast<const int *>(hops + static_cast<size_t>(hstrips) * 4 * b * 64 * kRcolHopRec(nks));
-#define MIPX_RC_S(B_, U_, W_, K_) fn = reinterpret_cast<const void *>(&k_rcol<B_, 1, 3, 1, U_, W_, K_>);
-#define MIPX_RC_S2(W_, K_)                                                                 \
-    fn = kmax == 3 ? reinterpret_cast<const void *>(&k_rcol<3, 2, 3, 1, false, W_, K_>) \
-                   : reinterpret_cast<const void *>(&k_rcol<3, 2, 6, 1, false, W_, K_>);
-#define MIPX_RC_SK(B_, U_, W_) \
-    if (a.k4) { MIPX_RC_S(B_, U_, W_, 1) } else { MIPX_RC_S(B_, U_, W_, 0) }
-#define MIPX_RC_SK2(W_) \
-    if (a.k4) { MIPX_RC_S2(W_, 1) } else { MIPX_RC_S2(W_, 0) }
-#define MIPX_RC_SW(B_, U_) \
-    if (a.wst == 1) { MIPX_RC_SK(B_, U_, 1) } else if (a.wst == 2) { MIPX_RC_SK(B_, U_, 2) } else { MIPX_RC_SK(B_, U_, 3) }
-        if (spec2 && unal) {
-#define MIPX_RC_SU2(W_)                                                                   \
-    fn = kmax == 3 ? reinterpret_cast<const void *>(&k_rcol<3, 2, 3, 1, true, W_, 0>) \
-                   : reinterpret_cast<const void *>(&k_rcol<3, 2, 6, 1, true, W_, 0>);
-            if (a.wst == 1) { MIPX_RC_SU2(1) } else if (a.wst == 2) { MIPX_RC_SU2(2) } else { MIPX_RC_SU2(3) }
-#undef MIPX_RC_SU2
-        } else if (spec2 && b == 4) {
-#define MIPX_RC_SA2(W_)                                                                    \
-    fn = kmax == 3 ? reinterpret_cast<const void *>(&k_rcol<4, 2, 3, 1, false, W_, 0>) \
-                   : reinterpret_cast<const void *>(&k_rcol<4, 2, 6, 1, false, W_, 0>);
-            if (a.wst == 1) { MIPX_RC_SA2(1) } else { MIPX_RC_SA2(2) }
-#undef MIPX_RC_SA2
-        } else if (spec2) {
-            if (a.wst == 1) { MIPX_RC_SK2(1) } else if (a.wst == 2) { MIPX_RC_SK2(2) } else { MIPX_RC_SK2(3) }
-        }
-        else if (unal) { MIPX_RC_SW(3, true) }
-        else if (b == 3) { MIPX_RC_SW(3, false) }
-        else if (a.wst == 1) { MIPX_RC_S(4, false, 1, 0) }
-        else { MIPX_RC_S(4, false, 2, 0) }
-#undef MIPX_RC_SW
-#undef MIPX_RC_SK2
-#undef MIPX_RC_S2
-#undef MIPX_RC_SK
-#undef MIPX_RC_S
+        fn = b == 3 ? (unal ? rc_spec_pick<3, true>(nks, kmax, a.wst, a.k4) : rc_spec_pick<3, false>(nks, kmax, a.wst, a.k4))
+                    : rc_spec_pick<4, false>(nks, kmax, a.wst, a.k4);
     }
 
     // segments: a block's set-up (operand loads, the first group's rows) costs about two

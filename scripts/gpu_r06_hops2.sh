@@ -11,7 +11,14 @@ run 600 python3 -u -m pytest tests/test_rcol_gpu.py tests/test_chain_gpu.py test
 tail -1 "$O/pytest.log"
 ab() { run 150 python3 scripts/op_bench.py "$@" --iters 20 >> "$O/ab.jsonl" 2>> "$O/ab.err"; }
 # SHAPES=2: the RGBA and RGB-rows-off-a-dword builds (second pass)
-if [ "${SHAPES:-1}" = 2 ]; then
+# SHAPES=3: every geometry specialised (one K step with 6 chunks, RGBA with 4-byte K origins)
+if [ "${SHAPES:-1}" = 3 ]; then
+  set -- "--w 1920 --h 1080 --b 3 --n 64 --s 1.9" "--w 1920 --h 1080 --b 3 --n 64 --s 1.8" "--w 1333 --h 1000 --b 3 --n 48 --s 1.9" \
+    "--w 1024 --h 1024 --b 4 --n 128 --s 1.7" "--w 1024 --h 1024 --b 4 --n 128 --s 1.8" "--w 1024 --h 1024 --b 4 --n 128 --s 1.9" \
+    "--w 800 --h 600 --b 4 --n 128 --s 1.6666666666666667" "--w 1024 --h 1024 --b 4 --n 512 --s 1.3333333333333333" \
+    "--w 1920 --h 1080 --b 3 --n 64 --s 1.6" "--w 500 --h 375 --b 3 --n 128 --s 1.46484375" \
+    "--w 364 --h 273 --b 3 --n 128 --s 1.421875" "--w 1920 --h 1080 --b 3 --n 64 --s 2.4"
+elif [ "${SHAPES:-1}" = 2 ]; then
   set -- "--w 1024 --h 1024 --b 4 --n 128 --s 2.4" "--w 1024 --h 1024 --b 4 --n 128 --s 2.2" "--w 800 --h 600 --b 4 --n 128 --s 2.25" \
     "--w 1333 --h 1000 --b 3 --n 48 --s 2.4" "--w 1366 --h 768 --b 3 --n 64 --s 2.2" "--w 999 --h 750 --b 3 --n 128 --s 2.25" \
     "--w 1920 --h 1080 --b 3 --n 64 --s 2.4"
