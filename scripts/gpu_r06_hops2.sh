@@ -6,11 +6,12 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R"; export TMPDIR=/tmp
 O="$R/gpurun_out/${OUT:-r06_hops2}"; mkdir -p "$O"
 run() { local lim=$1; shift; timeout -k 10 "$lim" "$@"; local rc=$?; [ $rc -eq 0 ] || { echo "step failed rc=$rc: $*"; exit $rc; }; }
-run 600 python3 -u -m pytest tests/test_rcol_gpu.py tests/test_chain_gpu.py tests/test_parity_gpu.py \
+[ "${TESTS:-1}" = 1 ] && run 600 python3 -u -m pytest tests/test_rcol_gpu.py tests/test_chain_gpu.py tests/test_parity_gpu.py \
   -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1
-tail -1 "$O/pytest.log"
+[ "${TESTS:-1}" = 1 ] && tail -1 "$O/pytest.log"
 ab() { run 150 python3 scripts/op_bench.py "$@" --iters 20 >> "$O/ab.jsonl" 2>> "$O/ab.err"; }
 # SHAPES=2: the RGBA and RGB-rows-off-a-dword builds (second pass)
+# KNOB: the A/B switch (default MIPX_RCOL_SPEC=0,1); TESTS=0 skips the tests
 # SHAPES=3: every geometry specialised (one K step with 6 chunks, RGBA with 4-byte K origins)
 if [ "${SHAPES:-1}" = 3 ]; then
   set -- "--w 1920 --h 1080 --b 3 --n 64 --s 1.9" "--w 1920 --h 1080 --b 3 --n 64 --s 1.8" "--w 1333 --h 1000 --b 3 --n 48 --s 1.9" \
@@ -28,7 +29,7 @@ else
     "--w 480 --h 270 --b 3 --n 256 --s 1.6 --s2 1.5976331360946747" "--w 1333 --h 1000 --b 3 --n 48 --s 1.6666666666666667"
 fi
 for a in "$@"; do
-  ab reduce $a --ab MIPX_RCOL_SPEC=0,1
+  ab reduce $a --ab ${KNOB:-MIPX_RCOL_SPEC=0,1}
 done
 python3 - "$O" <<'PY'
 import json, sys
