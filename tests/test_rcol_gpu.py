@@ -143,6 +143,20 @@ def test_reduce_centre_c2_c1_shapes(gpu, oracle, rng, centre):
             assert_same(got[i], oracle.execute(rp, imgs[i]), f"centre plan {iw}x{ih}x{b} {opts}")
 
 
+def test_rcol_past_operand_table_cap(gpu, oracle, rng, monkeypatch):
+    """Past the host-built operand tables' cap (MIPX_RCOL_HOPCAP_MB=0 here, 256 MiB by
+    default) a new geometry runs the build that computes its operands; geometries whose
+    tables exist keep them.  Every case must give the oracle's bytes."""
+    cases = ((53, 611, 3, 1.55, 1.3), (47, 523, 4, 1.45, 1.7), (61, 739, 3, 2.2, 1.9), (29, 301, 3, 1.7, 1.7))
+    for cap in ("0", ""):
+        monkeypatch.setenv("MIPX_RCOL_HOPCAP_MB", cap)
+        for h, w, b, hs, vs in cases:
+            imgs = np.stack([rand_img(rng, h, w, b), smooth_img(rng, h, w, b)])
+            got = gpu.run_op("reduce", imgs, hshrink=hs, vshrink=vs)
+            for i in range(2):
+                assert_same(got[i], oracle.reduce(imgs[i], hs, vs), f"cap={cap!r} {h}x{w}x{b} {hs}x{vs} img{i}")
+
+
 @pytest.mark.parametrize("n", [128, 40, 3])
 def test_rcol_four_wave_build(gpu, oracle, rng, n):
     """C4's thumbnail reduce (12 MP / 11 = 364x273 -> 256x256): with 40 or 128 images the
